@@ -1,0 +1,101 @@
+"""ctypes wrapper over oracle/build/libttoracle.so (CPU ORACLE: test infrastructure + cpu_baseline).
+
+Never imported by the product package.  Layout of z is the reference's interleaved vector
+[x0,u0,...,x_{N-1},u_{N-1},x_N] (python-files/trajectory_planning.py:38-58).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "build" / "libttoracle.so"
+
+
+class TTOProblem(C.Structure):
+    _fields_ = [("N", C.c_int), ("dt", C.c_double), ("L1", C.c_double), ("L2", C.c_double), ("Mh", C.c_double),
+                ("Q", C.c_double * 36), ("R", C.c_double * 4), ("xlb", C.c_double * 6), ("xub", C.c_double * 6),
+                ("ulb", C.c_double * 2), ("uub", C.c_double * 2), ("tol", C.c_double), ("acc_tol", C.c_double),
+                ("max_iter", C.c_int), ("acc_iter", C.c_int)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", str(_HERE)])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        _lib = C.CDLL(str(LIB_PATH))
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int)
+        _lib.tto_solve_batch.argtypes = [C.POINTER(TTOProblem), C.c_int, dp, dp, dp, dp, dp, dp, dp, ip, ip, dp, C.c_int]
+        _lib.tto_solve_batch.restype = C.c_int
+    return _lib
+
+
+def _fin(a):
+    a = np.asarray(a, dtype=np.float64).copy()
+    a[np.isposinf(a)] = 1e300
+    a[np.isneginf(a)] = -1e300
+    return a
+
+
+def make_problem(N, params, Q, R, xlb, xub, ulb, uub, tol=1e-8, acc_tol=1e-6, max_iter=3000, acc_iter=15):
+    P = TTOProblem()
+    P.N = int(N)
+    P.dt, P.L1, P.L2, P.Mh = params["dt"], params["L1"], params["L2"], params["M"]
+    P.Q[:] = list(np.asarray(Q, float).reshape(36))
+    P.R[:] = list(np.asarray(R, float).reshape(4))
+    P.xlb[:] = list(_fin(xlb)); P.xub[:] = list(_fin(xub))
+    P.ulb[:] = list(_fin(ulb)); P.uub[:] = list(_fin(uub))
+    P.tol, P.acc_tol, P.max_iter, P.acc_iter = tol, acc_tol, max_iter, acc_iter
+    return P
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def solve_batch(P, x0, xref, uref, wq=None, wr=None, z_guess=None, nthreads=0):
+    """x0 (B,6), xref (B,N+1,6), uref (B,N,2) -> (z (B,n), status, iters, kkt)."""
+    N = P.N
+    n = 8 * N + 6
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    B = x0.shape[0]
+    xref = np.ascontiguousarray(xref, dtype=np.float64).reshape(B, N + 1, 6)
+    uref = np.ascontiguousarray(uref, dtype=np.float64).reshape(B, N, 2)
+    wq = None if wq is None else np.ascontiguousarray(wq, dtype=np.float64).reshape(B, 6)
+    wr = None if wr is None else np.ascontiguousarray(wr, dtype=np.float64).reshape(B, 2)
+    zg = None if z_guess is None else np.ascontiguousarray(z_guess, dtype=np.float64).reshape(B, n)
+    z = np.zeros((B, n))
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    kk = np.zeros(B)
+    rc = lib().tto_solve_batch(C.byref(P), B, _ptr(x0), _ptr(xref), _ptr(uref), _ptr(wq), _ptr(wr), _ptr(zg),
+                               _ptr(z), st.ctypes.data_as(C.POINTER(C.c_int)), it.ctypes.data_as(C.POINTER(C.c_int)),
+                               _ptr(kk), int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"tto_solve_batch failed: {rc}")
+    return z, st, it, kk
+
+
+def split(z, N):
+    """(B,n) -> X (B,N+1,6), U (B,N,2)."""
+    z = np.asarray(z)
+    B = z.shape[0]
+    body = z[:, : 8 * N].reshape(B, N, 8)
+    X = np.concatenate([body[:, :, :6], z[:, None, 8 * N:]], axis=1)
+    return X, body[:, :, 6:].copy()
+
+
+os.environ.setdefault("OMP_PROC_BIND", "false")
