@@ -1,0 +1,253 @@
+"""Benchmark: batched truck-trailer NMPC solves on MI355X (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5] [--batch B] [--horizon H]
+
+A "step" = one launch of the HIP solver over one batch of B independent NLP instances (B solves),
+inputs already resident in HBM.  Default workload = BASELINE configs[1] (C2): B = 1024 instances
+per GPU, horizon N = 20, synthetic reference tracking problems (SURVEY.md §8(d) generator, seeded
+per rank -> each rank owns its shard, no data-path collective: weak scaling).
+
+Prints ONE JSON line on rank 0.  `value` = solves/s of the whole job (sum over ranks / max time).
+`roofline` uses the algorithmic FP64 flop formula of SURVEY.md §8(d) over the per-instance Newton
+iteration counts the kernel returns, divided by the kernel time measured with HIP events on the
+stream the kernel is launched on.  `cpu_baseline` times the CPU oracle (oracle/, the same NLP and
+interior-point constants, banded-LU KKT, OpenMP over instances) on a bounded sample on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path[:0] = [str(REPO), str(REPO / "car-trailer-mpc_amd")]
+
+import torch  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6    # MI355X dense FP64 (vector = matrix on CDNA4), MI355X_MICROARCH / spec
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
+
+
+def flops_per_solve(N, iters):
+    """F = lin_evals*F_lin + kkt_solves*(F_ric + F_fwd + F_ipm), nx=6, nu=2,
+    lin_evals = iters + 1 (one linearisation per Newton step + the final convergence test),
+    kkt_solves = iters (one Riccati factorisation + solve per step; inertia retries not counted)."""
+    F_lin = N * (60 + 5 * 20)
+    F_ric = N * 1539
+    F_fwd = N * 152
+    F_ipm = N * 12 * 10
+    return (iters + 1) * F_lin + iters * (F_ric + F_fwd + F_ipm)
+
+
+def io_bytes_per_solve(N):
+    """Algorithmic HBM bytes per solve: x0 + xref + uref in, x_out + u_out + status/iters/kkt out."""
+    return 8 * (6 + 6 * (N + 1) + 2 * N) + 8 * (6 * (N + 1) + 2 * N) + 4 + 4 + 8
+
+
+def workload(cfg, B, N, seed):
+    from ttmpc import scenarios
+    if cfg == "c3":
+        return scenarios.synthetic_batch(B, N, seed=seed, psi_range=0.9)
+    if cfg == "c5":
+        cases = json.loads((REPO / "tests" / "golden" / "test_cases.json").read_text())["cases"]
+        return scenarios.test_case_batch(cases, B, N, seed=seed)
+    return scenarios.synthetic_batch(B, N, seed=seed)
+
+
+def cpu_baseline(cfg, B, N, seed, budget_s):
+    """CPU oracle on a bounded sample of the same workload (rank 0, N=1 only)."""
+    import numpy as np
+
+    from oracle import c_oracle as co
+    from oracle import ttmpc_oracle as to
+    ncores = len(os.sched_getaffinity(0))
+    threads = max(1, min(16, ncores))
+    x0, xr, ur = workload(cfg, B, N, seed)
+    nlp = to.TrackingNLP(N)
+    P = co.make_problem(N, to.DEFAULT_PARAMS, nlp.Q, nlp.R, nlp.xlb, nlp.xub, nlp.ulb, nlp.uub)
+    co.solve_batch(P, x0[: min(B, 64)], xr[: min(B, 64)], ur[: min(B, 64)], nthreads=threads)  # warm
+    done, t0 = 0, time.perf_counter()
+    chunk = min(B, 256 * threads)
+    while True:
+        lo = done % B
+        hi = min(B, lo + chunk)
+        co.solve_batch(P, x0[lo:hi], xr[lo:hi], ur[lo:hi], nthreads=threads)
+        done += hi - lo
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"{done} solves of the same {cfg} workload (N={N}) in {el:.1f}s, OpenMP {threads} threads "
+                      f"on {ncores} visible host cores; oracle/c/tt_oracle.c (IPOPT-restated IPM, banded LU)"}
+
+
+def p50_latency(solver, x0, xr, ur, reps=200):
+    """Host wall clock around one B=1 solve incl. H2D/D2H (mirrors simulation.py:519-522)."""
+    import numpy as np
+    ts = []
+    for r in range(reps + 10):
+        t0 = time.perf_counter()
+        solver.solve(x0[r % 8: r % 8 + 1], xr[r % 8: r % 8 + 1], ur[r % 8: r % 8 + 1])
+        ts.append(time.perf_counter() - t0)
+    ts = np.array(ts[10:]) * 1e3
+    return float(np.percentile(ts, 50)), float(np.percentile(ts, 99))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"])
+    ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default by config)")
+    ap.add_argument("--horizon", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV of this config (optional)")
+    args = ap.parse_args()
+
+    defaults = {"c2": (1024, 20), "c3": (8192, 40), "c5": (8192, 20)}
+    B = args.batch or defaults[args.config][0]
+    N = args.horizon or defaults[args.config][1]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="gloo")  # host-side barrier/max only: no data-path collective
+
+    import numpy as np
+
+    import ttmpc
+    from oracle import ttmpc_oracle as to  # constants only (bounds/weights of simulation.py:391-414)
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    solver = ttmpc.BatchSolver(N, to.DEFAULT_PARAMS, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB,
+                               to.MPC_UUB, device=local)
+    x0, xr, ur = workload(args.config, B, N, seed=1000 * rank + 7)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in (("x0", x0), ("xr", xr), ("ur", ur))}
+    X = torch.empty((B, N + 1, 6), dtype=torch.float64, device=dev)
+    U = torch.empty((B, N, 2), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    kk = torch.empty(B, dtype=torch.float64, device=dev)
+    stream = torch.cuda.Stream(dev)  # explicit non-null stream: the kernel and the timing events share it
+
+    def step():
+        solver.solve_device(B, t["x0"].data_ptr(), t["xr"].data_ptr(), t["ur"].data_ptr(), X.data_ptr(),
+                            U.data_ptr(), st.data_ptr(), it.data_ptr(), kk.data_ptr(), stream=stream.cuda_stream)
+
+    torch.cuda.synchronize(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    status = st.cpu().numpy()
+    iters = it.cpu().numpy()
+    kkt = kk.cpu().numpy()
+    ok = int(np.sum(status <= 1))
+    t_local = torch.tensor([wall, float(ok), float(B)], dtype=torch.float64)
+    if dist:
+        tmax = t_local.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t_local.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        wall_max, ok_total, B_total = float(tmax[0]), int(tsum[1]), int(tsum[2])
+    else:
+        wall_max, ok_total, B_total = wall, ok, B
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    ms_per_step = wall_max / args.steps * 1e3
+    value = B_total * args.steps / wall_max
+    F = float(np.sum(flops_per_solve(N, iters.astype(np.float64))))
+    achieved = F / (kernel_ms * 1e-3) / 1e12
+    io = io_bytes_per_solve(N) * B
+    traffic = None
+    traffic_src = None
+    if args.traffic_csv and Path(args.traffic_csv).exists():
+        traffic, traffic_src = read_traffic(args.traffic_csv), args.traffic_csv
+    out = {
+        "metric": "MPC solves/sec (N=20, nx=6, nu=2; BASELINE label says nx=5, the reference model has 6 states)"
+        if N == 20 else f"MPC solves/sec (N={N}, nx=6, nu=2)",
+        "value": round(value, 1),
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY §8(d) seeded reference-tracking instances, per-rank shard)",
+        "config": {"workload": f"{args.config}: B={B} instances/GPU, N={N}, tracking NMPC (mpc_control.py NLP), "
+                               "IPOPT tol 1e-8", "batch_per_gpu": B, "horizon": N,
+                   "parallelism": f"dp{world} (independent instance shards)"},
+        "solver": {"converged_or_acceptable": ok_total, "instances": B_total,
+                   "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
+                   "kkt_max": float(np.max(kkt)), "kernel_ms_per_launch": round(kernel_ms, 4)},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP64_PEAK_TFLOPS, 6), "traffic": traffic,
+                     "note": "FP64 VALU-bound kernel; on MI355X the dense FP64 peak is 78.6 TF for vector and matrix "
+                             "alike, so the FP64 'mfma' roof is the FP64 vector roof. Algorithmic flops: SURVEY §8(d) "
+                             f"formula x per-instance iterations ({F / B:.0f} flop/solve avg); HBM algorithmic "
+                             f"{io / (kernel_ms * 1e-3) / 1e9:.2f} GB/s = "
+                             f"{io / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS:.2e} of 8 TB/s",
+                     "traffic_source": traffic_src},
+    }
+    if not args.no_latency:
+        p50, p99 = p50_latency(solver, x0, xr, ur)
+        out["p50_latency_ms"] = round(p50, 4)
+        out["p99_latency_ms"] = round(p99, 4)
+    if args.cpu_budget > 0 and world == 1:
+        out["cpu_baseline"] = cpu_baseline(args.config, B, N, 1000 * rank + 7, args.cpu_budget)
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def read_traffic(path):
+    """Average FETCH_SIZE+WRITE_SIZE (KB -> bytes) per dispatch of track_kernel from a rocprofv3
+    --pmc counter_collection CSV; FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md."""
+    import csv
+    fetch, write = [], []
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if "track_kernel" not in row.get("Kernel_Name", ""):
+                continue
+            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", "nan"))
+            if name == "FETCH_SIZE":
+                fetch.append(val)
+            elif name == "WRITE_SIZE":
+                write.append(val)
+    if not fetch and not write:
+        return None
+    f = 2.0 * 1024 * (sum(fetch) / len(fetch) if fetch else 0.0)
+    w = 1024 * (sum(write) / len(write) if write else 0.0)
+    return round(f + w, 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,288 @@
+// C-ABI boundary of libttmpc.so (declared in include/ttmpc.h).
+//
+// Host side of the drop-in: validates shapes before any launch (a mis-sized LDS or grid is a
+// GPU fault), owns per-handle device workspaces for the host-pointer entry point, and forwards
+// device-pointer calls straight to the kernel on the caller's stream.  No CPU fallback exists:
+// every solve runs the gfx950 kernel in tt_track.hip.
+#include <errno.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "tt_kernel.hpp"
+#include "ttmpc.h"
+
+namespace {
+
+struct Handle {
+    tt_config cfg;
+    double Q[36], R[4], xlb[6], xub[6], ulb[2], uub[2];
+    int device = 0;
+    hipStream_t stream = nullptr;
+    size_t cap = 0;  // instances the workspace holds
+    double *d_x0 = nullptr, *d_xref = nullptr, *d_uref = nullptr, *d_w = nullptr, *d_zg = nullptr;
+    double *d_xo = nullptr, *d_uo = nullptr, *d_kkt = nullptr;
+    int *d_st = nullptr, *d_it = nullptr;
+    std::string err;
+};
+
+thread_local std::string g_err;
+
+int fail(Handle* h, int code, const char* fmt, const char* detail = "") {
+    char buf[512];
+    snprintf(buf, sizeof buf, fmt, detail);
+    if (h) h->err = buf;
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(Handle* h, hipError_t e, const char* where) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s: %s", where, hipGetErrorString(e));
+    if (h) h->err = buf;
+    g_err = buf;
+    return -EIO;
+}
+
+void free_ws(Handle* h) {
+    double** dp[] = {&h->d_x0, &h->d_xref, &h->d_uref, &h->d_w, &h->d_zg, &h->d_xo, &h->d_uo, &h->d_kkt};
+    for (double** p : dp) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    if (h->d_st) (void)hipFree(h->d_st);
+    if (h->d_it) (void)hipFree(h->d_it);
+    h->d_st = h->d_it = nullptr;
+    h->cap = 0;
+}
+
+int ensure_ws(Handle* h, int B) {
+    if ((size_t)B <= h->cap) return 0;
+    free_ws(h);
+    const size_t N = h->cfg.N, nz = 8 * N + 6;
+    const size_t cap = (size_t)B;
+    hipError_t e = hipSuccess;
+#define ALLOC(p, bytes) \
+    if (e == hipSuccess) e = hipMalloc((void**)&(p), (bytes))
+    ALLOC(h->d_x0, cap * 6 * 8);
+    ALLOC(h->d_xref, cap * (N + 1) * 6 * 8);
+    ALLOC(h->d_uref, cap * N * 2 * 8);
+    ALLOC(h->d_w, cap * 8 * 8);
+    ALLOC(h->d_zg, cap * nz * 8);
+    ALLOC(h->d_xo, cap * (N + 1) * 6 * 8);
+    ALLOC(h->d_uo, cap * N * 2 * 8);
+    ALLOC(h->d_kkt, cap * 8);
+    ALLOC(h->d_st, cap * 4);
+    ALLOC(h->d_it, cap * 4);
+#undef ALLOC
+    if (e != hipSuccess) {
+        free_ws(h);
+        return fail(h, -ENOMEM, "device workspace allocation failed for B=%s", std::to_string(B).c_str());
+    }
+    h->cap = cap;
+    return 0;
+}
+
+void defaults(tt_config& c) {
+    const bool relaxed = c.variant == TT_VARIANT_NMPC || c.variant == TT_VARIANT_FUZZY;
+    // IPOPT options of the reference classes: mpc_control.py:35-39 (defaults tol 1e-8, acceptable
+    // 1e-6 x 15), mpc_control_nmpc.py:36-45 / mpc_control_fuzzy.py:47-58 (tol 1e-3, acc 1e-2 x 5)
+    if (c.tol <= 0) c.tol = relaxed ? 1e-3 : 1e-8;
+    if (c.acc_tol <= 0) c.acc_tol = relaxed ? 1e-2 : 1e-6;
+    if (c.max_iter <= 0) c.max_iter = relaxed ? 2000 : 5000;
+    if (c.acc_iter <= 0) c.acc_iter = relaxed ? 5 : 15;
+}
+
+ttmpc::TrackArgs make_args(const Handle* h, int B) {
+    ttmpc::TrackArgs a;
+    memset(&a, 0, sizeof a);
+    a.N = h->cfg.N;
+    a.B = B;
+    a.max_iter = h->cfg.max_iter;
+    a.acc_iter = h->cfg.acc_iter;
+    a.dt = h->cfg.dt;
+    a.L1 = h->cfg.L1;
+    a.L2 = h->cfg.L2;
+    a.Mh = h->cfg.Mh;
+    a.tol = h->cfg.tol;
+    a.acc_tol = h->cfg.acc_tol;
+    memcpy(a.Q, h->Q, sizeof a.Q);
+    memcpy(a.R, h->R, sizeof a.R);
+    memcpy(a.xlb, h->xlb, sizeof a.xlb);
+    memcpy(a.xub, h->xub, sizeof a.xub);
+    memcpy(a.ulb, h->ulb, sizeof a.ulb);
+    memcpy(a.uub, h->uub, sizeof a.uub);
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tt_create(const tt_config* cfg, const double* Q, const double* R, const double* xlb, const double* xub,
+              const double* ulb, const double* uub, const double* obstacles, int device, void** handle) {
+    (void)obstacles;
+    if (!handle) return fail(nullptr, -EINVAL, "handle pointer is NULL%s");
+    *handle = nullptr;
+    if (!cfg || !Q || !R || !xlb || !xub || !ulb || !uub) return fail(nullptr, -EINVAL, "NULL argument%s");
+    if (cfg->nx != 6 || cfg->nu != 2)
+        return fail(nullptr, -EINVAL, "truck-trailer model has nx=6, nu=2 (truck_trailer_model.py:4-5)%s");
+    if (cfg->variant == TT_VARIANT_TRACK_OBCA || cfg->variant == TT_VARIANT_OBCA_PLAN)
+        return fail(nullptr, -ENOSYS, "OBCA variants are not in this build%s");
+    if (cfg->variant != TT_VARIANT_TRACK && cfg->variant != TT_VARIANT_NMPC && cfg->variant != TT_VARIANT_FUZZY)
+        return fail(nullptr, -EINVAL, "unknown variant%s");
+    if (cfg->N < 1 || cfg->N > ttmpc::max_horizon())
+        return fail(nullptr, -EINVAL, "horizon must be in [1, %s] (LDS-resident instance)",
+                    std::to_string(ttmpc::max_horizon()).c_str());
+    if (!(cfg->dt > 0) || !(cfg->L1 > 0) || !(cfg->L2 > 0) || !isfinite(cfg->Mh))
+        return fail(nullptr, -EINVAL, "params dt, L1, L2 must be > 0 and M finite%s");
+    for (int i = 0; i < 6; ++i)
+        if (!(xlb[i] <= xub[i])) return fail(nullptr, -EINVAL, "state bound lb > ub%s");
+    for (int i = 0; i < 2; ++i)
+        if (!(ulb[i] <= uub[i])) return fail(nullptr, -EINVAL, "input bound lb > ub%s");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(nullptr, -ENODEV, "no HIP device: ttmpc is GPU-only (gfx950)%s");
+    if (device < 0 || device >= ndev) return fail(nullptr, -ENODEV, "device ordinal out of range%s");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, -ENODEV, "device is not gfx950 (MI355X): %s", prop.gcnArchName);
+    Handle* h = new Handle();
+    h->cfg = *cfg;
+    defaults(h->cfg);
+    memcpy(h->Q, Q, sizeof h->Q);
+    memcpy(h->R, R, sizeof h->R);
+    memcpy(h->xlb, xlb, sizeof h->xlb);
+    memcpy(h->xub, xub, sizeof h->xub);
+    memcpy(h->ulb, ulb, sizeof h->ulb);
+    memcpy(h->uub, uub, sizeof h->uub);
+    h->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        int rc = hip_fail(nullptr, e, "tt_create");
+        delete h;
+        return rc;
+    }
+    *handle = h;
+    return 0;
+}
+
+int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xref, const double* d_uref,
+                          const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out,
+                          int* d_status, int* d_iters, double* d_kkt_res, void* stream) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
+    if (B < 0) return fail(h, -EINVAL, "B must be >= 0%s");
+    if (B == 0) return 0;
+    if (B > (1 << 30)) return fail(h, -EINVAL, "B too large%s");
+    if (!d_x0 || !d_xref || !d_uref || !d_x_out || !d_u_out || !d_status)
+        return fail(h, -EINVAL, "NULL device buffer%s");
+    if (h->cfg.variant == TT_VARIANT_FUZZY && !d_wq_wr)
+        return fail(h, -EINVAL, "fuzzy variant needs per-instance weights (mpc_control_fuzzy.py:54-58)%s");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    ttmpc::TrackArgs a = make_args(h, B);
+    a.x0 = d_x0;
+    a.xref = d_xref;
+    a.uref = d_uref;
+    a.wqwr = d_wq_wr;
+    a.zg = d_z_guess;
+    a.xout = d_x_out;
+    a.uout = d_u_out;
+    a.kkt = d_kkt_res;
+    a.status = d_status;
+    a.iters = d_iters;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+    e = ttmpc::launch_track(a, s);
+    if (e != hipSuccess) return hip_fail(h, e, "track kernel launch");
+    return 0;
+}
+
+int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, const double* uref,
+                   const double* wq_wr, const double* z_guess, double* x_out, double* u_out, int* status,
+                   int* iters, double* kkt_res) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
+    if (B < 0) return fail(h, -EINVAL, "B must be >= 0%s");
+    if (B == 0) return 0;
+    if (!x0 || !xref || !uref || !x_out || !u_out || !status) return fail(h, -EINVAL, "NULL host buffer%s");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    int rc = ensure_ws(h, B);
+    if (rc) return rc;
+    const size_t N = h->cfg.N, nz = 8 * N + 6, b = (size_t)B;
+    hipStream_t s = h->stream;
+#define H2D(d, hp, bytes) \
+    if (e == hipSuccess) e = hipMemcpyAsync((d), (hp), (bytes), hipMemcpyHostToDevice, s)
+#define D2H(hp, d, bytes) \
+    if (e == hipSuccess) e = hipMemcpyAsync((hp), (d), (bytes), hipMemcpyDeviceToHost, s)
+    H2D(h->d_x0, x0, b * 6 * 8);
+    H2D(h->d_xref, xref, b * (N + 1) * 6 * 8);
+    H2D(h->d_uref, uref, b * N * 2 * 8);
+    if (wq_wr) H2D(h->d_w, wq_wr, b * 8 * 8);
+    if (z_guess) H2D(h->d_zg, z_guess, b * nz * 8);
+    if (e != hipSuccess) return hip_fail(h, e, "H2D copy");
+    rc = tt_solve_batch_device(h, B, h->d_x0, h->d_xref, h->d_uref, wq_wr ? h->d_w : nullptr,
+                               z_guess ? h->d_zg : nullptr, h->d_xo, h->d_uo, h->d_st, h->d_it, h->d_kkt, s);
+    if (rc) return rc;
+    D2H(x_out, h->d_xo, b * (N + 1) * 6 * 8);
+    D2H(u_out, h->d_uo, b * N * 2 * 8);
+    D2H(status, h->d_st, b * 4);
+    if (iters) D2H(iters, h->d_it, b * 4);
+    if (kkt_res) D2H(kkt_res, h->d_kkt, b * 8);
+#undef H2D
+#undef D2H
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(h, e, "solve");
+    return 0;
+}
+
+#ifdef TT_STAMPS
+// Diagnostic-build-only entry point: per-instance phase cycle sums into d_stamps[B][kNumPhases].
+int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_xref, const double* d_uref,
+                      double* d_x_out, double* d_u_out, int* d_status, int* d_iters, unsigned long long* d_stamps,
+                      void* stream) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h || B <= 0 || !d_stamps) return -EINVAL;
+    ttmpc::TrackArgs a = make_args(h, B);
+    a.x0 = d_x0;
+    a.xref = d_xref;
+    a.uref = d_uref;
+    a.xout = d_x_out;
+    a.uout = d_u_out;
+    a.status = d_status;
+    a.iters = d_iters;
+    a.stamps = d_stamps;
+    hipError_t e = ttmpc::launch_track(a, stream ? static_cast<hipStream_t>(stream) : h->stream);
+    return e == hipSuccess ? 0 : hip_fail(h, e, "stamped launch");
+}
+#endif
+
+int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess, double* x_out,
+                  double* u_out, int* status, int* iters) {
+    (void)B; (void)x0; (void)xgoal; (void)z_guess; (void)x_out; (void)u_out; (void)status; (void)iters;
+    return fail(static_cast<Handle*>(handle), -ENOSYS, "tt_plan_batch (OBCA) is not in this build%s");
+}
+
+void tt_destroy(void* handle) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    free_ws(h);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char* tt_last_error(void* handle) {
+    Handle* h = static_cast<Handle*>(handle);
+    return h ? h->err.c_str() : g_err.c_str();
+}
+
+int tt_lds_bytes(int N) { return ttmpc::lds_bytes(N); }
+int tt_max_horizon(void) { return ttmpc::max_horizon(); }
+const char* tt_version(void) { return "ttmpc 0.1 (gfx950, wave-per-instance Riccati IPM)"; }
+
+}  // extern "C"

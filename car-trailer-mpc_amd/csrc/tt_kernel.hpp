@@ -1,0 +1,40 @@
+// Internal interface between the C-ABI layer (tt_api.hip) and the gfx950 kernels (tt_track.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ttmpc {
+
+// Everything one launch needs; passed by value as the kernel argument (< 1 KB).
+struct TrackArgs {
+    int N, B, max_iter, acc_iter;
+    double dt, L1, L2, Mh, tol, acc_tol;
+    double Q[36], R[4];                   // row-major, symmetrised in-kernel
+    double xlb[6], xub[6], ulb[2], uub[2];  // raw bounds; |b| >= 1e19 or inf = free
+    const double* x0;                     // [B][6]
+    const double* xref;                   // [B][N+1][6]
+    const double* uref;                   // [B][N][2]
+    const double* wqwr;                   // [B][8] or nullptr
+    const double* zg;                     // [B][8N+6] or nullptr
+    double* xout;                         // [B][N+1][6]
+    double* uout;                         // [B][N][2]
+    double* kkt;                          // [B] or nullptr
+    int* status;                          // [B]
+    int* iters;                           // [B] or nullptr
+    unsigned long long* stamps;           // [B][kNumPhases] cycle sums (TT_STAMPS diagnostic build only)
+};
+
+// phases timed by the TT_STAMPS diagnostic build
+enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC, PH_UPDATE, PH_TOTAL, kNumPhases };
+
+// LDS rows per stage and the fixed scratch tail (doubles); see tt_track.hip for the map.
+constexpr int kRowsPerStage = 149;  // 148 used + 1 pad (odd stride)
+constexpr int kScratch = 188;
+constexpr int kMaxLdsBytes = 160 * 1024;
+
+inline int lds_doubles(int N) { return kRowsPerStage * (N + 1) + kScratch; }
+inline int lds_bytes(int N) { return 8 * lds_doubles(N); }
+inline int max_horizon() { return (kMaxLdsBytes / 8 - kScratch) / kRowsPerStage - 1; }
+
+hipError_t launch_track(const TrackArgs& a, hipStream_t stream);
+
+}  // namespace ttmpc

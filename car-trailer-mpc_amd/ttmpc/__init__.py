@@ -1,0 +1,14 @@
+"""ttmpc -- MI355X-native batched truck-trailer NMPC (drop-in for the reference's mpc_control*.py).
+
+Reference: Avan1ko/car-trailer-mpc python-files/{mpc_control, mpc_control_nmpc, mpc_control_fuzzy,
+trajectory_planning, truck_trailer_model}.py.  All solves run in libttmpc.so on a gfx950 GPU.
+"""
+from ._lib import (STATUS_NAMES, TT_ACCEPTABLE, TT_CONVERGED, TT_INFEASIBLE, TT_MAX_ITER, TT_NONFINITE,  # noqa: F401
+                   TT_VARIANT_FUZZY, TT_VARIANT_NMPC, TT_VARIANT_TRACK, BatchSolver, TTError, lib)
+from .mpc_control import MPCTrackingControl  # noqa: F401
+from .mpc_control_fuzzy import MPCTrackingControlFuzzy, fuzzy_weights  # noqa: F401
+from .mpc_control_nmpc import TruckTrailerNMPC  # noqa: F401
+from .truck_trailer_model import TruckTrailerModel  # noqa: F401
+
+__all__ = ["MPCTrackingControl", "TruckTrailerNMPC", "MPCTrackingControlFuzzy", "TruckTrailerModel", "BatchSolver",
+           "fuzzy_weights", "TTError", "lib"]

@@ -1,0 +1,183 @@
+"""ctypes binding of libttmpc.so (the C ABI in include/ttmpc.h).
+
+The product path is GPU-only: if the library is missing or no gfx950 device is usable, every
+entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libttmpc.so"
+
+TT_CONVERGED, TT_ACCEPTABLE, TT_MAX_ITER, TT_INFEASIBLE, TT_NONFINITE = range(5)
+TT_VARIANT_TRACK, TT_VARIANT_TRACK_OBCA, TT_VARIANT_NMPC, TT_VARIANT_FUZZY, TT_VARIANT_OBCA_PLAN = range(5)
+STATUS_NAMES = {0: "converged", 1: "acceptable", 2: "max_iter", 3: "infeasible", 4: "non-finite"}
+
+
+class TTConfig(C.Structure):
+    _fields_ = [("nx", C.c_int), ("nu", C.c_int), ("N", C.c_int), ("M", C.c_int),
+                ("dt", C.c_double), ("L1", C.c_double), ("L2", C.c_double), ("Mh", C.c_double),
+                ("W1", C.c_double), ("W2", C.c_double), ("variant", C.c_int),
+                ("tol", C.c_double), ("acc_tol", C.c_double), ("max_iter", C.c_int), ("acc_iter", C.c_int),
+                ("warm_shift_compat", C.c_int)]
+
+
+class TTError(RuntimeError):
+    pass
+
+
+_lib = None
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+
+def _share_torch_hip_runtime():
+    """If PyTorch-ROCm is installed, pre-load ITS libamdhip64.so (SONAME libamdhip64.so.7) so that
+    libttmpc.so binds to the same HIP runtime torch uses.  Two HIP runtimes in one process do not
+    coexist (torch then reports no GPU), and torch tensors / streams must be valid for our kernel.
+    Set TTMPC_HIP_RUNTIME=system to use /opt/rocm's runtime instead."""
+    if os.environ.get("TTMPC_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    hip = Path(list(spec.submodule_search_locations)[0]) / "lib" / "libamdhip64.so"
+    if hip.exists():
+        C.CDLL(str(hip), mode=C.RTLD_GLOBAL)
+
+
+def lib():
+    """Load libttmpc.so (raises if it was not built: run ``make -C car-trailer-mpc_amd``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    _share_torch_hip_runtime()
+    if not LIB_PATH.exists():
+        raise TTError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                      " (ttmpc is GPU-only; there is no CPU fallback)")
+    L = C.CDLL(str(LIB_PATH))
+    L.tt_create.argtypes = [C.POINTER(TTConfig), _dp, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int, C.POINTER(C.c_void_p)]
+    L.tt_create.restype = C.c_int
+    L.tt_solve_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp]
+    L.tt_solve_batch.restype = C.c_int
+    L.tt_solve_batch_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 10 + [C.c_void_p]
+    L.tt_solve_batch_device.restype = C.c_int
+    L.tt_plan_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _ip, _ip]
+    L.tt_plan_batch.restype = C.c_int
+    L.tt_destroy.argtypes = [C.c_void_p]
+    L.tt_destroy.restype = None
+    L.tt_last_error.argtypes = [C.c_void_p]
+    L.tt_last_error.restype = C.c_char_p
+    L.tt_lds_bytes.argtypes = [C.c_int]
+    L.tt_lds_bytes.restype = C.c_int
+    L.tt_max_horizon.argtypes = []
+    L.tt_max_horizon.restype = C.c_int
+    L.tt_version.argtypes = []
+    L.tt_version.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_plan_batch", "tt_destroy",
+                    "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version")
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+def _bounds(v, n):
+    v = _f64(v).reshape(-1)
+    if v.size != n:
+        raise ValueError(f"bound vector must have {n} entries, got {v.size}")
+    return v
+
+
+def default_device() -> int:
+    for key in ("TTMPC_DEVICE", "LOCAL_RANK"):
+        if key in os.environ:
+            return int(os.environ[key])
+    return 0
+
+
+class BatchSolver:
+    """One library handle = one compiled NLP (the reference's CasADi ``nlpsol`` object) on one GPU."""
+
+    def __init__(self, N, params, Q, R, xlb, xub, ulb, uub, variant=TT_VARIANT_TRACK, tol=0.0, acc_tol=0.0,
+                 max_iter=0, acc_iter=0, device=None):
+        cfg = TTConfig()
+        cfg.nx, cfg.nu, cfg.N, cfg.M = 6, 2, int(N), 0
+        cfg.dt, cfg.L1, cfg.L2, cfg.Mh = float(params["dt"]), float(params["L1"]), float(params["L2"]), float(params["M"])
+        cfg.W1, cfg.W2 = float(params.get("W1", 0.0)), float(params.get("W2", 0.0))
+        cfg.variant = int(variant)
+        cfg.tol, cfg.acc_tol, cfg.max_iter, cfg.acc_iter = float(tol), float(acc_tol), int(max_iter), int(acc_iter)
+        cfg.warm_shift_compat = 0
+        self.N = int(N)
+        self.variant = int(variant)
+        self.Q = _f64(Q, (6, 6))
+        self.R = _f64(R, (2, 2))
+        self.bounds = tuple(_bounds(b, n) for b, n in ((xlb, 6), (xub, 6), (ulb, 2), (uub, 2)))
+        self.device = default_device() if device is None else int(device)
+        h = C.c_void_p()
+        L = lib()
+        rc = L.tt_create(C.byref(cfg), _ptr(self.Q), _ptr(self.R), *[_ptr(b) for b in self.bounds], None,
+                         self.device, C.byref(h))
+        if rc != 0:
+            raise TTError(f"tt_create failed ({rc}): {L.tt_last_error(None).decode()}")
+        self._h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.tt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def _err(self, rc, what):
+        raise TTError(f"{what} failed ({rc}): {self._L.tt_last_error(self._h).decode()}")
+
+    def solve(self, x0, xref, uref, wq_wr=None, z_guess=None):
+        """Host arrays: x0 (B,6), xref (B,N+1,6), uref (B,N,2), wq_wr (B,8)|None, z_guess (B,8N+6)|None.
+        Returns (X (B,N+1,6), U (B,N,2), status (B,), iters (B,), kkt (B,))."""
+        N = self.N
+        x0 = _f64(x0)
+        B = x0.shape[0] if x0.ndim == 2 else 1
+        x0 = x0.reshape(B, 6)
+        xref = _f64(xref, (B, N + 1, 6))
+        uref = _f64(uref, (B, N, 2))
+        w = None if wq_wr is None else _f64(wq_wr, (B, 8))
+        zg = None if z_guess is None else _f64(z_guess, (B, 8 * N + 6))
+        X = np.empty((B, N + 1, 6))
+        U = np.empty((B, N, 2))
+        st = np.empty(B, dtype=np.int32)
+        it = np.empty(B, dtype=np.int32)
+        kk = np.empty(B)
+        rc = self._L.tt_solve_batch(self._h, B, _ptr(x0), _ptr(xref), _ptr(uref), _ptr(w), _ptr(zg), _ptr(X), _ptr(U),
+                                    st.ctypes.data_as(_ip), it.ctypes.data_as(_ip), _ptr(kk))
+        if rc != 0:
+            self._err(rc, "tt_solve_batch")
+        return X, U, st, it, kk
+
+    def solve_device(self, B, x0, xref, uref, x_out, u_out, status, iters=0, kkt=0, wq_wr=0, z_guess=0, stream=0):
+        """Device pointers (ints, e.g. torch ``tensor.data_ptr()``), enqueued on ``stream`` (int handle)."""
+        rc = self._L.tt_solve_batch_device(self._h, int(B), x0, xref, uref, wq_wr or None, z_guess or None, x_out,
+                                           u_out, status, iters or None, kkt or None, stream or None)
+        if rc != 0:
+            self._err(rc, "tt_solve_batch_device")

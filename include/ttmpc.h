@@ -1,0 +1,98 @@
+/* ttmpc -- MI355X-native batched truck-trailer NMPC solver, C ABI (drop-in boundary).
+ *
+ * The reference (Avan1ko/car-trailer-mpc) solves one NLP per controller call through CasADi:
+ *     sol = self._solver(x0=vars_guess, lbx, ubx, lbg, ubg, p)          python-files/mpc_control.py:80-89
+ *     self._solver.stats()['success']                                     python-files/mpc_control.py:106
+ * and exposes it to its drivers as
+ *     MPCTrackingControl.solve(initial_state, reference_states, reference_inputs)
+ *                                                                          python-files/mpc_control.py:67-110
+ *     TruckTrailerNMPC.solve(...)                                          python-files/mpc_control_nmpc.py:90-113
+ *     MPCTrackingControlFuzzy.solve(...)                                   python-files/mpc_control_fuzzy.py:121-167
+ * This library replaces the CasADi/IPOPT call with a batched solve of B independent instances on
+ * one GPU.  The Python mirror (car-trailer-mpc_amd/ttmpc) binds it with ctypes; the binding a
+ * maintainer adds to the reference is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - plain C types only; every array is C-contiguous float64, instance-major:
+ *      x0    [B][nx]            initial_state                      (mpc_control.py:67)
+ *      xref  [B][N+1][nx]       reference_states.T                 (p layout, mpc_control.py:45-52, 86)
+ *      uref  [B][N][nu]         reference_inputs.T                 (p layout, mpc_control.py:86-87)
+ *      wq_wr [B][nx+nu]         fuzzy weights w_q, w_r             (mpc_control_fuzzy.py:54-58) or NULL
+ *      z_guess [B][n], n=(nx+nu)N+nx, the reference's interleaved decision vector
+ *                               [x0,u0,...,x_{N-1},u_{N-1},x_N]    (trajectory_planning.py:38-58) or NULL
+ *                               (NULL = reference-copy guess, mpc_control.py:58-65)
+ *      x_out [B][N+1][nx], u_out [B][N][nu]  = states.T / inputs.T of _split_decision_variables
+ *                                                                  (trajectory_planning.py:62-84)
+ *  - nx = 6 (x, y, theta, psi, phi, v), nu = 2 (a, omega)          (truck_trailer_model.py:4-5)
+ *  - bounds: +-HUGE_VAL (or |b| >= 1e19) = free (ca.inf in simulation.py:411-414)
+ *  - return value: 0 ok, negative errno-style code on API errors (-EINVAL bad dims/pointers,
+ *    -ENOMEM, -EIO HIP error, -ENOSYS not built); text from tt_last_error(handle).
+ *  - per-instance status: TT_CONVERGED (IPOPT tol), TT_ACCEPTABLE (acceptable_tol x acc_iter),
+ *    TT_MAX_ITER, TT_INFEASIBLE (x_init outside the state box -> x_0 = x_init unsatisfiable),
+ *    TT_NONFINITE.  CasADi's stats()['success'] == (status <= TT_ACCEPTABLE).
+ *  - a handle is not thread-safe (like the reference objects, which mutate _last_solution); use
+ *    one handle per host thread.  Host-pointer calls are synchronous; device-pointer calls are
+ *    asynchronous on the given HIP stream.
+ *  - GPU only: there is no CPU fallback; tt_create fails (-ENODEV) without a usable gfx950 device.
+ */
+#ifndef TTMPC_H
+#define TTMPC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { TT_CONVERGED = 0, TT_ACCEPTABLE = 1, TT_MAX_ITER = 2, TT_INFEASIBLE = 3, TT_NONFINITE = 4 };
+
+enum {
+    TT_VARIANT_TRACK = 0,      /* MPCTrackingControl       mpc_control.py       (max_iter 5000, tol 1e-8)  */
+    TT_VARIANT_TRACK_OBCA = 1, /* MPCTrackingControlObs    mpc_control_obs.py   (not in this build)        */
+    TT_VARIANT_NMPC = 2,       /* TruckTrailerNMPC         mpc_control_nmpc.py  (tol 1e-3, acc 1e-2 x5)    */
+    TT_VARIANT_FUZZY = 3,      /* MPCTrackingControlFuzzy  mpc_control_fuzzy.py (tol 1e-3, per-instance w) */
+    TT_VARIANT_OBCA_PLAN = 4   /* TrajectoryOptimization   trajectory_optimization.py (not in this build) */
+};
+
+typedef struct {
+    int nx, nu, N, M;                 /* nx=6, nu=2, horizon N (params['horizon']), obstacles M       */
+    double dt, L1, L2, Mh, W1, W2;    /* params dict keys dt, L1, L2, M, W1, W2 (simulation.py:391)  */
+    int variant;                      /* TT_VARIANT_*                                                 */
+    double tol, acc_tol;              /* IPOPT tol / acceptable_tol (<=0 -> variant default)          */
+    int max_iter, acc_iter;           /* IPOPT max_iter / acceptable_iter (<=0 -> variant default)    */
+    int warm_shift_compat;            /* reserved: warm-shift guesses are built host-side (ttmpc.nlp) */
+} tt_config;
+
+/* Replaces the controller constructors (mpc_control.py:6-15 -> _build_solver 27-56; the CasADi
+ * graph + IPOPT object).  Q: nx*nx row-major, R: nu*nu row-major (symmetrised), bounds nx / nu.
+ * obstacles: M*4 (cx, cy, w, h) or NULL.  device: HIP device ordinal (>= 0). */
+int tt_create(const tt_config* cfg, const double* Q, const double* R, const double* xlb, const double* xub,
+              const double* ulb, const double* uub, const double* obstacles, int device, void** handle);
+
+/* Replaces the per-call IPOPT solve + split (mpc_control.py:67-110) for B instances at once.
+ * Host pointers; synchronous.  kkt_res (may be NULL): IPOPT's scaled optimality error at exit. */
+int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, const double* uref,
+                   const double* wq_wr, const double* z_guess, double* x_out, double* u_out, int* status,
+                   int* iters, double* kkt_res);
+
+/* Same with DEVICE pointers (already resident in HBM), enqueued on `stream` (hipStream_t, NULL =
+ * the handle's stream); asynchronous.  Used by the bench and by device-resident callers. */
+int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xref, const double* d_uref,
+                          const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out,
+                          int* d_status, int* d_iters, double* d_kkt_res, void* stream);
+
+/* Replaces TrajectoryOptimization.plan (trajectory_optimization.py:311-331).  Not in this build:
+ * returns -ENOSYS (OBCA is a later milestone). */
+int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess,
+                  double* x_out, double* u_out, int* status, int* iters);
+
+void tt_destroy(void* handle);
+const char* tt_last_error(void* handle);
+
+/* Introspection: LDS bytes one instance needs at horizon N; max horizon supported; version. */
+int tt_lds_bytes(int N);
+int tt_max_horizon(void);
+const char* tt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTMPC_H */

@@ -18,8 +18,10 @@
  */
 #include "tt_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -414,6 +416,9 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
         double sd = fmax(smax, (sy + sz) / (double)(m + nb)) / smax;
         double sc = nb ? fmax(smax, sz / (double)nb) / smax : 1.0;
         E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
+        if (getenv("TTO_DEBUG"))
+            fprintf(stderr, "it %3d E0 %.3e dinf %.3e pinf %.3e c0 %.3e mu %.2e sd %.2e nu %.2e\n", iter, E0, dinf, pinf, c0,
+                    mu, sd, nu);
         if (E0 <= tol) { status = 0; break; }
         if (E0 <= acc_tol) {
             if (++acc_count >= P->acc_iter) { status = 1; break; }
@@ -511,7 +516,7 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
         for (int ls = 0; ls < 40 && !accepted; ++ls) {
             for (int v = 0; v < n; ++v) w->zt[v] = w->z[v] + alpha * w->dz[v];
             double phit = merit_at(P, w, w->zt, xinit, xref, uref, mu, nu, NULL);
-            if (phit <= phi0 + eta * alpha * D) { accepted = 1; break; }
+            if (phit - (phi0 + eta * alpha * D) <= 10.0 * DBL_EPSILON * fabs(phi0)) { accepted = 1; break; } /* IPOPT Compare_le */
             if (ls == 0 && isfinite(phit)) {
                 /* second-order correction: c_soc = alpha c(z) + c(z + alpha dz) */
                 for (int k = 0; k <= N; ++k) {
@@ -534,7 +539,7 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
                 }
                 for (int v = 0; v < n; ++v) w->zt[v] = w->z[v] + as * w->dzs[v];
                 double phis = merit_at(P, w, w->zt, xinit, xref, uref, mu, nu, NULL);
-                if (phis <= phi0 + eta * alpha * D) {
+                if (phis - (phi0 + eta * alpha * D) <= 10.0 * DBL_EPSILON * fabs(phi0)) {
                     accepted = 2;
                     alpha = as;
                     for (int j = 0; j < m; ++j) w->yp[j] = w->rhs2[ky(j / 6) + j % 6];
@@ -554,6 +559,7 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
             alpha *= 0.5;
         }
         if (!accepted) alpha *= 2.0; /* last tried */
+        if (getenv("TTO_DEBUG")) fprintf(stderr, "   ap %.3e az %.3e alpha %.3e acc %d D %.3e\n", ap, az, alpha, accepted, D);
         /* ---- update ---- */
         for (int v = 0; v < n; ++v) w->z[v] += alpha * w->dz[v];
         for (int j = 0; j < m; ++j) w->y[j] += alpha * (w->yp[j] - w->y[j]);
