@@ -26,9 +26,10 @@ struct TrackArgs {
 // phases timed by the TT_STAMPS diagnostic build
 enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC, PH_UPDATE, PH_TOTAL, kNumPhases };
 
-// LDS rows per stage and the fixed scratch tail (doubles); see tt_track.hip for the map.
-constexpr int kRowsPerStage = 149;  // 148 used + 1 pad (odd stride)
-constexpr int kScratch = 188;
+// LDS: fixed head + rows per stage (doubles); see tt_track.hip for the map.
+constexpr int kRowsPerStage = 157;  // 156 used + 1 zero pad (odd stride: conflict-free b64)
+constexpr int kHead = 64;
+constexpr int kScratch = kHead;
 constexpr int kMaxLdsBytes = 160 * 1024;
 
 inline int lds_doubles(int N) { return kRowsPerStage * (N + 1) + kScratch; }

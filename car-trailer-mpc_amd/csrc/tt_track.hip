@@ -12,25 +12,28 @@
 // 'ipopt'), restated with the same constants (tol/acc, mu_init 0.1, kappa_eps 10, kappa_mu 0.2,
 // theta_mu 1.5, tau = max(.99, 1-mu), bound_relax 1e-8, bound_push/frac 1e-2, kappa_sigma 1e10,
 // exact Lagrangian Hessian) and an l1-merit line search with one second-order correction.  The
-// Newton system is never assembled: it is the KKT system of an equality-constrained LQ problem and
-// is solved by a stage-wise Riccati recursion (inertia test = 2x2 Cholesky of each reduced input
-// Hessian), O(N) per iteration instead of IPOPT's sparse LDL^T.
+// Newton system is never assembled: it is the KKT system of an equality-constrained LQ problem,
+// solved by a stage-wise Riccati recursion on the FP64 matrix cores (inertia test = 2x2 Cholesky
+// of each reduced input Hessian), O(N) per iteration instead of IPOPT's sparse LDL^T.
 //
 // Lane mapping (wave-uniform control flow everywhere):
-//   * stage-parallel phases (model + Jacobian + curvature, residuals, barrier terms, merit
-//     evaluations, multiplier updates): lane k owns stage k (loop k += 64 for N >= 64);
-//   * Riccati backward sweep (serial in k): lanes 0..35 build PA = P A (one entry each), lanes
-//     36..41 w = P b + p; then lanes 0..20 the upper triangle of P_k, 21..26 p_k, 27..38 the gain
-//     K_k, 39 the feed-forward / inverse Hessian -- two barriers per stage, P ping-ponged in LDS;
-//   * forward sweep: lane 0 (~40 dependent FMAs per stage, operands read from LDS).
+//   * stage-parallel phases (model + Jacobian + curvature + barrier terms + residuals, step bounds,
+//     merit trials, multiplier updates): lane k owns stage k (loop k += 64 for N >= 64);
+//   * Riccati backward sweep and forward sweep (serial in k): one 16x16 f64 MFMA tile per stage,
+//     the 7x7 affine-augmented blocks spread over the 64 lanes (see phase_riccati).
 //
-// LDS map (doubles; row r of stage k at sm[k*149 + r]; the odd stride keeps lane-per-stage
-// ds_read_b64 accesses bank-conflict-free and turns every row offset into an immediate):
+// LDS map (doubles).  Head (fixed offsets, immediate addressing): Qw(36) Rw(4) x_init(6) lb(8)
+// ub(8) pad(2).  Stage k row r at sm[kHead + k*157 + r]; the odd stride keeps lane-per-stage
+// ds_read_b64 bank-conflict-free:
 //   0-5 X | 6-7 U | 8-13 Y (eq. multipliers, IPOPT sign) | 14-21 zL | 22-29 zU | 30-35 Xref
-//   36-37 Uref | 38-43 dX | 44-45 dU | 46-51 Y+ | 52-60 dt*J (9 nnz) | 61-67 curvature (7 nnz)
-//   68-75 Sigma | 76-83 barrier gradient | 84-89 c | 90-95 c(trial)/c_soc | 96-107 K | 108-109 k_ff
-//   110-112 inv(H_uu) | 113-133 P_k (upper) | 134-139 p_k | 140-145 dX_soc | 146-147 dU_soc | 148 pad
-//   tail: Qw(36) Rw(4) P ping/pong (2x36) p ping/pong (2x6) PA(36) w(6) x_init(6) lb(8) ub(8)
+//   36-37 Uref | 38-45 dX,dU | 46-51 Y+ | 52-60 dt*J (9 nnz) | 61-67 curvature (7 nnz)
+//   68-75 Sigma = zL/sL + zU/sU | 76-83 grad F | 84-89 c | 90-95 c(trial)/c_soc | 96-107 K
+//   108-109 k_ff | 110-112 inv(H_uu) | 113-133 P_k (upper) | 134-139 p_k | 140-147 dX,dU (soc)
+//   148-155 dB = 1/sU - 1/sL (barrier gradient = grad F + mu dB) | 156 zero pad
+//
+// Bound pattern: template parameter BM (bit v = finite lower bound on variable v, bit 8+v = finite
+// upper bound; v = 0..5 states, 6..7 inputs) so the common patterns compile to straight-line code;
+// BM < 0 = pattern read at run time.
 #include <math.h>
 
 #include "tt_kernel.hpp"
@@ -40,39 +43,62 @@ namespace {
 
 constexpr int W = 64;
 constexpr int SR = kRowsPerStage;
+constexpr int HEAD = kHead;
 
+// head
+constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54;
 // rows
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
-constexpr int rSG = 68, rGR = 76, rCC = 84, rCT = 90, rK = 96, rKF = 108, rIH = 110, rPS = 113, rPV = 134;
-constexpr int rDXS = 140;
+constexpr int rSG = 68, rGF = 76, rCC = 84, rCT = 90, rK = 96, rKF = 108, rIH = 110, rPS = 113, rPV = 134;
+constexpr int rDXS = 140, rDB = 148, PAD = 156;
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, W);
-    return v;
+// ---- wave reductions: DPP inside each 16-lane row (xor 1, xor 2, half-mirror, mirror), then the four
+// row results by v_readlane into SGPRs.  No LDS; the result is wave-uniform and bitwise identical in
+// every lane (the final combine runs on uniform operands).
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)(b & 0xffffffffll), (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ __forceinline__ double wmax(double v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, W));
-    return v;
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ __forceinline__ double wmin(double v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmin(v, __shfl_xor(v, m, W));
-    return v;
+struct OpSum { __device__ double operator()(double a, double b) const { return a + b; } };
+struct OpMax { __device__ double operator()(double a, double b) const { return fmax(a, b); } };
+struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
+template <class Op>
+__device__ __forceinline__ double wred(double v, Op op) {
+    v = op(v, dppd<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dppd<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dppd<0x141>(v));  // row_half_mirror
+    v = op(v, dppd<0x140>(v));  // row_mirror
+    return op(op(readlane_d(v, 0), readlane_d(v, 16)), op(readlane_d(v, 32), readlane_d(v, 48)));
 }
+__device__ __forceinline__ double wsum(double v) { return wred(v, OpSum()); }
+__device__ __forceinline__ double wmax(double v) { return wred(v, OpMax()); }
+__device__ __forceinline__ double wmin(double v) { return wred(v, OpMin()); }
 
-// upper-triangle enumeration of a symmetric 6x6
-__device__ __forceinline__ void ut_ij(int e, int& i, int& j) {
-    i = e < 6 ? 0 : e < 11 ? 1 : e < 15 ? 2 : e < 18 ? 3 : e < 20 ? 4 : 5;
-    const int start = i == 0 ? 0 : i == 1 ? 6 : i == 2 ? 11 : i == 3 ? 15 : i == 4 ? 18 : 20;
-    j = i + (e - start);
-}
+// packed upper-triangle index of a symmetric 6x6
 __host__ __device__ constexpr int sym_idx(int i, int j) {
     return i <= j ? i * 6 - (i * (i - 1)) / 2 + (j - i) : j * 6 - (j * (j - 1)) / 2 + (i - j);
 }
-
-// dt*J nonzeros: 0:J02 1:J05 2:J12 3:J15 4:J24 5:J25 6:J33 7:J34 8:J35   (A = I + dt*J)
+// nonzeros of dt*J (rows rAJ): 0:D02 1:D05 2:D12 3:D15 4:D24 5:D25 6:D33 7:D34 8:D35  (A = I + dt*J)
+__host__ __device__ constexpr int d_idx(int r, int c) {
+    return (r == 0 && c == 2) ? 0 : (r == 0 && c == 5) ? 1 : (r == 1 && c == 2) ? 2 : (r == 1 && c == 5) ? 3
+         : (r == 2 && c == 4) ? 4 : (r == 2 && c == 5) ? 5 : (r == 3 && c == 3) ? 6 : (r == 3 && c == 4) ? 7
+         : (r == 3 && c == 5) ? 8 : -1;
+}
+// nonzeros of the curvature (rows rWC), symmetric: 0:(2,2) 1:(2,5) 2:(3,3) 3:(3,4) 4:(3,5) 5:(4,4) 6:(4,5)
+__host__ __device__ constexpr int w_idx(int i, int j) {
+    return i > j ? w_idx(j, i)
+         : (i == 2 && j == 2) ? 0 : (i == 2 && j == 5) ? 1 : (i == 3 && j == 3) ? 2 : (i == 3 && j == 4) ? 3
+         : (i == 3 && j == 5) ? 4 : (i == 4 && j == 4) ? 5 : (i == 4 && j == 5) ? 6 : -1;
+}
 // sum_l dtJ[l][v] * y[l*st]   (column v of dtJ)
 __device__ __forceinline__ double colJ(const double* aj, int v, const double* y, int st) {
     switch (v) {
@@ -83,30 +109,27 @@ __device__ __forceinline__ double colJ(const double* aj, int v, const double* y,
         default: return 0.0;
     }
 }
-// sum_l dtJ[r][l] * x[l]   (row r of dtJ)
-__device__ __forceinline__ double rowJ(const double* aj, int r, const double* x) {
-    switch (r) {
-        case 0: return aj[0] * x[2] + aj[1] * x[5];
-        case 1: return aj[2] * x[2] + aj[3] * x[5];
-        case 2: return aj[4] * x[4] + aj[5] * x[5];
-        case 3: return aj[6] * x[3] + aj[7] * x[4] + aj[8] * x[5];
-        default: return 0.0;
-    }
+
+// 1/x by v_rcp_f64 + two Newton steps (within 1 ulp of IEEE division; x finite, nonzero, normal)
+__device__ __forceinline__ double frcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
 }
-// curvature nonzeros: 0:(2,2) 1:(2,5) 2:(3,3) 3:(3,4) 4:(3,5) 5:(4,4) 6:(4,5); -1 = structural zero
-__device__ __forceinline__ int wc_idx(int i, int j) {
-    if (i > j) { int t = i; i = j; j = t; }
-    switch (i * 6 + j) {
-        case 14: return 0;
-        case 17: return 1;
-        case 21: return 2;
-        case 22: return 3;
-        case 23: return 4;
-        case 28: return 5;
-        case 29: return 6;
-        default: return -1;
+
+// sum of logs as log(prod of mantissas) + (sum of exponents) ln 2: one log per stage instead of 16
+struct LogSum {
+    double m = 1.0;
+    int e = 0;
+    __device__ __forceinline__ void add(double s) {
+        int ex;
+        m *= frexp(s, &ex);
+        e += ex;
     }
-}
+    __device__ __forceinline__ double value() const { return log(m) + (double)e * 0.69314718055994530942; }
+};
 
 // Diagnostic phase stamps (MI355X_MICROARCH: s_memtime counts shader cycles).  Compiled out unless
 // -DTT_STAMPS; never in the shipped library.
@@ -136,50 +159,64 @@ __device__ __forceinline__ bool armijo(double trial, double ref, double alpha, d
     return trial - (ref + 1e-4 * alpha * D) <= 10.0 * 2.220446049250313e-16 * fabs(ref);
 }
 
-// fraction-to-boundary helper: largest a with s + a*d >= (1-tau) s
+// fraction-to-boundary: largest a with s + a*d >= (1-tau) s  (divide only when the bound is active)
 __device__ __forceinline__ void ftb(double s, double d, double tau, double& a) {
-    if (d < 0.0) a = fmin(a, -tau * s / d);
+    if (d < 0.0 && tau * s < -a * d) a = -tau * s / d;
 }
 
-// Per-wave solver context (registers: a handful of scalars; data: LDS)
+// Per-wave solver context: a handful of scalars; the data lives in LDS
+template <int BM>
 struct Ctx {
     double* sm;
-    double *QW, *RW, *PW0, *PW1, *PV0, *PV1, *PA, *WV, *XI, *LB, *UB;
     int N, lane;
-    double dt, L1, L2, Mh;
+    double dt, iL1, iL2, Mh;
     double mu, tau, nu;
-    __device__ __forceinline__ double& r(int row, int k) const { return sm[k * SR + row]; }
-    __device__ __forceinline__ bool hl(int v) const { return LB[v] > -INFINITY; }
-    __device__ __forceinline__ bool hu(int v) const { return UB[v] < INFINITY; }
+    __device__ __forceinline__ double& r(int row, int k) const { return sm[HEAD + k * SR + row]; }
+    __device__ __forceinline__ double& h(int i) const { return sm[i]; }
+    __device__ __forceinline__ bool hl(int v) const {
+        if constexpr (BM >= 0) return (BM >> v) & 1;
+        else return sm[hLB + v] > -INFINITY;
+    }
+    __device__ __forceinline__ bool hu(int v) const {
+        if constexpr (BM >= 0) return (BM >> (8 + v)) & 1;
+        else return sm[hUB + v] < INFINITY;
+    }
+    __device__ __forceinline__ double lb(int v) const { return sm[hLB + v]; }
+    __device__ __forceinline__ double ub(int v) const { return sm[hUB + v]; }
+    // barrier gradient component: grad F + mu * (1/sU - 1/sL)
+    __device__ __forceinline__ double gr(int v, int k) const { return r(rGF + v, k) + mu * r(rDB + v, k); }
 };
 
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
-__device__ __forceinline__ void model_f(const Ctx& c, const double* x, const double* u, double* fo) {
+template <int BM>
+__device__ __forceinline__ void model_f(const Ctx<BM>& c, const double* x, const double* u, double* fo) {
     double sth, cth, sps, cps;
     sincos(x[2], &sth, &cth);
     sincos(x[3], &sps, &cps);
     const double t = tan(x[4]), v = x[5];
     fo[0] = v * cth;
     fo[1] = v * sth;
-    fo[2] = v * t / c.L1;
-    fo[3] = -v * t / c.L1 * (1.0 + c.Mh / c.L2 * cps) - v * sps / c.L2;
+    fo[2] = v * t * c.iL1;
+    fo[3] = -v * t * c.iL1 * (1.0 + c.Mh * c.iL2 * cps) - v * sps * c.iL2;
     fo[4] = u[1];
     fo[5] = u[0];
 }
 
 // f, dt*J and the curvature -dt * sum_i y_i d2f_i/dx2 in one pass (5 transcendentals)
-__device__ __forceinline__ void model_lin(const Ctx& c, const double* x, const double* u, const double* y, double* fo,
-                                          double* aj, double* wc) {
-    double sth, cth, sps, cps;
+template <int BM>
+__device__ __forceinline__ void model_lin(const Ctx<BM>& c, const double* x, const double* u, const double* y,
+                                          double* fo, double* aj, double* wc) {
+    double sth, cth, sps, cps, sph, cph;
     sincos(x[2], &sth, &cth);
     sincos(x[3], &sps, &cps);
-    const double phi = x[4], v = x[5], dt = c.dt, Mh = c.Mh, L2 = c.L2;
-    const double t = tan(phi), cph = cos(phi), c2 = 1.0 / (cph * cph);
-    const double k = 1.0 + Mh / L2 * cps, iL1 = 1.0 / c.L1, iL1L2 = 1.0 / (c.L1 * L2);
+    sincos(x[4], &sph, &cph);
+    const double v = x[5], dt = c.dt, Mh = c.Mh, iL1 = c.iL1, iL2 = c.iL2, iL1L2 = iL1 * iL2;
+    const double ic = frcp(cph), t = sph * ic, c2 = ic * ic;
+    const double k = 1.0 + Mh * iL2 * cps;
     fo[0] = v * cth;
     fo[1] = v * sth;
     fo[2] = v * t * iL1;
-    fo[3] = -v * t * iL1 * k - v * sps / L2;
+    fo[3] = -v * t * iL1 * k - v * sps * iL2;
     fo[4] = u[1];
     fo[5] = u[0];
     aj[0] = dt * (-v * sth);
@@ -188,28 +225,31 @@ __device__ __forceinline__ void model_lin(const Ctx& c, const double* x, const d
     aj[3] = dt * sth;
     aj[4] = dt * (v * c2 * iL1);
     aj[5] = dt * (t * iL1);
-    aj[6] = dt * (v * t * Mh * sps * iL1L2 - v * cps / L2);
+    aj[6] = dt * (v * t * Mh * sps * iL1L2 - v * cps * iL2);
     aj[7] = dt * (-v * c2 * iL1 * k);
-    aj[8] = dt * (-t * iL1 * k - sps / L2);
+    aj[8] = dt * (-t * iL1 * k - sps * iL2);
     const double s = -dt;
     wc[0] = s * (y[0] * (-v * cth) + y[1] * (-v * sth));
     wc[1] = s * (y[0] * (-sth) + y[1] * cth);
-    wc[2] = s * (y[3] * (v * t * Mh * cps * iL1L2 + v * sps / L2));
+    wc[2] = s * (y[3] * (v * t * Mh * cps * iL1L2 + v * sps * iL2));
     wc[3] = s * (y[3] * (v * c2 * Mh * sps * iL1L2));
-    wc[4] = s * (y[3] * (t * Mh * sps * iL1L2 - cps / L2));
+    wc[4] = s * (y[3] * (t * Mh * sps * iL1L2 - cps * iL2));
     wc[5] = s * (y[2] * (2.0 * v * t * c2 * iL1) + y[3] * (-2.0 * v * t * c2 * k * iL1));
     wc[6] = s * (y[2] * (c2 * iL1) + y[3] * (-c2 * k * iL1));
 }
 
-struct Err {
-    double dinf, pinf, c0, cmu, sy, sz;
+struct Lin {
+    double dinf, pinf, c0, cmu, sy, sz;  // optimality-error pieces
+    double cost, logs, th;               // merit pieces at the current point: F, sum log s, ||c||_1
 };
 
-// ============ linearise at the current point + optimality-error pieces (stage-parallel) ============
-__device__ __forceinline__ Err phase_linearize(const Ctx& c) {
+// ============ linearise at the current point (stage-parallel) ============
+// f, dt*J, curvature, constraint residual c, grad F, Sigma, dB, and the optimality / merit pieces.
+template <int BM>
+__device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
     const int N = c.N;
-    double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0;
-    bool fin = true;
+    double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0, cost = 0.0, th = 0.0, logs = 0.0;
+    bool fin = true, bad = false;
     for (int k = c.lane; k <= N; k += W) {
         double x[6], u[2] = {0.0, 0.0}, yk[6], y1[6] = {0, 0, 0, 0, 0, 0}, aj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -217,9 +257,10 @@ __device__ __forceinline__ Err phase_linearize(const Ctx& c) {
         if (k == 0) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const double cc = x[i] - c.XI[i];
+                const double cc = x[i] - c.h(hXI + i);
                 c.r(rCC + i, 0) = cc;
                 pinf = fmax(pinf, fabs(cc));
+                th += fabs(cc);
             }
         }
         if (k < N) {
@@ -238,228 +279,268 @@ __device__ __forceinline__ Err phase_linearize(const Ctx& c) {
                 const double cc = c.r(rX + i, k + 1) - (x[i] + c.dt * fo[i]);
                 c.r(rCC + i, k + 1) = cc;
                 pinf = fmax(pinf, fabs(cc));
+                th += fabs(cc);
             }
         }
+        // tracking cost and its gradient (no 1/2: F = dx' Qw dx + du' Rw du, grad = 2 Qw dx)
         double dxr[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.r(rXR + i, k);
+        double du0 = 0.0, du1 = 0.0;
+        if (k < N) { du0 = u[0] - c.r(rUR, k); du1 = u[1] - c.r(rUR + 1, k); }
+        LogSum ls;
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
-            double g;  // d/dz of the Lagrangian: 2 Qw dx + y_k - A'y_{k+1} - zL + zU
+            double gf;
             if (v < 6) {
-                g = 0.0;
+                gf = 0.0;
 #pragma unroll
-                for (int j = 0; j < 6; ++j) g += c.QW[v * 6 + j] * dxr[j];
-                g = 2.0 * g + yk[v];
-                if (k < N) g -= y1[v] + colJ(aj, v, y1, 1);
+                for (int j = 0; j < 6; ++j) gf += c.h(hQW + v * 6 + j) * dxr[j];
+                cost += dxr[v] * gf;
+                gf *= 2.0;
             } else {
                 const int rr = v - 6;
-                g = 2.0 * (c.RW[rr * 2] * (u[0] - c.r(rUR, k)) + c.RW[rr * 2 + 1] * (u[1] - c.r(rUR + 1, k)));
-                g -= c.dt * y1[rr == 0 ? 5 : 4];
+                gf = c.h(hRW + rr * 2) * du0 + c.h(hRW + rr * 2 + 1) * du1;
+                cost += (rr == 0 ? du0 : du1) * gf;
+                gf *= 2.0;
+            }
+            c.r(rGF + v, k) = gf;
+            // d/dz of the Lagrangian: grad F + y_k - A'y_{k+1} - zL + zU
+            double g = gf;
+            if (v < 6) {
+                g += yk[v];
+                if (k < N) g -= y1[v] + colJ(aj, v, y1, 1);
+            } else {
+                g -= c.dt * y1[v == 6 ? 5 : 4];
             }
             const double xv = v < 6 ? x[v] : u[v - 6];
+            double sg = 0.0, db = 0.0;
             if (c.hl(v)) {
-                const double zl = c.r(rZL + v, k), s = xv - c.LB[v];
+                const double zl = c.r(rZL + v, k), s = xv - c.lb(v), rs = frcp(s);
                 g -= zl;
                 c0 = fmax(c0, fabs(zl * s));
                 cmu = fmax(cmu, fabs(zl * s - c.mu));
                 sz += zl;
+                sg += zl * rs;
+                db -= rs;
+                if (s <= 0.0) bad = true; else ls.add(s);
             }
             if (c.hu(v)) {
-                const double zu = c.r(rZU + v, k), s = c.UB[v] - xv;
+                const double zu = c.r(rZU + v, k), s = c.ub(v) - xv, rs = frcp(s);
                 g += zu;
                 c0 = fmax(c0, fabs(zu * s));
                 cmu = fmax(cmu, fabs(zu * s - c.mu));
                 sz += zu;
+                sg += zu * rs;
+                db += rs;
+                if (s <= 0.0) bad = true; else ls.add(s);
             }
+            c.r(rSG + v, k) = sg;
+            c.r(rDB + v, k) = db;
             if (!isfinite(g)) fin = false;
             dinf = fmax(dinf, fabs(g));
         }
+        logs += ls.value();
     }
-    Err e;
-    e.dinf = wmax(fin ? dinf : INFINITY);
+    Lin e;
+    e.dinf = wmax((fin && !bad) ? dinf : INFINITY);
     e.pinf = wmax(pinf);
     e.c0 = wmax(c0);
     e.cmu = wmax(cmu);
     e.sy = wsum(sy);
     e.sz = wsum(sz);
+    e.cost = wsum(cost);
+    e.logs = wsum(logs);
+    e.th = wsum(th);
+    __syncthreads();
     return e;
 }
 
-__device__ __forceinline__ double phase_compl_mu(const Ctx& c) {
+template <int BM>
+__device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
     double cm = 0.0;
     for (int k = c.lane; k <= c.N; k += W) {
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == c.N) break;
             const double xv = c.r(rX + v, k);
-            if (c.hl(v)) cm = fmax(cm, fabs(c.r(rZL + v, k) * (xv - c.LB[v]) - c.mu));
-            if (c.hu(v)) cm = fmax(cm, fabs(c.r(rZU + v, k) * (c.UB[v] - xv) - c.mu));
+            if (c.hl(v)) cm = fmax(cm, fabs(c.r(rZL + v, k) * (xv - c.lb(v)) - c.mu));
+            if (c.hu(v)) cm = fmax(cm, fabs(c.r(rZU + v, k) * (c.ub(v) - xv) - c.mu));
         }
     }
     return wmax(cm);
 }
 
-// ============ barrier Hessian diagonal Sigma and barrier gradient (stage-parallel) ============
-__device__ __forceinline__ void phase_barrier(const Ctx& c) {
-    const int N = c.N;
-    for (int k = c.lane; k <= N; k += W) {
-        double dxr[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) dxr[i] = c.r(rX + i, k) - c.r(rXR + i, k);
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == N) break;
-            double g;
-            if (v < 6) {
-                g = 0.0;
-#pragma unroll
-                for (int j = 0; j < 6; ++j) g += c.QW[v * 6 + j] * dxr[j];
-                g *= 2.0;
-            } else {
-                const int rr = v - 6;
-                g = 2.0 * (c.RW[rr * 2] * (c.r(rX + 6, k) - c.r(rUR, k)) + c.RW[rr * 2 + 1] * (c.r(rX + 7, k) - c.r(rUR + 1, k)));
-            }
-            const double xv = c.r(rX + v, k);
-            double sg = 0.0;
-            if (c.hl(v)) { const double s = xv - c.LB[v]; sg += c.r(rZL + v, k) / s; g -= c.mu / s; }
-            if (c.hu(v)) { const double s = c.UB[v] - xv; sg += c.r(rZU + v, k) / s; g += c.mu / s; }
-            c.r(rSG + v, k) = sg;
-            c.r(rGR + v, k) = g;
-        }
-    }
-    __syncthreads();
+// ============ Riccati on the FP64 matrix cores (v_mfma_f64_16x16x4_f64) ============
+// Affine augmentation x^ = [dx; 1] turns the value function, dynamics and feed-forward into 7x7
+// matrices, padded into one 16x16 f64 tile:
+//   A^ = [[A, b],[0, 1]] (b = -c_{k+1}),  H^ = [[H_xx, g_x],[g_x', 0]],  S^ = [0, g_u],  B^ = [B; 0]
+//   PA = P^ A^  (2 MFMA, K = 8),  F = A^' PA + H^  (2 MFMA, C = H^),
+//   G = B^' PA + S^ = dt * rows (5,4) of PA + S^,  H_uu = 2Rw + Sig_u + dt^2 P[{5,4},{5,4}],
+//   P^_k = F - G' (H_uu^-1 G)  (1 MFMA, K = 2 of 4),  K^ = [K, k_ff] = -H_uu^-1 G.
+// Layouts (lane l, c = l & 15, q = l >> 4): accumulator reg r = element (q + 4r, c); A operand of
+// k-step s = element (c, 4s + q); B operand of k-step s = element (4s + q, c).  P^ is symmetric, so
+// its accumulator registers ARE its A- and B-operand registers: P^ never leaves VGPRs.  A^ as the
+// B operand of step 1 and A^' as the A operand of step 2 are the same lane value.  G needs rows 4
+// and 5 of PA in each lane: one lane swap (xor 16).  Five MFMAs per stage, no barrier.
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// ============ Riccati backward sweep; returns false if a reduced input Hessian is not PD ============
-__device__ __forceinline__ bool phase_riccati(const Ctx& c, double dw) {
-    const int N = c.N, lane = c.lane;
-    const double dt = c.dt, dt2 = dt * dt;
-    double* Pc = c.PW0;
-    double* Pn = c.PW1;
-    double* pc = c.PV0;
-    double* pn = c.PV1;
-    double* PA = c.PA;
-    double* WV = c.WV;
-    if (lane < 21) {
-        int i, j;
-        ut_ij(lane, i, j);
-        const double v = 2.0 * c.QW[i * 6 + j] + (i == j ? c.r(rSG + i, N) + dw : 0.0);
-        Pc[i * 6 + j] = v;
-        Pc[j * 6 + i] = v;
-        c.r(rPS + lane, N) = v;
-    } else if (lane < 27) {
-        const int rr = lane - 21;
-        const double v = c.r(rGR + rr, N);
-        pc[rr] = v;
-        c.r(rPV + rr, N) = v;
+// Per-lane operand slots of the Riccati tile (stage-relative LDS rows; PAD reads zero).
+struct RicMap {
+    int aj0, aj1, cr0, cr1;    // A^[4s+q][cc] = one + row aj (stage k) - row cr (stage k+1)
+    double one0, one1;
+    int hw0, hw1, hsg0, hsg1, hgr0, hgr1;  // H^[q+4r][cc] = q2 + w + sigma + g_x (+ dw on the diagonal)
+    double q20, q21, dg0, dg1;
+    int ps0, ps1;             // store row of P^_k[q+4r][cc] (upper part), -1 = none
+    __device__ __forceinline__ void init(int lane, const double* QW) {
+        const int q = lane >> 4, cc = lane & 15;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int kap = 4 * s + q, n = cc;
+            const double one = (kap == n && kap <= 6) ? 1.0 : 0.0;
+            const int aj = (kap < 6 && n < 6 && d_idx(kap, n) >= 0) ? rAJ + d_idx(kap, n) : PAD;
+            const int cr = (kap < 6 && n == 6) ? rCC + kap : PAD;
+            const int row = q + 4 * s, col = cc;  // s doubles as the accumulator register r
+            const double q2 = (row < 6 && col < 6) ? 2.0 * QW[row * 6 + col] : 0.0;
+            const int hw = (row < 6 && col < 6 && w_idx(row, col) >= 0) ? rWC + w_idx(row, col) : PAD;
+            const int hsg = (row == col && row < 6) ? rSG + row : PAD;
+            const int hgr = (row < 6 && col == 6) ? row : (row == 6 && col < 6) ? col : -1;
+            const double dg = (row == col && row < 6) ? 1.0 : 0.0;
+            const int ps = (row <= col && col < 6) ? rPS + sym_idx(row, col) : (row < 6 && col == 6) ? rPV + row : -1;
+            if (s == 0) { aj0 = aj; cr0 = cr; one0 = one; q20 = q2; hw0 = hw; hsg0 = hsg; hgr0 = hgr; dg0 = dg; ps0 = ps; }
+            else        { aj1 = aj; cr1 = cr; one1 = one; q21 = q2; hw1 = hw; hsg1 = hsg; hgr1 = hgr; dg1 = dg; ps1 = ps; }
+        }
     }
-    __syncthreads();
+};
+
+template <int BM>
+__device__ __forceinline__ double hhat(const Ctx<BM>& c, int hw, int hsg, int hgr, double q2, double dg, int k,
+                                       double dw, bool with_w) {
+    double v = q2 + c.r(hsg, k) + dg * dw;
+    if (hgr >= 0) v += c.gr(hgr, k);
+    if (with_w) v += c.r(hw, k);
+    return v;
+}
+
+template <int BM>
+__device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
+    const int N = c.N, q = c.lane >> 4, cc = c.lane & 15;
+    RicMap m;
+    m.init(c.lane, c.sm + hQW);
+    const double dt = c.dt, dt2 = dt * dt;
+    const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
+    d4 P;
+    P[0] = hhat(c, m.hw0, m.hsg0, m.hgr0, m.q20, m.dg0, N, dw, false);
+    P[1] = hhat(c, m.hw1, m.hsg1, m.hgr1, m.q21, m.dg1, N, dw, false);
+    P[2] = 0.0;
+    P[3] = 0.0;
+    if (m.ps0 >= 0) c.r(m.ps0, N) = P[0];
+    if (m.ps1 >= 0) c.r(m.ps1, N) = P[1];
+    bool pd = true;
     for (int k = N - 1; k >= 0; --k) {
-        double aj[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) aj[i] = c.r(rAJ + i, k);
-        // --- step 1: PA = P A ; w = P b + p  (b = -c_{k+1})
-        if (lane < 36) {
-            const int i = lane / 6, j = lane % 6;
-            PA[lane] = Pc[lane] + colJ(aj, j, Pc + i * 6, 1);
-        } else if (lane < 42) {
-            const int rr = lane - 36;
-            double s = pc[rr];
-#pragma unroll
-            for (int l = 0; l < 6; ++l) s -= Pc[rr * 6 + l] * c.r(rCC + l, k + 1);
-            WV[rr] = s;
-        }
-        __syncthreads();
-        // --- step 2: reduced input Hessian H = 2R + Sigma_u + B'PB (every lane, wave-uniform)
-        const double h00 = 2.0 * c.RW[0] + c.r(rSG + 6, k) + dw + dt2 * Pc[35];
-        const double h01 = 2.0 * c.RW[1] + dt2 * Pc[34];
-        const double h11 = 2.0 * c.RW[3] + c.r(rSG + 7, k) + dw + dt2 * Pc[28];
+        // operands (independent of P)
+        const double a0 = m.one0 + c.r(m.aj0, k) - c.r(m.cr0, k + 1);
+        const double a1 = m.one1 + c.r(m.aj1, k) - c.r(m.cr1, k + 1);
+        d4 H;
+        H[0] = hhat(c, m.hw0, m.hsg0, m.hgr0, m.q20, m.dg0, k, dw, true);
+        H[1] = hhat(c, m.hw1, m.hsg1, m.hgr1, m.q21, m.dg1, k, dw, true);
+        H[2] = 0.0;
+        H[3] = 0.0;
+        const double sgu0 = c.r(rSG + 6, k), sgu1 = c.r(rSG + 7, k), gu0 = c.gr(6, k), gu1 = c.gr(7, k);
+        // reduced input Hessian from P_{k+1}: P[5][5] lane 21, P[5][4] lane 20, P[4][4] lane 4 (reg 1)
+        const double p55 = readlane_d(P[1], 21), p54 = readlane_d(P[1], 20), p44 = readlane_d(P[1], 4);
+        const double h00 = r00 + sgu0 + dw + dt2 * p55, h01 = r01 + dt2 * p54, h11 = r11 + sgu1 + dw + dt2 * p44;
         const double det = h00 * h11 - h01 * h01;
-        if (!(h00 > 0.0 && h11 > 0.0 && det > 1e-13 * h00 * h11)) {
-            __syncthreads();
-            return false;
-        }
-        const double id = 1.0 / det, i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
-        const double hv0 = c.r(rGR + 6, k) + dt * WV[5];
-        const double hv1 = c.r(rGR + 7, k) + dt * WV[4];
-        const double kf0 = -(i00 * hv0 + i01 * hv1), kf1 = -(i01 * hv0 + i11 * hv1);
-        if (lane < 21) {  // P_k = A'PA + H_xx - G' H^-1 G, G = B'PA (rows 5, 4 of PA scaled by dt)
-            int i, j;
-            ut_ij(lane, i, j);
-            const int wi = wc_idx(i, j);
-            double F = PA[i * 6 + j] + colJ(aj, i, PA + j, 6) + 2.0 * c.QW[i * 6 + j] + (wi >= 0 ? c.r(rWC + wi, k) : 0.0);
-            if (i == j) F += c.r(rSG + i, k) + dw;
-            const double g0i = dt * PA[30 + i], g1i = dt * PA[24 + i];
-            const double g0j = dt * PA[30 + j], g1j = dt * PA[24 + j];
-            const double v = F - (g0i * (i00 * g0j + i01 * g1j) + g1i * (i01 * g0j + i11 * g1j));
-            Pn[i * 6 + j] = v;
-            Pn[j * 6 + i] = v;
-            c.r(rPS + lane, k) = v;
-        } else if (lane < 27) {  // p_k = g_x + A'w + G' k_ff
-            const int rr = lane - 21;
-            const double v = c.r(rGR + rr, k) + WV[rr] + colJ(aj, rr, WV, 1) + dt * PA[30 + rr] * kf0 + dt * PA[24 + rr] * kf1;
-            pn[rr] = v;
-            c.r(rPV + rr, k) = v;
-        } else if (lane < 39) {  // K = -H^-1 G
-            const int e = lane - 27, rr = e / 6, cc = e % 6;
-            const double g0c = dt * PA[30 + cc], g1c = dt * PA[24 + cc];
-            c.r(rK + e, k) = rr == 0 ? -(i00 * g0c + i01 * g1c) : -(i01 * g0c + i11 * g1c);
-        } else if (lane == 39) {
-            c.r(rKF, k) = kf0;
-            c.r(rKF + 1, k) = kf1;
+        if (!(h00 > 0.0 && h11 > 0.0 && det > 1e-13 * h00 * h11)) { pd = false; break; }
+        const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
+        // PA = P^ A^
+        d4 PA = {0.0, 0.0, 0.0, 0.0};
+        PA = mfma(P[0], a0, PA);
+        PA = mfma(P[1], a1, PA);
+        // F = A^' PA + H^
+        d4 F = mfma(a0, PA[0], H);
+        F = mfma(a1, PA[1], F);
+        // G rows: lanes q = 0 / 1 hold PA rows 4 / 5 in reg 1; swap to get the other row
+        const double own = PA[1], sw = __shfl_xor(own, 16, W);
+        const double pa5 = q == 0 ? sw : own, pa4 = q == 0 ? own : sw;
+        const double g0 = dt * pa5 + (cc == 6 ? gu0 : 0.0);
+        const double g1 = dt * pa4 + (cc == 6 ? gu1 : 0.0);
+        const double m0 = i00 * g0 + i01 * g1, m1 = i01 * g0 + i11 * g1;
+        const double aop = q == 0 ? -g0 : q == 1 ? -g1 : 0.0;
+        const double bop = q == 0 ? m0 : q == 1 ? m1 : 0.0;
+        P = mfma(aop, bop, F);
+        // K^ = -M, inverse input Hessian, P^_k
+        if (q < 2 && cc < 7) c.r(cc < 6 ? rK + 6 * q + cc : rKF + q, k) = -bop;
+        if (c.lane == 0) {
             c.r(rIH, k) = i00;
             c.r(rIH + 1, k) = i01;
             c.r(rIH + 2, k) = i11;
         }
-        double* t = Pc; Pc = Pn; Pn = t;
-        t = pc; pc = pn; pn = t;
-        __syncthreads();
+        if (m.ps0 >= 0) c.r(m.ps0, k) = P[0];
+        if (m.ps1 >= 0) c.r(m.ps1, k) = P[1];
     }
-    return true;
+    __syncthreads();
+    return pd;
 }
 
-// ============ forward sweep (lane 0): dx_0 = -c_0; du = K dx + k_ff; dx' = A dx + B du - c ============
-__device__ __forceinline__ void phase_forward(const Ctx& c, int crow, int orow) {
-    if (c.lane == 0) {
-        const double dt = c.dt;
-        double dx[6];
+// ============ forward sweep on the matrix cores: [x^_{k+1}; du_k] = [Phi_k; K^_k] x^_k ============
+// Phi = A^ + B^ K^ (rows 0..6), rows 7,8 = K^; x^ stays in accumulator column 0, which is exactly
+// the B-operand layout of the next step (2 MFMAs per stage, nothing moves between lanes).
+template <int BM>
+__device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int orow) {
+    const int N = c.N, q = c.lane >> 4, i = c.lane & 15;
+    // operand slots: Phi[i][kappa], kappa = 4s + q
+    int faj[2], fcr[2], fk[2];
+    double fone[2], fkc[2];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) { dx[i] = -c.r(crow + i, 0); c.r(orow + i, 0) = dx[i]; }
-        for (int k = 0; k < c.N; ++k) {
-            double aj[9], K[12], cc[6];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) aj[i] = c.r(rAJ + i, k);
-#pragma unroll
-            for (int i = 0; i < 12; ++i) K[i] = c.r(rK + i, k);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) cc[i] = c.r(crow + i, k + 1);
-            double du0 = c.r(rKF, k), du1 = c.r(rKF + 1, k);
-#pragma unroll
-            for (int j = 0; j < 6; ++j) { du0 += K[j] * dx[j]; du1 += K[6 + j] * dx[j]; }
-            c.r(orow + 6, k) = du0;
-            c.r(orow + 7, k) = du1;
-            double nx[6];
-#pragma unroll
-            for (int rr = 0; rr < 6; ++rr) nx[rr] = dx[rr] + rowJ(aj, rr, dx) - cc[rr];
-            nx[5] += dt * du0;
-            nx[4] += dt * du1;
-#pragma unroll
-            for (int rr = 0; rr < 6; ++rr) { dx[rr] = nx[rr]; c.r(orow + rr, k + 1) = nx[rr]; }
+    for (int s = 0; s < 2; ++s) {
+        const int kap = 4 * s + q;
+        fone[s] = (i == kap && i <= 6) ? 1.0 : 0.0;
+        faj[s] = (i < 6 && kap < 6 && d_idx(i, kap) >= 0) ? rAJ + d_idx(i, kap) : PAD;
+        fcr[s] = (i < 6 && kap == 6) ? crow + i : PAD;
+        const int u = (i == 5 || i == 7) ? 0 : (i == 4 || i == 8) ? 1 : -1;
+        fk[s] = (u >= 0 && kap < 6) ? rK + 6 * u + kap : (u >= 0 && kap == 6) ? rKF + u : PAD;
+        fkc[s] = (u >= 0 && kap <= 6) ? (i < 6 ? c.dt : 1.0) : 0.0;
+    }
+    d4 X = {0.0, 0.0, 0.0, 0.0};
+    if (i == 0) {  // x^_0 = [-c_0; 1]
+        X[0] = -c.r(crow + q, 0);
+        X[1] = q < 2 ? -c.r(crow + q + 4, 0) : (q == 2 ? 1.0 : 0.0);
+        c.r(orow + q, 0) = X[0];
+        if (q < 2) c.r(orow + q + 4, 0) = X[1];
+    }
+    for (int k = 0; k < N; ++k) {
+        const double a0 = fone[0] + c.r(faj[0], k) - c.r(fcr[0], k + 1) + fkc[0] * c.r(fk[0], k);
+        const double a1 = fone[1] + c.r(faj[1], k) - c.r(fcr[1], k + 1) + fkc[1] * c.r(fk[1], k);
+        d4 Y = {0.0, 0.0, 0.0, 0.0};
+        Y = mfma(a0, X[0], Y);
+        Y = mfma(a1, X[1], Y);
+        if (i == 0) {
+            // rows 0..5 -> dx_{k+1}; row 7 (q=3, reg 1) -> du0; row 8 (q=0, reg 2) -> du1
+            c.r(orow + q, k + 1) = Y[0];
+            if (q < 2) c.r(orow + q + 4, k + 1) = Y[1];
+            if (q == 3) c.r(orow + 6, k) = Y[1];
+            if (q == 0) c.r(orow + 7, k) = Y[2];
         }
+        X = Y;
     }
     __syncthreads();
 }
 
 // ============ SOC: backward vector pass with the stored factorisation, rhs c_soc in rCT ============
-__device__ __forceinline__ void phase_soc_backward(const Ctx& c) {
+template <int BM>
+__device__ __forceinline__ void phase_soc_backward(const Ctx<BM>& c) {
     if (c.lane == 0) {
         const int N = c.N;
         const double dt = c.dt;
         double p[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) p[i] = c.r(rGR + i, N);
+        for (int i = 0; i < 6; ++i) p[i] = c.gr(i, N);
         for (int k = N - 1; k >= 0; --k) {
             double aj[9], w[6], cn[6];
 #pragma unroll
@@ -473,13 +554,13 @@ __device__ __forceinline__ void phase_soc_backward(const Ctx& c) {
                 for (int l = 0; l < 6; ++l) s -= c.r(rPS + sym_idx(rr, l), k + 1) * cn[l];
                 w[rr] = s;
             }
-            const double h0 = c.r(rGR + 6, k) + dt * w[5], h1 = c.r(rGR + 7, k) + dt * w[4];
+            const double h0 = c.gr(6, k) + dt * w[5], h1 = c.gr(7, k) + dt * w[4];
             const double i00 = c.r(rIH, k), i01 = c.r(rIH + 1, k), i11 = c.r(rIH + 2, k);
             c.r(rKF, k) = -(i00 * h0 + i01 * h1);
             c.r(rKF + 1, k) = -(i01 * h0 + i11 * h1);
 #pragma unroll
             for (int rr = 0; rr < 6; ++rr) {
-                p[rr] = c.r(rGR + rr, k) + w[rr] + colJ(aj, rr, w, 1) + c.r(rK + rr, k) * h0 + c.r(rK + 6 + rr, k) * h1;
+                p[rr] = c.gr(rr, k) + w[rr] + colJ(aj, rr, w, 1) + c.r(rK + rr, k) * h0 + c.r(rK + 6 + rr, k) * h1;
                 c.r(rPV + rr, k) = p[rr];
             }
         }
@@ -488,13 +569,14 @@ __device__ __forceinline__ void phase_soc_backward(const Ctx& c) {
 }
 
 struct StepInfo {
-    double ap, az, ymax, Dg, th0, rel;
+    double ap, az, ymax, Dg, rel;
 };
 
 // ============ new multipliers y+ = -(P dx + p), step bounds, merit slope (stage-parallel) ============
-__device__ __forceinline__ StepInfo phase_step(const Ctx& c, int dzr, bool primal_pieces) {
+template <int BM>
+__device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool primal_pieces) {
     const int N = c.N;
-    double ap = 1.0, az = 1.0, ymax = 0.0, Dg = 0.0, th0 = 0.0, rel = 0.0;
+    double ap = 1.0, az = 1.0, ymax = 0.0, Dg = 0.0, rel = 0.0;
     for (int k = c.lane; k <= N; k += W) {
         double dx[6];
 #pragma unroll
@@ -506,23 +588,22 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx& c, int dzr, bool prima
             for (int j = 0; j < 6; ++j) s += c.r(rPS + sym_idx(i, j), k) * dx[j];
             c.r(rYP + i, k) = -s;
             ymax = fmax(ymax, fabs(s));
-            th0 += fabs(c.r(rCC + i, k));
         }
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
             const double d = c.r(dzr + v, k), xv = c.r(rX + v, k);
-            Dg += c.r(rGR + v, k) * d;
+            Dg += c.gr(v, k) * d;
             rel = fmax(rel, fabs(d) / (1.0 + fabs(xv)));
             if (c.hl(v)) {
-                const double s = xv - c.LB[v], zl = c.r(rZL + v, k);
+                const double s = xv - c.lb(v), rs = frcp(s), zl = c.r(rZL + v, k);
                 ftb(s, d, c.tau, ap);
-                ftb(zl, c.mu / s - zl - zl / s * d, c.tau, az);
+                ftb(zl, (c.mu - zl * d) * rs - zl, c.tau, az);
             }
             if (c.hu(v)) {
-                const double s = c.UB[v] - xv, zu = c.r(rZU + v, k);
+                const double s = c.ub(v) - xv, rs = frcp(s), zu = c.r(rZU + v, k);
                 ftb(s, -d, c.tau, ap);
-                ftb(zu, c.mu / s - zu + zu / s * d, c.tau, az);
+                ftb(zu, (c.mu + zu * d) * rs - zu, c.tau, az);
             }
         }
     }
@@ -532,19 +613,19 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx& c, int dzr, bool prima
     if (primal_pieces) {
         r.ymax = wmax(ymax);
         r.Dg = wsum(Dg);
-        r.th0 = wsum(th0);
         r.rel = wmax(rel);
     } else {
-        r.ymax = r.Dg = r.th0 = r.rel = 0.0;
+        r.ymax = r.Dg = r.rel = 0.0;
     }
     __syncthreads();
     return r;
 }
 
 // ============ merit value at z + alpha*dz (rows dzr): F - mu*sum(log s) + nu*||c||_1 ============
-__device__ __forceinline__ double phase_merit(const Ctx& c, double alpha, int dzr, bool storeC) {
+template <int BM>
+__device__ __forceinline__ double phase_merit(const Ctx<BM>& c, double alpha, int dzr, bool storeC) {
     const int N = c.N;
-    double cost = 0.0, bar = 0.0, th = 0.0;
+    double val = 0.0;
     bool bad = false;
     for (int k = c.lane; k <= N; k += W) {
         double x[6], u[2] = {0.0, 0.0};
@@ -554,31 +635,32 @@ __device__ __forceinline__ double phase_merit(const Ctx& c, double alpha, int dz
             u[0] = c.r(rX + 6, k) + alpha * c.r(dzr + 6, k);
             u[1] = c.r(rX + 7, k) + alpha * c.r(dzr + 7, k);
         }
-        double dxr[6];
+        double dxr[6], cost = 0.0, th = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.r(rXR + i, k);
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             double s = 0.0;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) s += c.QW[i * 6 + j] * dxr[j];
+            for (int j = 0; j < 6; ++j) s += c.h(hQW + i * 6 + j) * dxr[j];
             cost += dxr[i] * s;
         }
         if (k < N) {
             const double e0 = u[0] - c.r(rUR, k), e1 = u[1] - c.r(rUR + 1, k);
-            cost += e0 * (c.RW[0] * e0 + c.RW[1] * e1) + e1 * (c.RW[2] * e0 + c.RW[3] * e1);
+            cost += e0 * (c.h(hRW) * e0 + c.h(hRW + 1) * e1) + e1 * (c.h(hRW + 2) * e0 + c.h(hRW + 3) * e1);
         }
+        LogSum ls;
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
             const double xv = v < 6 ? x[v] : u[v - 6];
-            if (c.hl(v)) { const double s = xv - c.LB[v]; if (s <= 0.0) bad = true; else bar -= c.mu * log(s); }
-            if (c.hu(v)) { const double s = c.UB[v] - xv; if (s <= 0.0) bad = true; else bar -= c.mu * log(s); }
+            if (c.hl(v)) { const double s = xv - c.lb(v); if (s <= 0.0) bad = true; else ls.add(s); }
+            if (c.hu(v)) { const double s = c.ub(v) - xv; if (s <= 0.0) bad = true; else ls.add(s); }
         }
         if (k == 0) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const double cc = x[i] - c.XI[i];
+                const double cc = x[i] - c.h(hXI + i);
                 th += fabs(cc);
                 if (storeC) c.r(rCT + i, 0) = cc;
             }
@@ -594,17 +676,16 @@ __device__ __forceinline__ double phase_merit(const Ctx& c, double alpha, int dz
                 if (storeC) c.r(rCT + i, k + 1) = cc;
             }
         }
+        val += cost - c.mu * ls.value() + c.nu * th;
     }
-    const double badv = wmax(bad ? 1.0 : 0.0);
-    cost = wsum(cost);
-    bar = wsum(bar);
-    th = wsum(th);
+    const double v = wsum(bad ? INFINITY : val);  // one reduction; any bad lane -> +inf
     __syncthreads();
-    return badv > 0.0 ? INFINITY : cost + bar + c.nu * th;
+    return v;
 }
 
 // ============ accept the step (stage-parallel) ============
-__device__ __forceinline__ void phase_update(const Ctx& c, int dzr, double alpha, double az) {
+template <int BM>
+__device__ __forceinline__ void phase_update(const Ctx<BM>& c, int dzr, double alpha, double az) {
     const int N = c.N;
     for (int k = c.lane; k <= N; k += W) {
 #pragma unroll
@@ -612,14 +693,14 @@ __device__ __forceinline__ void phase_update(const Ctx& c, int dzr, double alpha
             if (v >= 6 && k == N) break;
             const double d = c.r(dzr + v, k), xo = c.r(rX + v, k), xn = xo + alpha * d;
             if (c.hl(v)) {
-                const double s = xo - c.LB[v], zl = c.r(rZL + v, k);
-                const double znew = zl + az * (c.mu / s - zl - zl / s * d), sn = xn - c.LB[v];
-                c.r(rZL + v, k) = fmax(fmin(znew, 1e10 * c.mu / sn), c.mu / (1e10 * sn));  // kappa_sigma
+                const double zl = c.r(rZL + v, k), rs = frcp(xo - c.lb(v));
+                const double znew = zl + az * ((c.mu - zl * d) * rs - zl), rn = c.mu * frcp(xn - c.lb(v));
+                c.r(rZL + v, k) = fmax(fmin(znew, 1e10 * rn), 1e-10 * rn);  // kappa_sigma = 1e10
             }
             if (c.hu(v)) {
-                const double s = c.UB[v] - xo, zu = c.r(rZU + v, k);
-                const double znew = zu + az * (c.mu / s - zu + zu / s * d), sn = c.UB[v] - xn;
-                c.r(rZU + v, k) = fmax(fmin(znew, 1e10 * c.mu / sn), c.mu / (1e10 * sn));
+                const double zu = c.r(rZU + v, k), rs = frcp(c.ub(v) - xo);
+                const double znew = zu + az * ((c.mu + zu * d) * rs - zu), rn = c.mu * frcp(c.ub(v) - xn);
+                c.r(rZU + v, k) = fmax(fmin(znew, 1e10 * rn), 1e-10 * rn);
             }
             c.r(rX + v, k) = xn;
         }
@@ -630,7 +711,8 @@ __device__ __forceinline__ void phase_update(const Ctx& c, int dzr, double alpha
 }
 
 // ============ c_soc = alpha c(z) + c(z + alpha dz), in place in rCT ============
-__device__ __forceinline__ void phase_soc_rhs(const Ctx& c, double alpha) {
+template <int BM>
+__device__ __forceinline__ void phase_soc_rhs(const Ctx<BM>& c, double alpha) {
     for (int k = c.lane; k <= c.N; k += W) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) c.r(rCT + i, k) = alpha * c.r(rCC + i, k) + c.r(rCT + i, k);
@@ -638,42 +720,44 @@ __device__ __forceinline__ void phase_soc_rhs(const Ctx& c, double alpha) {
     __syncthreads();
 }
 
-__device__ __forceinline__ double phase_soc_alpha(const Ctx& c) {
+template <int BM>
+__device__ __forceinline__ double phase_soc_alpha(const Ctx<BM>& c) {
     double as = 1.0;
     for (int k = c.lane; k <= c.N; k += W) {
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == c.N) break;
             const double d = c.r(rDXS + v, k), xv = c.r(rX + v, k);
-            if (c.hl(v)) ftb(xv - c.LB[v], d, c.tau, as);
-            if (c.hu(v)) ftb(c.UB[v] - xv, -d, c.tau, as);
+            if (c.hl(v)) ftb(xv - c.lb(v), d, c.tau, as);
+            if (c.hu(v)) ftb(c.ub(v) - xv, -d, c.tau, as);
         }
     }
     return wmin(as);
 }
 
 // ---------------- load one instance into LDS (coalesced flat copies) ----------------
-__device__ __forceinline__ void phase_load(const Ctx& c, const TrackArgs& a, int b) {
+template <int BM>
+__device__ __forceinline__ void phase_load(const Ctx<BM>& c, const TrackArgs& a, int b) {
     const int lane = c.lane, N = c.N, S = N + 1, n = 8 * N + 6;
     if (lane < 8) {  // relaxed bounds (bound_relax_factor 1e-8), -inf/+inf = free
         const int v = lane;
         const double l = v < 6 ? a.xlb[v] : a.ulb[v - 6];
         const double u = v < 6 ? a.xub[v] : a.uub[v - 6];
         const bool hl = isfinite(l) && l > -1e19, hu = isfinite(u) && u < 1e19;
-        c.LB[v] = hl ? l - 1e-8 * fmax(1.0, fabs(l)) : -INFINITY;
-        c.UB[v] = hu ? u + 1e-8 * fmax(1.0, fabs(u)) : INFINITY;
+        c.h(hLB + v) = hl ? l - 1e-8 * fmax(1.0, fabs(l)) : -INFINITY;
+        c.h(hUB + v) = hu ? u + 1e-8 * fmax(1.0, fabs(u)) : INFINITY;
     }
     const double* wq = a.wqwr ? a.wqwr + (size_t)b * 8 : nullptr;
     if (lane < 36) {  // Qw = diag(wq) sym(Q) diag(wq)   (mpc_control_fuzzy.py:23-24)
         const int i = lane / 6, j = lane % 6;
         const double q = 0.5 * (a.Q[i * 6 + j] + a.Q[j * 6 + i]);
-        c.QW[lane] = wq ? q * wq[i] * wq[j] : q;
+        c.h(hQW + lane) = wq ? q * wq[i] * wq[j] : q;
     } else if (lane < 40) {
         const int e = lane - 36, i = e / 2, j = e % 2;
         const double r = 0.5 * (a.R[i * 2 + j] + a.R[j * 2 + i]);
-        c.RW[e] = wq ? r * wq[6 + i] * wq[6 + j] : r;
+        c.h(hRW + e) = wq ? r * wq[6 + i] * wq[6 + j] : r;
     } else if (lane < 46) {
-        c.XI[lane - 40] = a.x0[(size_t)b * 6 + (lane - 40)];
+        c.h(hXI + lane - 40) = a.x0[(size_t)b * 6 + (lane - 40)];
     }
     const double* xr = a.xref + (size_t)b * S * 6;
     for (int t = lane; t < S * 6; t += W) c.r(rXR + t % 6, t / 6) = xr[t];
@@ -695,15 +779,16 @@ __device__ __forceinline__ void phase_load(const Ctx& c, const TrackArgs& a, int
     __syncthreads();
 }
 
-// bound push (IPOPT bound_push / bound_frac = 1e-2), z_L = z_U = 1, y = 0
-__device__ __forceinline__ void phase_init(const Ctx& c) {
+// bound push (IPOPT bound_push / bound_frac = 1e-2), z_L = z_U = 1, y = 0, zero pad row
+template <int BM>
+__device__ __forceinline__ void phase_init(const Ctx<BM>& c) {
     const int N = c.N;
     for (int k = c.lane; k <= N; k += W) {
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
             double z = c.r(rX + v, k);
-            const double l = c.LB[v], u = c.UB[v];
+            const double l = c.lb(v), u = c.ub(v);
             if (c.hl(v) && c.hu(v)) {
                 const double pl = fmin(1e-2 * fmax(1.0, fabs(l)), 1e-2 * (u - l));
                 const double pu = fmin(1e-2 * fmax(1.0, fabs(u)), 1e-2 * (u - l));
@@ -719,37 +804,27 @@ __device__ __forceinline__ void phase_init(const Ctx& c) {
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) c.r(rY + i, k) = 0.0;
+        c.r(PAD, k) = 0.0;
     }
     __syncthreads();
 }
 
+template <int BM>
 __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
     const int N = a.N, S = N + 1;
-    Ctx c;
+    Ctx<BM> c;
     c.sm = sm;
-    c.QW = sm + SR * S;
-    c.RW = c.QW + 36;
-    c.PW0 = c.RW + 4;
-    c.PW1 = c.PW0 + 36;
-    c.PV0 = c.PW1 + 36;
-    c.PV1 = c.PV0 + 6;
-    c.PA = c.PV1 + 6;
-    c.WV = c.PA + 36;
-    c.XI = c.WV + 6;
-    c.LB = c.XI + 6;
-    c.UB = c.LB + 8;
     c.N = N;
     c.lane = threadIdx.x;
     c.dt = a.dt;
-    c.L1 = a.L1;
-    c.L2 = a.L2;
+    c.iL1 = 1.0 / a.L1;
+    c.iL2 = 1.0 / a.L2;
     c.Mh = a.Mh;
     c.mu = 0.1;
     c.tau = fmax(0.99, 1.0 - c.mu);
     c.nu = 1.0;
-
 #ifdef TT_STAMPS
     Stamps stamps;
     stamps.begin();
@@ -766,8 +841,8 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
     bool infeas = false;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        const double xi = c.XI[i];
-        if (!isfinite(xi) || (c.hl(i) && xi < c.LB[i]) || (c.hu(i) && xi > c.UB[i])) infeas = true;
+        const double xi = c.h(hXI + i);
+        if (!isfinite(xi) || (c.hl(i) && xi < c.lb(i)) || (c.hu(i) && xi > c.ub(i))) infeas = true;
     }
     int status = infeas ? 3 : 2, iter = 0;
     double E0 = INFINITY;
@@ -777,8 +852,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
         double dw_last = 0.0;
         int acc_count = 0;
         for (iter = 0;; ++iter) {
-            const Err e = phase_linearize(c);
-            __syncthreads();
+            const Lin e = phase_linearize(c);
             STAMP(PH_LIN);
             if (!isfinite(e.dinf) || !isfinite(e.pinf)) { status = 4; break; }
             const double sd = fmax(100.0, (e.sy + e.sz) / (double)(6 * (N + 1) + nb)) / 100.0;
@@ -796,11 +870,10 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             for (;;) {
                 const double Emu = fmax(fmax(e.dinf / sd, e.pinf), cmu / sc);
                 if (!(Emu <= 10.0 * c.mu && c.mu > a.tol / 10.0 * 1.0000001)) break;
-                c.mu = fmax(a.tol / 10.0, fmin(0.2 * c.mu, pow(c.mu, 1.5)));
+                c.mu = fmax(a.tol / 10.0, fmin(0.2 * c.mu, c.mu * sqrt(c.mu)));
                 c.tau = fmax(0.99, 1.0 - c.mu);
                 cmu = phase_compl_mu(c);
             }
-            phase_barrier(c);
             STAMP(PH_MU_BAR);
             // Newton step: Riccati with inertia correction
             double dw = 0.0;
@@ -819,10 +892,10 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             const StepInfo si = phase_step(c, rDX, true);
             STAMP(PH_STEP);
             if (c.nu < si.ymax + 1.0) c.nu = fmax(1.1 * si.ymax + 1.0, c.nu);
-            // l1-merit backtracking line search with one second-order correction
-            const double phi0 = phase_merit(c, 0.0, rDX, false);
-            STAMP(PH_MERIT);
-            const double D = si.Dg - c.nu * si.th0;
+            // l1-merit backtracking line search with one second-order correction; the merit value of
+            // the current point comes from the linearisation pass
+            const double phi0 = e.cost - c.mu * e.logs + c.nu * e.th;
+            const double D = si.Dg - c.nu * e.th;
             double alpha = si.ap, az = si.az;
             int accepted = si.rel < 1e-15 ? 1 : 0;
             bool soc = false;
@@ -836,15 +909,14 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
                     phase_forward(c, rCT, rDXS);
                     const double as = phase_soc_alpha(c);
                     const double phis = phase_merit(c, as, rDXS, false);
+                    STAMP(PH_SOC);
                     if (armijo(phis, phi0, alpha, D)) {
                         accepted = 2;
                         soc = true;
                         alpha = as;
                         az = phase_step(c, rDXS, false).az;  // y+ and dual step bound of the corrected step
-                        STAMP(PH_SOC);
                         break;
                     }
-                    STAMP(PH_SOC);
                 }
                 alpha *= 0.5;
             }
@@ -871,18 +943,42 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
     }
 }
 
-}  // namespace
+// bound pattern of the variables (bit v: finite lower, bit 8+v: finite upper), as the kernel sees it
+int bound_mask(const TrackArgs& a) {
+    int m = 0;
+    for (int v = 0; v < 8; ++v) {
+        const double l = v < 6 ? a.xlb[v] : a.ulb[v - 6], u = v < 6 ? a.xub[v] : a.uub[v - 6];
+        if (isfinite(l) && l > -1e19) m |= 1 << v;
+        if (isfinite(u) && u < 1e19) m |= 1 << (8 + v);
+    }
+    return m;
+}
 
-hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
+template <int BM>
+hipError_t launch(const TrackArgs& a, hipStream_t stream) {
     const int bytes = lds_bytes(a.N);
     static int configured = 0;
     if (bytes > 64 * 1024 && configured < bytes) {
-        hipError_t e = hipFuncSetAttribute((const void*)track_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipError_t e = hipFuncSetAttribute((const void*)track_kernel<BM>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
         configured = bytes;
     }
-    hipLaunchKernelGGL(track_kernel, dim3(a.B), dim3(W), bytes, stream, a);
+    hipLaunchKernelGGL(track_kernel<BM>, dim3(a.B), dim3(W), bytes, stream, a);
     return hipGetLastError();
+}
+
+}  // namespace
+
+// Specialised bound patterns: the reference MPC box (x, y free; theta, psi, phi, v, a, omega boxed:
+// simulation.py:411-414) and the OBCA box (theta free too: trajectory_animation.py:77-80).
+constexpr int kMaskMPC = 0xFCFC;
+constexpr int kMaskOBCA = 0xF8F8;
+
+hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
+    const int m = bound_mask(a);
+    if (m == kMaskMPC) return launch<kMaskMPC>(a, stream);
+    if (m == kMaskOBCA) return launch<kMaskOBCA>(a, stream);
+    return launch<-1>(a, stream);
 }
 
 }  // namespace ttmpc
