@@ -23,7 +23,7 @@
 //     the 7x7 affine-augmented blocks spread over the 64 lanes (see phase_riccati).
 //
 // LDS map (doubles).  Head (fixed offsets, immediate addressing): Qw(36) Rw(4) x_init(6) lb(8)
-// ub(8) pad(2).  Stage k row r at sm[kHead + k*157 + r]; the odd stride keeps lane-per-stage
+// ub(8) pad(2) dump(64: per-lane sink for branch-free predicated stores).  Stage k row r at sm[kHead + k*157 + r]; the odd stride keeps lane-per-stage
 // ds_read_b64 bank-conflict-free:
 //   0-5 X | 6-7 U | 8-13 Y (eq. multipliers, IPOPT sign) | 14-21 zL | 22-29 zU | 30-35 Xref
 //   36-37 Uref | 38-45 dX,dU | 46-51 Y+ | 52-60 dt*J (9 nnz) | 61-67 curvature (7 nnz)
@@ -46,7 +46,7 @@ constexpr int SR = kRowsPerStage;
 constexpr int HEAD = kHead;
 
 // head
-constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54;
+constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54, hDUMP = 64;  // dump: one slot per lane
 // rows
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
 constexpr int rSG = 68, rGF = 76, rCC = 84, rCT = 90, rK = 96, rKF = 108, rIH = 110, rPS = 113, rPV = 134;
@@ -390,13 +390,23 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// rows 0/1 of the wave after v_permlane16_swap(v, v): lo = row-0 value of the lane's column,
+// hi = row-1 value (for lanes of rows 0 and 1).  Pure VALU, no LDS.
+__device__ __forceinline__ void rows01(double v, double& r0, double& r1) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)(b & 0xffffffffll), (unsigned)(b & 0xffffffffll), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    r0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+    r1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
 // Per-lane operand slots of the Riccati tile (stage-relative LDS rows; PAD reads zero).
 struct RicMap {
     int aj0, aj1, cr0, cr1;    // A^[4s+q][cc] = one + row aj (stage k) - row cr (stage k+1)
     double one0, one1;
-    int hw0, hw1, hsg0, hsg1, hgr0, hgr1;  // H^[q+4r][cc] = q2 + w + sigma + g_x (+ dw on the diagonal)
+    int hw0, hw1, hsg0, hsg1, hgf0, hgf1, hdb0, hdb1;  // H^[q+4r][cc] = q2 + w + sigma + gF + mu dB (+ dw on diag)
     double q20, q21, dg0, dg1;
-    int ps0, ps1;             // store row of P^_k[q+4r][cc] (upper part), -1 = none
+    int ps0, ps1;             // store row of P^_k[q+4r][cc] (upper part), -1 = none (-> lane dump slot)
     __device__ __forceinline__ void init(int lane, const double* QW) {
         const int q = lane >> 4, cc = lane & 15;
 #pragma unroll
@@ -409,22 +419,27 @@ struct RicMap {
             const double q2 = (row < 6 && col < 6) ? 2.0 * QW[row * 6 + col] : 0.0;
             const int hw = (row < 6 && col < 6 && w_idx(row, col) >= 0) ? rWC + w_idx(row, col) : PAD;
             const int hsg = (row == col && row < 6) ? rSG + row : PAD;
-            const int hgr = (row < 6 && col == 6) ? row : (row == 6 && col < 6) ? col : -1;
+            const int gi = (row < 6 && col == 6) ? row : (row == 6 && col < 6) ? col : -1;
+            const int hgf = gi >= 0 ? rGF + gi : PAD, hdb = gi >= 0 ? rDB + gi : PAD;
             const double dg = (row == col && row < 6) ? 1.0 : 0.0;
             const int ps = (row <= col && col < 6) ? rPS + sym_idx(row, col) : (row < 6 && col == 6) ? rPV + row : -1;
-            if (s == 0) { aj0 = aj; cr0 = cr; one0 = one; q20 = q2; hw0 = hw; hsg0 = hsg; hgr0 = hgr; dg0 = dg; ps0 = ps; }
-            else        { aj1 = aj; cr1 = cr; one1 = one; q21 = q2; hw1 = hw; hsg1 = hsg; hgr1 = hgr; dg1 = dg; ps1 = ps; }
+            if (s == 0) { aj0 = aj; cr0 = cr; one0 = one; q20 = q2; hw0 = hw; hsg0 = hsg; hgf0 = hgf; hdb0 = hdb; dg0 = dg; ps0 = ps; }
+            else        { aj1 = aj; cr1 = cr; one1 = one; q21 = q2; hw1 = hw; hsg1 = hsg; hgf1 = hgf; hdb1 = hdb; dg1 = dg; ps1 = ps; }
         }
     }
 };
 
 template <int BM>
-__device__ __forceinline__ double hhat(const Ctx<BM>& c, int hw, int hsg, int hgr, double q2, double dg, int k,
+__device__ __forceinline__ double hhat(const Ctx<BM>& c, int hw, int hsg, int hgf, int hdb, double q2, double dg, int k,
                                        double dw, bool with_w) {
-    double v = q2 + c.r(hsg, k) + dg * dw;
-    if (hgr >= 0) v += c.gr(hgr, k);
+    double v = q2 + c.r(hsg, k) + dg * dw + c.r(hgf, k) + c.mu * c.r(hdb, k);
     if (with_w) v += c.r(hw, k);
     return v;
+}
+// branch-free predicated LDS store: invalid lanes write their own dump slot
+template <int BM>
+__device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
+    c.sm[valid ? HEAD + k * SR + row : hDUMP + c.lane] = v;
 }
 
 template <int BM>
@@ -435,20 +450,20 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const double dt = c.dt, dt2 = dt * dt;
     const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
     d4 P;
-    P[0] = hhat(c, m.hw0, m.hsg0, m.hgr0, m.q20, m.dg0, N, dw, false);
-    P[1] = hhat(c, m.hw1, m.hsg1, m.hgr1, m.q21, m.dg1, N, dw, false);
+    P[0] = hhat(c, m.hw0, m.hsg0, m.hgf0, m.hdb0, m.q20, m.dg0, N, dw, false);
+    P[1] = hhat(c, m.hw1, m.hsg1, m.hgf1, m.hdb1, m.q21, m.dg1, N, dw, false);
     P[2] = 0.0;
     P[3] = 0.0;
-    if (m.ps0 >= 0) c.r(m.ps0, N) = P[0];
-    if (m.ps1 >= 0) c.r(m.ps1, N) = P[1];
+    pstore(c, m.ps0 >= 0, m.ps0, N, P[0]);
+    pstore(c, m.ps1 >= 0, m.ps1, N, P[1]);
     bool pd = true;
     for (int k = N - 1; k >= 0; --k) {
         // operands (independent of P)
         const double a0 = m.one0 + c.r(m.aj0, k) - c.r(m.cr0, k + 1);
         const double a1 = m.one1 + c.r(m.aj1, k) - c.r(m.cr1, k + 1);
         d4 H;
-        H[0] = hhat(c, m.hw0, m.hsg0, m.hgr0, m.q20, m.dg0, k, dw, true);
-        H[1] = hhat(c, m.hw1, m.hsg1, m.hgr1, m.q21, m.dg1, k, dw, true);
+        H[0] = hhat(c, m.hw0, m.hsg0, m.hgf0, m.hdb0, m.q20, m.dg0, k, dw, true);
+        H[1] = hhat(c, m.hw1, m.hsg1, m.hgf1, m.hdb1, m.q21, m.dg1, k, dw, true);
         H[2] = 0.0;
         H[3] = 0.0;
         const double sgu0 = c.r(rSG + 6, k), sgu1 = c.r(rSG + 7, k), gu0 = c.gr(6, k), gu1 = c.gr(7, k);
@@ -465,24 +480,20 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         // F = A^' PA + H^
         d4 F = mfma(a0, PA[0], H);
         F = mfma(a1, PA[1], F);
-        // G rows: lanes q = 0 / 1 hold PA rows 4 / 5 in reg 1; swap to get the other row
-        const double own = PA[1], sw = __shfl_xor(own, 16, W);
-        const double pa5 = q == 0 ? sw : own, pa4 = q == 0 ? own : sw;
+        // G rows: lanes of rows q = 0 / 1 hold PA rows 4 / 5 in reg 1; exchange them across the rows
+        double pa4, pa5;
+        rows01(PA[1], pa4, pa5);
         const double g0 = dt * pa5 + (cc == 6 ? gu0 : 0.0);
         const double g1 = dt * pa4 + (cc == 6 ? gu1 : 0.0);
         const double m0 = i00 * g0 + i01 * g1, m1 = i01 * g0 + i11 * g1;
         const double aop = q == 0 ? -g0 : q == 1 ? -g1 : 0.0;
         const double bop = q == 0 ? m0 : q == 1 ? m1 : 0.0;
         P = mfma(aop, bop, F);
-        // K^ = -M, inverse input Hessian, P^_k
-        if (q < 2 && cc < 7) c.r(cc < 6 ? rK + 6 * q + cc : rKF + q, k) = -bop;
-        if (c.lane == 0) {
-            c.r(rIH, k) = i00;
-            c.r(rIH + 1, k) = i01;
-            c.r(rIH + 2, k) = i11;
-        }
-        if (m.ps0 >= 0) c.r(m.ps0, k) = P[0];
-        if (m.ps1 >= 0) c.r(m.ps1, k) = P[1];
+        // K^ = -M, inverse input Hessian, P^_k (branch-free stores)
+        pstore(c, q < 2 && cc < 7, cc < 6 ? rK + 6 * q + cc : rKF + q, k, -bop);
+        pstore(c, c.lane < 3, rIH + c.lane, k, c.lane == 0 ? i00 : c.lane == 1 ? i01 : i11);
+        pstore(c, m.ps0 >= 0, m.ps0, k, P[0]);
+        pstore(c, m.ps1 >= 0, m.ps1, k, P[1]);
     }
     __syncthreads();
     return pd;
@@ -520,13 +531,11 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int or
         d4 Y = {0.0, 0.0, 0.0, 0.0};
         Y = mfma(a0, X[0], Y);
         Y = mfma(a1, X[1], Y);
-        if (i == 0) {
-            // rows 0..5 -> dx_{k+1}; row 7 (q=3, reg 1) -> du0; row 8 (q=0, reg 2) -> du1
-            c.r(orow + q, k + 1) = Y[0];
-            if (q < 2) c.r(orow + q + 4, k + 1) = Y[1];
-            if (q == 3) c.r(orow + 6, k) = Y[1];
-            if (q == 0) c.r(orow + 7, k) = Y[2];
-        }
+        // rows 0..5 -> dx_{k+1}; row 7 (q=3, reg 1) -> du0; row 8 (q=0, reg 2) -> du1 (column-0 lanes)
+        pstore(c, i == 0, orow + q, k + 1, Y[0]);
+        pstore(c, i == 0 && q < 2, orow + q + 4, k + 1, Y[1]);
+        pstore(c, i == 0 && q == 3, orow + 6, k, Y[1]);
+        pstore(c, i == 0 && q == 0, orow + 7, k, Y[2]);
         X = Y;
     }
     __syncthreads();
