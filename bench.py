@@ -84,6 +84,24 @@ def cpu_baseline(cfg, B, N, seed, budget_s):
                       f"on {ncores} visible host cores; oracle/c/tt_oracle.c (IPOPT-restated IPM, banded LU)"}
 
 
+def rank_seed(rank):
+    """Each rank owns a disjoint seeded shard of instances (weak scaling, no data-path collective)."""
+    return 1000 * rank + 7
+
+
+def reduce_over_ranks(dist, wall, ok, B):
+    """Host-side (gloo) reduction of the per-rank timing: MAX wall clock, SUM of solved/instances.
+    Returns (wall_max, ok_total, B_total); identity when dist is None (single process)."""
+    if dist is None:
+        return wall, ok, B
+    t_local = torch.tensor([wall, float(ok), float(B)], dtype=torch.float64)
+    tmax = t_local.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tsum = t_local.clone()
+    dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+    return float(tmax[0]), int(tsum[1]), int(tsum[2])
+
+
 def p50_latency(solver, x0, xr, ur, reps=200):
     """Host wall clock around one B=1 solve incl. H2D/D2H (mirrors simulation.py:519-522)."""
     import numpy as np
@@ -106,7 +124,9 @@ def main():
     ap.add_argument("--horizon", type=int, default=0)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
     ap.add_argument("--no-latency", action="store_true")
-    ap.add_argument("--traffic-csv", default="", help="rocprofv3 --pmc counter CSV of this config (optional)")
+    ap.add_argument("--traffic-csv", default="",
+                    help="comma-separated rocprofv3 --pmc CSVs (FETCH_SIZE, WRITE_SIZE) of this config; "
+                         "default: the committed profiles/ pair when the config is the default C2")
     args = ap.parse_args()
 
     defaults = {"c2": (1024, 20), "c3": (8192, 40), "c5": (8192, 20)}
@@ -132,7 +152,7 @@ def main():
     dev = torch.device("cuda", local)
     solver = ttmpc.BatchSolver(N, to.DEFAULT_PARAMS, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB,
                                to.MPC_UUB, device=local)
-    x0, xr, ur = workload(args.config, B, N, seed=1000 * rank + 7)
+    x0, xr, ur = workload(args.config, B, N, seed=rank_seed(rank))
     t = {k: torch.from_numpy(v).to(dev) for k, v in (("x0", x0), ("xr", xr), ("ur", ur))}
     X = torch.empty((B, N + 1, 6), dtype=torch.float64, device=dev)
     U = torch.empty((B, N, 2), dtype=torch.float64, device=dev)
@@ -167,15 +187,7 @@ def main():
     iters = it.cpu().numpy()
     kkt = kk.cpu().numpy()
     ok = int(np.sum(status <= 1))
-    t_local = torch.tensor([wall, float(ok), float(B)], dtype=torch.float64)
-    if dist:
-        tmax = t_local.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t_local.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        wall_max, ok_total, B_total = float(tmax[0]), int(tsum[1]), int(tsum[2])
-    else:
-        wall_max, ok_total, B_total = wall, ok, B
+    wall_max, ok_total, B_total = reduce_over_ranks(dist, wall, ok, B)
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -186,8 +198,13 @@ def main():
     io = io_bytes_per_solve(N) * B
     traffic = None
     traffic_src = None
-    if args.traffic_csv and Path(args.traffic_csv).exists():
-        traffic, traffic_src = read_traffic(args.traffic_csv), args.traffic_csv
+    csvs = [p for p in args.traffic_csv.split(",") if p]
+    if not csvs and args.config == "c2" and B == 1024 and N == 20:
+        csvs = [str(REPO / "profiles" / "r01" / f) for f in ("r01_pmc_fetch_size.csv", "r01_pmc_write_size.csv")]
+    if csvs and all(Path(p).exists() for p in csvs):
+        traffic = read_traffic(csvs)
+        traffic_src = ", ".join(str(Path(p).relative_to(REPO)) if str(p).startswith(str(REPO)) else p for p in csvs) + \
+            " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of this bench config; HBM bytes per launch)"
     out = {
         "metric": "MPC solves/sec (N=20, nx=6, nu=2; BASELINE label says nx=5, the reference model has 6 states)"
         if N == 20 else f"MPC solves/sec (N={N}, nx=6, nu=2)",
@@ -222,31 +239,29 @@ def main():
         out["p50_latency_ms"] = round(p50, 4)
         out["p99_latency_ms"] = round(p99, 4)
     if args.cpu_budget > 0 and world == 1:
-        out["cpu_baseline"] = cpu_baseline(args.config, B, N, 1000 * rank + 7, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(args.config, B, N, rank_seed(rank), args.cpu_budget)
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
 
 
-def read_traffic(path):
-    """Average FETCH_SIZE+WRITE_SIZE (KB -> bytes) per dispatch of track_kernel from a rocprofv3
-    --pmc counter_collection CSV; FETCH_SIZE doubled per the gfx950 note in MI355X_MICROARCH.md."""
+def read_traffic(paths):
+    """HBM bytes per dispatch of track_kernel = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes), averaged over
+    the dispatches in rocprofv3 --pmc counter_collection CSVs (FETCH_SIZE and WRITE_SIZE need separate
+    passes on gfx950).  The x2 on FETCH_SIZE is the gfx950 correction of MI355X_MICROARCH.md; it was
+    re-calibrated for this kernel's 8-B/lane loads with tools/calib_fetch.hip (1 GiB read -> 524,299 KB
+    FETCH_SIZE; 1 GiB written -> 1,048,576 KB WRITE_SIZE; profiles/r01/calib/)."""
     import csv
-    fetch, write = [], []
-    with open(path) as fh:
-        for row in csv.DictReader(fh):
-            if "track_kernel" not in row.get("Kernel_Name", ""):
-                continue
-            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", "nan"))
-            if name == "FETCH_SIZE":
-                fetch.append(val)
-            elif name == "WRITE_SIZE":
-                write.append(val)
-    if not fetch and not write:
+    acc = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+    for path in paths:
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                if "track_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") in acc:
+                    acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    if not acc["FETCH_SIZE"] or not acc["WRITE_SIZE"]:
         return None
-    f = 2.0 * 1024 * (sum(fetch) / len(fetch) if fetch else 0.0)
-    w = 1024 * (sum(write) / len(write) if write else 0.0)
-    return round(f + w, 1)
+    return round(1024 * (2.0 * sum(acc["FETCH_SIZE"]) / len(acc["FETCH_SIZE"]) +
+                         sum(acc["WRITE_SIZE"]) / len(acc["WRITE_SIZE"])), 1)
 
 
 if __name__ == "__main__":
