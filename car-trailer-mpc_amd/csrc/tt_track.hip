@@ -30,6 +30,9 @@
 //   68-75 Sigma = zL/sL + zU/sU | 76-83 grad F | 84-89 c | 90-95 c(trial)/c_soc | 96-107 K
 //   108-109 k_ff | 110-112 inv(H_uu) | 113-133 P_k (upper) | 134-139 p_k | 140-147 dX,dU (soc)
 //   148-155 dB = 1/sU - 1/sL (barrier gradient = grad F + mu dB) | 156 zero pad
+// Rows reused with a second life (their first owner is dead at that point of the iteration):
+//   during the Riccati sweep  38-45 g = grad F + mu dB | 140-145 diag(Sigma) + diag(W) | 46-51 -c_{k+1}
+//   during the SOC            61-66 -c_soc_{k+1} (b^ of the SOC forward sweep)
 //
 // Bound pattern: template parameter BM (bit v = finite lower bound on variable v, bit 8+v = finite
 // upper bound; v = 0..5 states, 6..7 inputs) so the common patterns compile to straight-line code;
@@ -51,6 +54,10 @@ constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54, hDUMP = 64;  // d
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
 constexpr int rSG = 68, rGF = 76, rCC = 84, rCT = 90, rK = 96, rKF = 108, rIH = 110, rPS = 113, rPV = 134;
 constexpr int rDXS = 140, rDB = 148, PAD = 156;
+// Riccati operand rows, written by phase_ric_prep into rows that are dead during the backward sweep
+// (dX, dX_soc and Y+ are all produced after it): g = grad F + mu dB (8), diag(Sigma) + diag(W) (6),
+// b^ = -c_{k+1} stored at stage k (6).
+constexpr int rHG = rDX, rHD = rDXS, rBH = rYP;
 
 // ---- wave reductions: DPP inside each 16-lane row (xor 1, xor 2, half-mirror, mirror), then the four
 // row results by v_readlane into SGPRs.  No LDS; the result is wave-uniform and bitwise identical in
@@ -400,12 +407,13 @@ __device__ __forceinline__ void rows01(double v, double& r0, double& r1) {
     r1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
 }
 
-// Per-lane operand slots of the Riccati tile (stage-relative LDS rows; PAD reads zero).
+// Per-lane operand slots of the Riccati tile (stage-relative LDS rows; PAD reads zero).  After
+// phase_ric_prep every tile entry is a constant plus at most ONE LDS value:
+//   A^[4s+q][cc] = one + row as (dt*J nonzero, or b^ = -c_{k+1} in column 6)
+//   H^[q+4r][cc] = 2 Qw + dg*dw + row hs (diag Sigma+W, off-diagonal W, or g in row/column 6)
 struct RicMap {
-    int aj0, aj1, cr0, cr1;    // A^[4s+q][cc] = one + row aj (stage k) - row cr (stage k+1)
-    double one0, one1;
-    int hw0, hw1, hsg0, hsg1, hgf0, hgf1, hdb0, hdb1;  // H^[q+4r][cc] = q2 + w + sigma + gF + mu dB (+ dw on diag)
-    double q20, q21, dg0, dg1;
+    int as0, as1, hs0, hs1;
+    double one0, one1, q20, q21, dg0, dg1;
     int ps0, ps1;             // store row of P^_k[q+4r][cc] (upper part), -1 = none (-> lane dump slot)
     __device__ __forceinline__ void init(int lane, const double* QW) {
         const int q = lane >> 4, cc = lane & 15;
@@ -413,35 +421,77 @@ struct RicMap {
         for (int s = 0; s < 2; ++s) {
             const int kap = 4 * s + q, n = cc;
             const double one = (kap == n && kap <= 6) ? 1.0 : 0.0;
-            const int aj = (kap < 6 && n < 6 && d_idx(kap, n) >= 0) ? rAJ + d_idx(kap, n) : PAD;
-            const int cr = (kap < 6 && n == 6) ? rCC + kap : PAD;
+            const int as = (kap < 6 && n < 6 && d_idx(kap, n) >= 0) ? rAJ + d_idx(kap, n)
+                         : (kap < 6 && n == 6) ? rBH + kap : PAD;
             const int row = q + 4 * s, col = cc;  // s doubles as the accumulator register r
             const double q2 = (row < 6 && col < 6) ? 2.0 * QW[row * 6 + col] : 0.0;
-            const int hw = (row < 6 && col < 6 && w_idx(row, col) >= 0) ? rWC + w_idx(row, col) : PAD;
-            const int hsg = (row == col && row < 6) ? rSG + row : PAD;
             const int gi = (row < 6 && col == 6) ? row : (row == 6 && col < 6) ? col : -1;
-            const int hgf = gi >= 0 ? rGF + gi : PAD, hdb = gi >= 0 ? rDB + gi : PAD;
+            const int hs = (row == col && row < 6) ? rHD + row
+                         : (row < 6 && col < 6 && w_idx(row, col) >= 0) ? rWC + w_idx(row, col)
+                         : gi >= 0 ? rHG + gi : PAD;
             const double dg = (row == col && row < 6) ? 1.0 : 0.0;
             const int ps = (row <= col && col < 6) ? rPS + sym_idx(row, col) : (row < 6 && col == 6) ? rPV + row : -1;
-            if (s == 0) { aj0 = aj; cr0 = cr; one0 = one; q20 = q2; hw0 = hw; hsg0 = hsg; hgf0 = hgf; hdb0 = hdb; dg0 = dg; ps0 = ps; }
-            else        { aj1 = aj; cr1 = cr; one1 = one; q21 = q2; hw1 = hw; hsg1 = hsg; hgf1 = hgf; hdb1 = hdb; dg1 = dg; ps1 = ps; }
+            if (s == 0) { as0 = as; hs0 = hs; one0 = one; q20 = q2; dg0 = dg; ps0 = ps; }
+            else        { as1 = as; hs1 = hs; one1 = one; q21 = q2; dg1 = dg; ps1 = ps; }
         }
     }
 };
 
+// stage-parallel: fold the barrier, curvature and constraint terms into the Riccati operand rows
 template <int BM>
-__device__ __forceinline__ double hhat(const Ctx<BM>& c, int hw, int hsg, int hgf, int hdb, double q2, double dg, int k,
-                                       double dw, bool with_w) {
-    double v = q2 + c.r(hsg, k) + dg * dw + c.r(hgf, k) + c.mu * c.r(hdb, k);
-    if (with_w) v += c.r(hw, k);
-    return v;
+__device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
+    const int N = c.N;
+    for (int k = c.lane; k <= N; k += W) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            if (v >= 6 && k == N) break;
+            c.r(rHG + v, k) = c.gr(v, k);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const int wi = w_idx(i, i);
+            double d = c.r(rSG + i, k);
+            if (wi >= 0 && k < N) d += c.r(rWC + wi, k);
+            c.r(rHD + i, k) = d;
+        }
+        if (k < N) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) c.r(rBH + i, k) = -c.r(rCC + i, k + 1);
+        } else {  // terminal stage: no dynamics, so no curvature
+#pragma unroll
+            for (int i = 0; i < 7; ++i) c.r(rWC + i, k) = 0.0;
+        }
+    }
+    __syncthreads();
 }
+
 // branch-free predicated LDS store: invalid lanes write their own dump slot
 template <int BM>
 __device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
     c.sm[valid ? HEAD + k * SR + row : hDUMP + c.lane] = v;
 }
 
+// Stage operands of the Riccati tile: everything that does not depend on P^_{k+1}.  Fetched one
+// stage ahead (software pipelining) so the LDS latency hides behind the previous stage's MFMA chain.
+struct RicOps {
+    double a0, a1, h0, h1, sgu0, sgu1, gu0, gu1;
+};
+template <int BM>
+__device__ __forceinline__ RicOps ric_ops(const Ctx<BM>& c, const RicMap& m, int k, double dw) {
+    RicOps o;
+    o.a0 = m.one0 + c.r(m.as0, k);
+    o.a1 = m.one1 + c.r(m.as1, k);
+    o.h0 = m.q20 + m.dg0 * dw + c.r(m.hs0, k);
+    o.h1 = m.q21 + m.dg1 * dw + c.r(m.hs1, k);
+    o.sgu0 = c.r(rSG + 6, k);
+    o.sgu1 = c.r(rSG + 7, k);
+    o.gu0 = c.r(rHG + 6, k);
+    o.gu1 = c.r(rHG + 7, k);
+    return o;
+}
+
+// Backward Riccati sweep (operand rows from phase_ric_prep).  Returns false when a reduced input
+// Hessian is not positive definite (the caller raises the primal regularisation dw and retries).
 template <int BM>
 __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const int N = c.N, q = c.lane >> 4, cc = c.lane & 15;
@@ -450,41 +500,38 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const double dt = c.dt, dt2 = dt * dt;
     const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
     d4 P;
-    P[0] = hhat(c, m.hw0, m.hsg0, m.hgf0, m.hdb0, m.q20, m.dg0, N, dw, false);
-    P[1] = hhat(c, m.hw1, m.hsg1, m.hgf1, m.hdb1, m.q21, m.dg1, N, dw, false);
+    P[0] = m.q20 + m.dg0 * dw + c.r(m.hs0, N);
+    P[1] = m.q21 + m.dg1 * dw + c.r(m.hs1, N);
     P[2] = 0.0;
     P[3] = 0.0;
     pstore(c, m.ps0 >= 0, m.ps0, N, P[0]);
     pstore(c, m.ps1 >= 0, m.ps1, N, P[1]);
+    // inertia flag accumulated without branching: a failed stage only poisons the (discarded) factors
     bool pd = true;
+    RicOps nxt = ric_ops(c, m, N - 1, dw);
     for (int k = N - 1; k >= 0; --k) {
-        // operands (independent of P)
-        const double a0 = m.one0 + c.r(m.aj0, k) - c.r(m.cr0, k + 1);
-        const double a1 = m.one1 + c.r(m.aj1, k) - c.r(m.cr1, k + 1);
-        d4 H;
-        H[0] = hhat(c, m.hw0, m.hsg0, m.hgf0, m.hdb0, m.q20, m.dg0, k, dw, true);
-        H[1] = hhat(c, m.hw1, m.hsg1, m.hgf1, m.hdb1, m.q21, m.dg1, k, dw, true);
-        H[2] = 0.0;
-        H[3] = 0.0;
-        const double sgu0 = c.r(rSG + 6, k), sgu1 = c.r(rSG + 7, k), gu0 = c.gr(6, k), gu1 = c.gr(7, k);
+        const RicOps o = nxt;
+        nxt = ric_ops(c, m, k > 0 ? k - 1 : 0, dw);
         // reduced input Hessian from P_{k+1}: P[5][5] lane 21, P[5][4] lane 20, P[4][4] lane 4 (reg 1)
         const double p55 = readlane_d(P[1], 21), p54 = readlane_d(P[1], 20), p44 = readlane_d(P[1], 4);
-        const double h00 = r00 + sgu0 + dw + dt2 * p55, h01 = r01 + dt2 * p54, h11 = r11 + sgu1 + dw + dt2 * p44;
+        const double h00 = r00 + o.sgu0 + dw + dt2 * p55, h01 = r01 + dt2 * p54, h11 = r11 + o.sgu1 + dw + dt2 * p44;
         const double det = h00 * h11 - h01 * h01;
-        if (!(h00 > 0.0 && h11 > 0.0 && det > 1e-13 * h00 * h11)) { pd = false; break; }
+        pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
         const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
         // PA = P^ A^
         d4 PA = {0.0, 0.0, 0.0, 0.0};
-        PA = mfma(P[0], a0, PA);
-        PA = mfma(P[1], a1, PA);
+        PA = mfma(P[0], o.a0, PA);
+        PA = mfma(P[1], o.a1, PA);
         // F = A^' PA + H^
-        d4 F = mfma(a0, PA[0], H);
-        F = mfma(a1, PA[1], F);
+        d4 H = {o.h0, o.h1, 0.0, 0.0};
+        d4 F = mfma(o.a0, PA[0], H);
+        F = mfma(o.a1, PA[1], F);
+        __builtin_amdgcn_sched_barrier(0);  // issue F before the G/M lane work so the two overlap
         // G rows: lanes of rows q = 0 / 1 hold PA rows 4 / 5 in reg 1; exchange them across the rows
         double pa4, pa5;
         rows01(PA[1], pa4, pa5);
-        const double g0 = dt * pa5 + (cc == 6 ? gu0 : 0.0);
-        const double g1 = dt * pa4 + (cc == 6 ? gu1 : 0.0);
+        const double g0 = dt * pa5 + (cc == 6 ? o.gu0 : 0.0);
+        const double g1 = dt * pa4 + (cc == 6 ? o.gu1 : 0.0);
         const double m0 = i00 * g0 + i01 * g1, m1 = i01 * g0 + i11 * g1;
         const double aop = q == 0 ? -g0 : q == 1 ? -g1 : 0.0;
         const double bop = q == 0 ? m0 : q == 1 ? m1 : 0.0;
@@ -502,18 +549,18 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
 // ============ forward sweep on the matrix cores: [x^_{k+1}; du_k] = [Phi_k; K^_k] x^_k ============
 // Phi = A^ + B^ K^ (rows 0..6), rows 7,8 = K^; x^ stays in accumulator column 0, which is exactly
 // the B-operand layout of the next step (2 MFMAs per stage, nothing moves between lanes).
+// crow: constraint residual rows (x^_0 = [-c_0; 1]); bhrow: b^ = -c_{k+1} stored at stage k.
 template <int BM>
-__device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int orow) {
+__device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bhrow, int orow) {
     const int N = c.N, q = c.lane >> 4, i = c.lane & 15;
-    // operand slots: Phi[i][kappa], kappa = 4s + q
-    int faj[2], fcr[2], fk[2];
+    // operand slots: Phi[i][kappa] = fone + row fas + fkc * row fk, kappa = 4s + q
+    int fas[2], fk[2];
     double fone[2], fkc[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
         const int kap = 4 * s + q;
         fone[s] = (i == kap && i <= 6) ? 1.0 : 0.0;
-        faj[s] = (i < 6 && kap < 6 && d_idx(i, kap) >= 0) ? rAJ + d_idx(i, kap) : PAD;
-        fcr[s] = (i < 6 && kap == 6) ? crow + i : PAD;
+        fas[s] = (i < 6 && kap < 6 && d_idx(i, kap) >= 0) ? rAJ + d_idx(i, kap) : (i < 6 && kap == 6) ? bhrow + i : PAD;
         const int u = (i == 5 || i == 7) ? 0 : (i == 4 || i == 8) ? 1 : -1;
         fk[s] = (u >= 0 && kap < 6) ? rK + 6 * u + kap : (u >= 0 && kap == 6) ? rKF + u : PAD;
         fkc[s] = (u >= 0 && kap <= 6) ? (i < 6 ? c.dt : 1.0) : 0.0;
@@ -525,9 +572,15 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int or
         c.r(orow + q, 0) = X[0];
         if (q < 2) c.r(orow + q + 4, 0) = X[1];
     }
+    auto ops = [&](int k, double& a0, double& a1) {
+        a0 = fone[0] + c.r(fas[0], k) + fkc[0] * c.r(fk[0], k);
+        a1 = fone[1] + c.r(fas[1], k) + fkc[1] * c.r(fk[1], k);
+    };
+    double n0, n1;  // operands of the next stage, fetched one stage ahead
+    ops(0, n0, n1);
     for (int k = 0; k < N; ++k) {
-        const double a0 = fone[0] + c.r(faj[0], k) - c.r(fcr[0], k + 1) + fkc[0] * c.r(fk[0], k);
-        const double a1 = fone[1] + c.r(faj[1], k) - c.r(fcr[1], k + 1) + fkc[1] * c.r(fk[1], k);
+        const double a0 = n0, a1 = n1;
+        ops(k + 1 < N ? k + 1 : k, n0, n1);
         d4 Y = {0.0, 0.0, 0.0, 0.0};
         Y = mfma(a0, X[0], Y);
         Y = mfma(a1, X[1], Y);
@@ -724,7 +777,11 @@ template <int BM>
 __device__ __forceinline__ void phase_soc_rhs(const Ctx<BM>& c, double alpha) {
     for (int k = c.lane; k <= c.N; k += W) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) c.r(rCT + i, k) = alpha * c.r(rCC + i, k) + c.r(rCT + i, k);
+        for (int i = 0; i < 6; ++i) {
+            const double cs = alpha * c.r(rCC + i, k) + c.r(rCT + i, k);
+            c.r(rCT + i, k) = cs;
+            if (k > 0) c.r(rWC + i, k - 1) = -cs;  // b^ of the SOC forward sweep (rWC is dead after Riccati)
+        }
     }
     __syncthreads();
 }
@@ -887,6 +944,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             // Newton step: Riccati with inertia correction
             double dw = 0.0;
             bool ok = false;
+            phase_ric_prep(c);
             for (int attempt = 0; attempt < 30; ++attempt) {
                 if (phase_riccati(c, dw)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0))
@@ -896,7 +954,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             if (!ok) { status = 4; break; }
             if (dw > 0.0) dw_last = dw;
             STAMP(PH_RIC);
-            phase_forward(c, rCC, rDX);
+            phase_forward(c, rCC, rBH, rDX);
             STAMP(PH_FWD);
             const StepInfo si = phase_step(c, rDX, true);
             STAMP(PH_STEP);
@@ -915,7 +973,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
                 if (ls == 0 && isfinite(phit)) {
                     phase_soc_rhs(c, alpha);
                     phase_soc_backward(c);
-                    phase_forward(c, rCT, rDXS);
+                    phase_forward(c, rCT, rWC, rDXS);
                     const double as = phase_soc_alpha(c);
                     const double phis = phase_merit(c, as, rDXS, false);
                     STAMP(PH_SOC);
