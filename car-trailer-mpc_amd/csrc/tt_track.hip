@@ -391,6 +391,8 @@ __device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
 // its accumulator registers ARE its A- and B-operand registers: P^ never leaves VGPRs.  A^ as the
 // B operand of step 1 and A^' as the A operand of step 2 are the same lane value.  G needs rows 4
 // and 5 of PA in each lane: one lane swap (xor 16).  Five MFMAs per stage, no barrier.
+// (Splitting each K = 8 product into two independent MFMAs summed on the VALU measured slower, and it
+// makes the compiler overwrite the sources of a queued MFMA right after issue: kept as srcC chains.)
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
