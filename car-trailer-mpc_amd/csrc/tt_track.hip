@@ -50,6 +50,7 @@ constexpr int HEAD = kHead;
 
 // head
 constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54, hDUMP = 64;  // dump: one slot per lane
+// (128..255: the P and transposed-PA tiles of the Riccati sweep, see phase_riccati)
 // rows
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
 constexpr int rSG = 68, rGF = 76, rCC = 84, rCT = 90, rK = 96, rKF = 108, rIH = 110, rPS = 113, rPV = 134;
@@ -379,65 +380,24 @@ __device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
     return wmax(cm);
 }
 
-// ============ Riccati on the FP64 matrix cores (v_mfma_f64_16x16x4_f64) ============
+// ============ Riccati recursion, entry-parallel on the VALU ============
 // Affine augmentation x^ = [dx; 1] turns the value function, dynamics and feed-forward into 7x7
-// matrices, padded into one 16x16 f64 tile:
-//   A^ = [[A, b],[0, 1]] (b = -c_{k+1}),  H^ = [[H_xx, g_x],[g_x', 0]],  S^ = [0, g_u],  B^ = [B; 0]
-//   PA = P^ A^  (2 MFMA, K = 8),  F = A^' PA + H^  (2 MFMA, C = H^),
-//   G = B^' PA + S^ = dt * rows (5,4) of PA + S^,  H_uu = 2Rw + Sig_u + dt^2 P[{5,4},{5,4}],
-//   P^_k = F - G' (H_uu^-1 G)  (1 MFMA, K = 2 of 4),  K^ = [K, k_ff] = -H_uu^-1 G.
-// Layouts (lane l, c = l & 15, q = l >> 4): accumulator reg r = element (q + 4r, c); A operand of
-// k-step s = element (c, 4s + q); B operand of k-step s = element (4s + q, c).  P^ is symmetric, so
-// its accumulator registers ARE its A- and B-operand registers: P^ never leaves VGPRs.  A^ as the
-// B operand of step 1 and A^' as the A operand of step 2 are the same lane value.  G needs rows 4
-// and 5 of PA in each lane: one lane swap (xor 16).  Five MFMAs per stage, no barrier.
-// (Splitting each K = 8 product into two independent MFMAs summed on the VALU measured slower, and it
-// makes the compiler overwrite the sources of a queued MFMA right after issue: kept as srcC chains.)
-typedef double d4 __attribute__((ext_vector_type(4)));
+// blocks: A^ = [[A, b],[0, 1]] = I + D (b = -c_{k+1}), H^ = [[H_xx, g_x],[g_x', 0]], B^ = [B; 0]
+// (B[5][0] = B[4][1] = dt), S^ = [0, g_u].  Per stage (k = N-1 .. 0):
+//   PA = P^ A^ = P^ + P^ D,   F = A^' PA + H^ = PA + D' PA + H^,   G = B^' PA + S^ (rows 5, 4 of PA),
+//   H_uu = 2Rw + Sig_u + dt^2 P[{5,4},{5,4}],  M = H_uu^-1 G,  P^_k = F - G' M,  K^ = -M.
+// Lane 8i + j owns entry (i, j) of every 8x8 (padded) block.  The only cross-lane traffic is row i of
+// P^ (read from the P tile in LDS, written by the previous stage) and column j of PA (written
+// transposed into the PA tile, so both are contiguous b128 reads).  The 16x16 f64 MFMA was measured
+// at ~185 cycles per srcC-chained link on gfx950 and runs no faster than the VALU for f64, so the
+// whole recursion stays on the VALU with ~300 cycles of dependent latency per stage.
+constexpr int hPF = 128, hPT = 192;  // P tile [8i + j] and transposed PA tile [8j + i] (64 doubles each)
 
-__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
-    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+// branch-free predicated LDS store: invalid lanes write their own dump slot
+template <int BM>
+__device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
+    c.sm[valid ? HEAD + k * SR + row : hDUMP + c.lane] = v;
 }
-
-// rows 0/1 of the wave after v_permlane16_swap(v, v): lo = row-0 value of the lane's column,
-// hi = row-1 value (for lanes of rows 0 and 1).  Pure VALU, no LDS.
-__device__ __forceinline__ void rows01(double v, double& r0, double& r1) {
-    const long long b = __double_as_longlong(v);
-    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)(b & 0xffffffffll), (unsigned)(b & 0xffffffffll), false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-    r0 = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
-    r1 = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
-}
-
-// Per-lane operand slots of the Riccati tile (stage-relative LDS rows; PAD reads zero).  After
-// phase_ric_prep every tile entry is a constant plus at most ONE LDS value:
-//   A^[4s+q][cc] = one + row as (dt*J nonzero, or b^ = -c_{k+1} in column 6)
-//   H^[q+4r][cc] = 2 Qw + dg*dw + row hs (diag Sigma+W, off-diagonal W, or g in row/column 6)
-struct RicMap {
-    int as0, as1, hs0, hs1;
-    double one0, one1, q20, q21, dg0, dg1;
-    int ps0, ps1;             // store row of P^_k[q+4r][cc] (upper part), -1 = none (-> lane dump slot)
-    __device__ __forceinline__ void init(int lane, const double* QW) {
-        const int q = lane >> 4, cc = lane & 15;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int kap = 4 * s + q, n = cc;
-            const double one = (kap == n && kap <= 6) ? 1.0 : 0.0;
-            const int as = (kap < 6 && n < 6 && d_idx(kap, n) >= 0) ? rAJ + d_idx(kap, n)
-                         : (kap < 6 && n == 6) ? rBH + kap : PAD;
-            const int row = q + 4 * s, col = cc;  // s doubles as the accumulator register r
-            const double q2 = (row < 6 && col < 6) ? 2.0 * QW[row * 6 + col] : 0.0;
-            const int gi = (row < 6 && col == 6) ? row : (row == 6 && col < 6) ? col : -1;
-            const int hs = (row == col && row < 6) ? rHD + row
-                         : (row < 6 && col < 6 && w_idx(row, col) >= 0) ? rWC + w_idx(row, col)
-                         : gi >= 0 ? rHG + gi : PAD;
-            const double dg = (row == col && row < 6) ? 1.0 : 0.0;
-            const int ps = (row <= col && col < 6) ? rPS + sym_idx(row, col) : (row < 6 && col == 6) ? rPV + row : -1;
-            if (s == 0) { as0 = as; hs0 = hs; one0 = one; q20 = q2; dg0 = dg; ps0 = ps; }
-            else        { as1 = as; hs1 = hs; one1 = one; q21 = q2; dg1 = dg; ps1 = ps; }
-        }
-    }
-};
 
 // stage-parallel: fold the barrier, curvature and constraint terms into the Riccati operand rows
 template <int BM>
@@ -467,24 +427,42 @@ __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
     __syncthreads();
 }
 
-// branch-free predicated LDS store: invalid lanes write their own dump slot
-template <int BM>
-__device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
-    c.sm[valid ? HEAD + k * SR + row : hDUMP + c.lane] = v;
-}
+// Per-lane slots of entry (i, j): D[m][j] (m = 0..5) for PA, D[l][i] for F, H^[i][j], store rows.
+struct EpMap {
+    int dj[6], di[6];
+    int hs, ps;
+    double q2, dg;
+    __device__ __forceinline__ static int dslot(int m, int n) {  // row of D[m][n] (PAD = 0)
+        return (m < 6 && n < 6 && d_idx(m, n) >= 0) ? rAJ + d_idx(m, n) : (m < 6 && n == 6) ? rBH + m : PAD;
+    }
+    __device__ __forceinline__ void init(int i, int j, const double* QW) {
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            dj[m] = dslot(m, j);
+            di[m] = dslot(m, i);
+        }
+        const int gi = (i < 6 && j == 6) ? i : (i == 6 && j < 6) ? j : -1;
+        hs = (i == j && i < 6) ? rHD + i : (i < 6 && j < 6 && w_idx(i, j) >= 0) ? rWC + w_idx(i, j)
+           : gi >= 0 ? rHG + gi : PAD;
+        q2 = (i < 6 && j < 6) ? 2.0 * QW[i * 6 + j] : 0.0;
+        dg = (i == j && i < 6) ? 1.0 : 0.0;
+        ps = (i <= j && j < 6) ? rPS + sym_idx(i, j) : (i < 6 && j == 6) ? rPV + i : -1;
+    }
+};
 
-// Stage operands of the Riccati tile: everything that does not depend on P^_{k+1}.  Fetched one
-// stage ahead (software pipelining) so the LDS latency hides behind the previous stage's MFMA chain.
-struct RicOps {
-    double a0, a1, h0, h1, sgu0, sgu1, gu0, gu1;
+// stage operands (independent of P^_{k+1}): fetched one stage ahead so LDS latency hides
+struct EpOps {
+    double dj[6], di[6], h, sgu0, sgu1, gu0, gu1;
 };
 template <int BM>
-__device__ __forceinline__ RicOps ric_ops(const Ctx<BM>& c, const RicMap& m, int k, double dw) {
-    RicOps o;
-    o.a0 = m.one0 + c.r(m.as0, k);
-    o.a1 = m.one1 + c.r(m.as1, k);
-    o.h0 = m.q20 + m.dg0 * dw + c.r(m.hs0, k);
-    o.h1 = m.q21 + m.dg1 * dw + c.r(m.hs1, k);
+__device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k, double dw) {
+    EpOps o;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        o.dj[t] = c.r(m.dj[t], k);
+        o.di[t] = c.r(m.di[t], k);
+    }
+    o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
     o.sgu0 = c.r(rSG + 6, k);
     o.sgu1 = c.r(rSG + 7, k);
     o.gu0 = c.r(rHG + 6, k);
@@ -492,106 +470,121 @@ __device__ __forceinline__ RicOps ric_ops(const Ctx<BM>& c, const RicMap& m, int
     return o;
 }
 
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
 // Backward Riccati sweep (operand rows from phase_ric_prep).  Returns false when a reduced input
 // Hessian is not positive definite (the caller raises the primal regularisation dw and retries).
 template <int BM>
 __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
-    const int N = c.N, q = c.lane >> 4, cc = c.lane & 15;
-    RicMap m;
-    m.init(c.lane, c.sm + hQW);
+    const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
+    EpMap m;
+    m.init(i, j, c.sm + hQW);
     const double dt = c.dt, dt2 = dt * dt;
     const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
-    d4 P;
-    P[0] = m.q20 + m.dg0 * dw + c.r(m.hs0, N);
-    P[1] = m.q21 + m.dg1 * dw + c.r(m.hs1, N);
-    P[2] = 0.0;
-    P[3] = 0.0;
-    pstore(c, m.ps0 >= 0, m.ps0, N, P[0]);
-    pstore(c, m.ps1 >= 0, m.ps1, N, P[1]);
+    double* PF = c.sm + hPF;
+    double* PT = c.sm + hPT;
+    // terminal P^_N = H^_N (no dynamics): padded lanes hold exact zeros
+    double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
+    PF[c.lane] = Pij;
+    asm volatile("" ::: "memory");
+    pstore(c, m.ps >= 0, m.ps, N, Pij);
     // inertia flag accumulated without branching: a failed stage only poisons the (discarded) factors
     bool pd = true;
-    RicOps nxt = ric_ops(c, m, N - 1, dw);
-    for (int k = N - 1; k >= 0; --k) {
-        const RicOps o = nxt;
-        nxt = ric_ops(c, m, k > 0 ? k - 1 : 0, dw);
-        // reduced input Hessian from P_{k+1}: P[5][5] lane 21, P[5][4] lane 20, P[4][4] lane 4 (reg 1)
-        const double p55 = readlane_d(P[1], 21), p54 = readlane_d(P[1], 20), p44 = readlane_d(P[1], 4);
-        const double h00 = r00 + o.sgu0 + dw + dt2 * p55, h01 = r01 + dt2 * p54, h11 = r11 + o.sgu1 + dw + dt2 * p44;
+    // one stage; `o` = this stage's operands, `nx` receives stage kn's (prefetch, issued after the
+    // P-tile reads so that waiting for the tile never waits for the prefetch)
+    auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
+        // row i of P^_{k+1} and the reduced input Hessian entries (uniform)
+        const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
+        const double2 p5 = ld2(PF + 44);  // P[5][4], P[5][5]
+        const double p44 = PF[36];
+        __builtin_amdgcn_sched_barrier(0);
+        nx = ep_ops(c, m, kn, dw);
+        const double h00 = r00 + o.sgu0 + dw + dt2 * p5.y, h01 = r01 + dt2 * p5.x, h11 = r11 + o.sgu1 + dw + dt2 * p44;
         const double det = h00 * h11 - h01 * h01;
         pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
         const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
-        // PA = P^ A^
-        d4 PA = {0.0, 0.0, 0.0, 0.0};
-        PA = mfma(P[0], o.a0, PA);
-        PA = mfma(P[1], o.a1, PA);
-        // F = A^' PA + H^
-        d4 H = {o.h0, o.h1, 0.0, 0.0};
-        d4 F = mfma(o.a0, PA[0], H);
-        F = mfma(o.a1, PA[1], F);
-        __builtin_amdgcn_sched_barrier(0);  // issue F before the G/M lane work so the two overlap
-        // G rows: lanes of rows q = 0 / 1 hold PA rows 4 / 5 in reg 1; exchange them across the rows
-        double pa4, pa5;
-        rows01(PA[1], pa4, pa5);
-        const double g0 = dt * pa5 + (cc == 6 ? o.gu0 : 0.0);
-        const double g1 = dt * pa4 + (cc == 6 ? o.gu1 : 0.0);
-        const double m0 = i00 * g0 + i01 * g1, m1 = i01 * g0 + i11 * g1;
-        const double aop = q == 0 ? -g0 : q == 1 ? -g1 : 0.0;
-        const double bop = q == 0 ? m0 : q == 1 ? m1 : 0.0;
-        P = mfma(aop, bop, F);
-        // K^ = -M, inverse input Hessian, P^_k (branch-free stores)
-        pstore(c, q < 2 && cc < 7, cc < 6 ? rK + 6 * q + cc : rKF + q, k, -bop);
+        // PA[i][j] = P[i][j] + sum_m P[i][m] D[m][j]
+        double pa = fma(r01v.x, o.dj[0], Pij), pb = r01v.y * o.dj[1];
+        pa = fma(r23v.x, o.dj[2], pa);
+        pb = fma(r23v.y, o.dj[3], pb);
+        pa = fma(r45v.x, o.dj[4], pa);
+        pb = fma(r45v.y, o.dj[5], pb);
+        const double PAij = pa + pb;
+        PT[8 * j + i] = PAij;
+        asm volatile("" ::: "memory");  // the tile is read by other lanes: keep program order
+        // column j of PA (rows 0..5; rows 4, 5 also give G[.][j]) and G[.][i]
+        const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
+        const double2 gi = ld2(PT + 8 * i + 4);  // PA[4][i], PA[5][i]
+        // F[i][j] = PA[i][j] + sum_l D[l][i] PA[l][j] + H^[i][j]
+        double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
+        fa = fma(o.di[2], c23.x, fa);
+        fb = fma(o.di[3], c23.y, fb);
+        fa = fma(o.di[4], c45.x, fa);
+        fb = fma(o.di[5], c45.y, fb);
+        const double F = fa + fb;
+        // G[0][.] = dt PA[5][.] + S, G[1][.] = dt PA[4][.] + S;  M = H_uu^-1 G;  P^_k = F - G' M
+        const double g0j = fma(dt, c45.y, j == 6 ? o.gu0 : 0.0), g1j = fma(dt, c45.x, j == 6 ? o.gu1 : 0.0);
+        const double g0i = fma(dt, gi.y, i == 6 ? o.gu0 : 0.0), g1i = fma(dt, gi.x, i == 6 ? o.gu1 : 0.0);
+        const double m0 = fma(i00, g0j, i01 * g1j), m1 = fma(i01, g0j, i11 * g1j);
+        Pij = F - fma(g0i, m0, g1i * m1);
+        PF[c.lane] = Pij;
+        asm volatile("" ::: "memory");
+        // factorisation rows for the forward sweep, the step and the SOC (branch-free stores)
+        pstore(c, i < 2 && j < 7, j < 6 ? rK + 6 * i + j : rKF + i, k, i == 0 ? -m0 : -m1);
         pstore(c, c.lane < 3, rIH + c.lane, k, c.lane == 0 ? i00 : c.lane == 1 ? i01 : i11);
-        pstore(c, m.ps0 >= 0, m.ps0, k, P[0]);
-        pstore(c, m.ps1 >= 0, m.ps1, k, P[1]);
+        pstore(c, m.ps >= 0, m.ps, k, Pij);
+    };
+    // two stages per trip with ping-pong operand buffers (no register copies between stages)
+    EpOps oa = ep_ops(c, m, N - 1, dw), ob;
+    int k = N - 1;
+    for (; k >= 1; k -= 2) {
+        stage(k, oa, ob, k - 1);
+        stage(k - 1, ob, oa, k > 1 ? k - 2 : 0);
     }
+    if (k == 0) stage(0, oa, ob, 0);
     __syncthreads();
     return pd;
 }
 
-// ============ forward sweep on the matrix cores: [x^_{k+1}; du_k] = [Phi_k; K^_k] x^_k ============
-// Phi = A^ + B^ K^ (rows 0..6), rows 7,8 = K^; x^ stays in accumulator column 0, which is exactly
-// the B-operand layout of the next step (2 MFMAs per stage, nothing moves between lanes).
-// crow: constraint residual rows (x^_0 = [-c_0; 1]); bhrow: b^ = -c_{k+1} stored at stage k.
+// ============ forward sweep: [x^_{k+1}; du_k] = [Phi_k; K^_k] x^_k, Phi = A^ + B^ K^ ============
+// Lane 8g + m owns the term Phi[row(g)][m] x^_k[m] (rows g = 0..5: dx_{k+1}; g = 6, 7: du0, du1).
+// The row sums are three in-row DPP adds (quad xor 1, xor 2, half-mirror); the next stage's x^[m]
+// comes from group m by one ds_bpermute.  crow: residual rows (x^_0 = [-c_0; 1]); bhrow: b^ = -c_{k+1}
+// stored at stage k.
+__device__ __forceinline__ double bperm_d(double v, int src_lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 template <int BM>
 __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bhrow, int orow) {
-    const int N = c.N, q = c.lane >> 4, i = c.lane & 15;
-    // operand slots: Phi[i][kappa] = fone + row fas + fkc * row fk, kappa = 4s + q
-    int fas[2], fk[2];
-    double fone[2], fkc[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const int kap = 4 * s + q;
-        fone[s] = (i == kap && i <= 6) ? 1.0 : 0.0;
-        fas[s] = (i < 6 && kap < 6 && d_idx(i, kap) >= 0) ? rAJ + d_idx(i, kap) : (i < 6 && kap == 6) ? bhrow + i : PAD;
-        const int u = (i == 5 || i == 7) ? 0 : (i == 4 || i == 8) ? 1 : -1;
-        fk[s] = (u >= 0 && kap < 6) ? rK + 6 * u + kap : (u >= 0 && kap == 6) ? rKF + u : PAD;
-        fkc[s] = (u >= 0 && kap <= 6) ? (i < 6 ? c.dt : 1.0) : 0.0;
-    }
-    d4 X = {0.0, 0.0, 0.0, 0.0};
-    if (i == 0) {  // x^_0 = [-c_0; 1]
-        X[0] = -c.r(crow + q, 0);
-        X[1] = q < 2 ? -c.r(crow + q + 4, 0) : (q == 2 ? 1.0 : 0.0);
-        c.r(orow + q, 0) = X[0];
-        if (q < 2) c.r(orow + q + 4, 0) = X[1];
-    }
-    auto ops = [&](int k, double& a0, double& a1) {
-        a0 = fone[0] + c.r(fas[0], k) + fkc[0] * c.r(fk[0], k);
-        a1 = fone[1] + c.r(fas[1], k) + fkc[1] * c.r(fk[1], k);
-    };
-    double n0, n1;  // operands of the next stage, fetched one stage ahead
-    ops(0, n0, n1);
+    const int N = c.N, g = c.lane >> 3, mm = c.lane & 7;
+    // output row of this lane's group: 0..5 = dx_{k+1}[g], 6/7 = du0/du1 (rows 7/8 of [Phi; K^])
+    const int u = (g == 5 || g == 6) ? 0 : (g == 4 || g == 7) ? 1 : -1;
+    const double fone = (g < 6 && mm == g) ? 1.0 : 0.0;
+    const int fas = (g < 6 && mm < 6 && d_idx(g, mm) >= 0) ? rAJ + d_idx(g, mm) : (g < 6 && mm == 6) ? bhrow + g : PAD;
+    const int fk = (u >= 0 && mm < 6) ? rK + 6 * u + mm : (u >= 0 && mm == 6) ? rKF + u : PAD;
+    const double fkc = u >= 0 ? (g < 6 ? c.dt : 1.0) : 0.0;
+    // x^_0[m] = -c_0[m] (m < 6), 1 (m = 6), 0 (m = 7)
+    double x = mm < 6 ? -c.r(crow + mm, 0) : (mm == 6 ? 1.0 : 0.0);
+    if (c.lane < 6) c.r(orow + c.lane, 0) = -c.r(crow + c.lane, 0);
+    const int src = 8 * (mm < 6 ? mm : 0);  // group holding x_{k+1}[mm]
+    double nph = fone + c.r(fas, 0) + fkc * c.r(fk, 0);
     for (int k = 0; k < N; ++k) {
-        const double a0 = n0, a1 = n1;
-        ops(k + 1 < N ? k + 1 : k, n0, n1);
-        d4 Y = {0.0, 0.0, 0.0, 0.0};
-        Y = mfma(a0, X[0], Y);
-        Y = mfma(a1, X[1], Y);
-        // rows 0..5 -> dx_{k+1}; row 7 (q=3, reg 1) -> du0; row 8 (q=0, reg 2) -> du1 (column-0 lanes)
-        pstore(c, i == 0, orow + q, k + 1, Y[0]);
-        pstore(c, i == 0 && q < 2, orow + q + 4, k + 1, Y[1]);
-        pstore(c, i == 0 && q == 3, orow + 6, k, Y[1]);
-        pstore(c, i == 0 && q == 0, orow + 7, k, Y[2]);
-        X = Y;
+        const double ph = nph;
+        const int kn = k + 1 < N ? k + 1 : k;
+        nph = fone + c.r(fas, kn) + fkc * c.r(fk, kn);
+        double y = ph * x;
+        y += dppd<0xB1>(y);   // quad_perm [1,0,3,2]
+        y += dppd<0x4E>(y);   // quad_perm [2,3,0,1]
+        y += dppd<0x141>(y);  // row_half_mirror: the 8-lane group sum, in every lane of the group
+        // rows 0..5 -> dx_{k+1}; groups 6/7 -> du0/du1 at stage k
+        pstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
+        pstore(c, mm == 0 && g >= 6, orow + g, k, y);
+        const double xn = bperm_d(y, src);
+        x = mm < 6 ? xn : (mm == 6 ? 1.0 : 0.0);
     }
     __syncthreads();
 }
