@@ -497,8 +497,6 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
         const double2 p5 = ld2(PF + 44);  // P[5][4], P[5][5]
         const double p44 = PF[36];
-        __builtin_amdgcn_sched_barrier(0);
-        nx = ep_ops(c, m, kn, dw);
         const double h00 = r00 + o.sgu0 + dw + dt2 * p5.y, h01 = r01 + dt2 * p5.x, h11 = r11 + o.sgu1 + dw + dt2 * p44;
         const double det = h00 * h11 - h01 * h01;
         pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
@@ -515,6 +513,9 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         // column j of PA (rows 0..5; rows 4, 5 also give G[.][j]) and G[.][i]
         const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
         const double2 gi = ld2(PT + 8 * i + 4);  // PA[4][i], PA[5][i]
+        // next stage's operands: issued behind the tile reads (LDS serves a wave in order)
+        __builtin_amdgcn_sched_barrier(0);
+        nx = ep_ops(c, m, kn, dw);
         // F[i][j] = PA[i][j] + sum_l D[l][i] PA[l][j] + H^[i][j]
         double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
         fa = fma(o.di[2], c23.x, fa);

@@ -12,6 +12,9 @@ from pathlib import Path
 import numpy as np
 
 LIB_PATH = Path(__file__).resolve().parent / "libttmpc.so"
+# diagnostics only (A/B timing of two builds in one GPU session): TTMPC_LIB=<path to another build>
+if os.environ.get("TTMPC_LIB"):
+    LIB_PATH = Path(os.environ["TTMPC_LIB"]).resolve()
 
 TT_CONVERGED, TT_ACCEPTABLE, TT_MAX_ITER, TT_INFEASIBLE, TT_NONFINITE = range(5)
 TT_VARIANT_TRACK, TT_VARIANT_TRACK_OBCA, TT_VARIANT_NMPC, TT_VARIANT_FUZZY, TT_VARIANT_OBCA_PLAN = range(5)
