@@ -141,3 +141,109 @@ def test_case_batch(cases, B: int, N: int, seed: int = 0, pos_sigma=0.5, ang_sig
 
 def default_data_dir() -> Path:
     return Path(__file__).resolve().parent / "data"
+
+
+# ----------------------------------------------------------------------------------------------
+# OBCA planning scenarios (BASELINE config C4; trajectory_optimization.py / trajectory_animation.py)
+# ----------------------------------------------------------------------------------------------
+OBCA_PARAMS = {"M": 0.15, "L1": 7.05, "L2": 12.45, "W1": 3.05, "W2": 2.95, "dt": 0.1}  # trajectory_animation.py:48-52
+# trajectory_animation.py:77-80 (theta free, v in [-5, 10])
+OBCA_XLB = np.array([-np.inf, -np.inf, -np.inf, -np.pi / 3.0, -np.pi / 4.0, -5.0])
+OBCA_XUB = np.array([np.inf, np.inf, np.inf, np.pi / 3.0, np.pi / 4.0, 10.0])
+OBCA_ULB = np.array([-5.0, -np.pi / 2])
+OBCA_UUB = np.array([5.0, np.pi / 2])
+OBCA_Q = np.eye(NX)                      # trajectory_animation.py:63-69
+OBCA_R = 10.0 * np.eye(NU)               # trajectory_animation.py:70-72
+LAM_PATTERN = np.array([100.0, 105.0, 110.0, 115.0, 100.0, 105.0, 110.0, 115.0])  # trajectory_optimization.py:222
+
+
+def obstacles_array(obstacle_list):
+    """[{'center': (cx, cy), 'width': w, 'height': h}] -> (M,4) float64 (cx, cy, w, h)."""
+    return np.array([[o["center"][0], o["center"][1], o["width"], o["height"]] for o in obstacle_list],
+                    dtype=np.float64).reshape(-1, 4)
+
+
+def interpolate_waypoints(waypoints, num_output_nodes):
+    """interpolate_waypoints.py:5-26: scipy CubicSpline over linspace(0,1,W) sampled at
+    linspace(0,1,num_output_nodes).  Returns the array (the reference wraps it in a 1-list)."""
+    from scipy.interpolate import CubicSpline
+    w = np.asarray(waypoints, dtype=np.float64)
+    sp = CubicSpline(np.linspace(0.0, 1.0, len(w)), w)
+    return sp(np.linspace(0.0, 1.0, num_output_nodes))
+
+
+def obca_guess(positions, headings, hitch, N, M):
+    """_hybrid_a_star_initial_trajectory (trajectory_optimization.py:227-274): waypoint splines to N
+    nodes, x_k = (p_k, theta_k, psi_k, 0, 0) for k < N, x_N = last node, u = 0, mu = 100,
+    lam = kron(1_M, [100,105,110,115,100,105,110,115]).  ``headings`` already carry the +pi/2 shift
+    (trajectory_optimization.py:238).  Returns the reference's interleaved z (n = N(8+16M)+6+16M)."""
+    P = interpolate_waypoints(positions, N)
+    H = interpolate_waypoints(headings, N)
+    S = interpolate_waypoints(hitch, N)
+    st = 8 + 16 * M
+    z = np.zeros(N * st + 6 + 16 * M)
+    duals = np.concatenate([np.full(8 * M, 100.0), np.tile(LAM_PATTERN, M)])
+    for k in range(N):
+        z[k * st:k * st + 6] = [P[k, 0], P[k, 1], H[k], S[k], 0.0, 0.0]
+        z[k * st + 8:(k + 1) * st] = duals
+    z[N * st:N * st + 6] = [P[-1, 0], P[-1, 1], H[-1], S[-1], 0.0, 0.0]
+    z[N * st + 6:] = duals
+    return z
+
+
+def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5, ang_sigma=0.05):
+    """C4 generator: test_cases.json cases x Monte-Carlo start perturbations.  Each instance is the
+    2-waypoint initialize.json of its case (apply_case.py:16-34) with a perturbed start; the guess is
+    built from those waypoints (obca_guess) and (x_init, x_goal) as get_initial_goal_states.py:5-26 +
+    trajectory_animation.py:83-92 (speed and steering appended as 0).
+    Returns x0 (B,6), x_goal (B,6), z_guess (B,n)."""
+    rng = np.random.default_rng(seed)
+    x0 = np.empty((B, NX))
+    xg = np.empty((B, NX))
+    st = 8 + 16 * M
+    zg = np.empty((B, N * st + 6 + 16 * M))
+    for b in range(B):
+        c = cases[b % len(cases)]
+        pos = np.array([[c["start"]["x"], c["start"]["y"]], [c["goal"]["x"], c["goal"]["y"]]], dtype=np.float64)
+        hd = np.array([c["start"]["heading_rad"], c["goal"]["heading_rad"]], dtype=np.float64) + np.pi / 2
+        hi = np.array([c["start"]["hitch_angle_rad"], c["goal"]["hitch_angle_rad"]], dtype=np.float64)
+        if b >= len(cases):  # instance 0..len-1 are the exact cases, the rest Monte-Carlo perturbed
+            pos[0] += rng.normal(0.0, pos_sigma, 2)
+            hd[0] += rng.normal(0.0, ang_sigma)
+            hi[0] = float(np.clip(hi[0] + rng.normal(0.0, ang_sigma), -0.5, 0.5))
+        x0[b] = [pos[0, 0], pos[0, 1], hd[0], hi[0], 0.0, 0.0]
+        xg[b] = [pos[1, 0], pos[1, 1], hd[1], hi[1], 0.0, 0.0]
+        zg[b] = obca_guess(pos, hd, hi, N, M)
+    return x0, xg, zg
+
+
+def obca_replan_batch(base_states, B: int, N: int, M: int, seed: int = 0, n_waypoints: int = 8,
+                      pos_sigma=0.5, ang_sigma=0.05):
+    """C4 generator: Monte-Carlo re-plans around a collision-free OBCA plan.
+
+    ``base_states`` (6, N+1) is a plan such as the reference's committed IPOPT solution
+    (python-files/data/state_traj.txt).  Each instance subsamples it to ``n_waypoints`` waypoints
+    (the shape of a Hybrid-A* initialize.json, trajectory_optimization.py:227-274), perturbs the
+    start pose (instance 0 unperturbed) and builds the reference's guess from those waypoints
+    (obca_guess).  x_init = first waypoint, x_goal = last waypoint with zero steering and speed
+    (get_initial_goal_states.py + trajectory_animation.py:83-92).
+    Returns x0 (B,6), x_goal (B,6), z_guess (B,n)."""
+    S = np.asarray(base_states, dtype=np.float64)
+    rng = np.random.default_rng(seed)
+    idx = np.linspace(0, S.shape[1] - 1, n_waypoints).round().astype(int)
+    st = 8 + 16 * M
+    x0 = np.empty((B, NX))
+    xg = np.empty((B, NX))
+    zg = np.empty((B, N * st + 6 + 16 * M))
+    for b in range(B):
+        pos = S[0:2, idx].T.copy()
+        hd = S[2, idx].copy()
+        hi = S[3, idx].copy()
+        if b > 0:
+            pos[0] += rng.normal(0.0, pos_sigma, 2)
+            hd[0] += rng.normal(0.0, ang_sigma)
+            hi[0] += rng.normal(0.0, ang_sigma)
+        x0[b] = [pos[0, 0], pos[0, 1], hd[0], hi[0], 0.0, 0.0]
+        xg[b] = [pos[-1, 0], pos[-1, 1], hd[-1], hi[-1], 0.0, 0.0]
+        zg[b] = obca_guess(pos, hd, hi, N, M)
+    return x0, xg, zg

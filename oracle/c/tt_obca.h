@@ -1,0 +1,58 @@
+/* CPU ORACLE for the OBCA NLPs (test infrastructure + bench cpu_baseline only; never linked into
+ * the product library).
+ *
+ * Restates two reference NLPs that share the OBCA collision-avoidance structure:
+ *   mode TTO_OBCA_PLAN  : TrajectoryOptimization (python-files/trajectory_optimization.py:9-331)
+ *                         goal cost with terminal weight 100 Q (168-183), final box |x_N-g|<=1e-2
+ *                         (168-174), OBCA rows (93-166), x/u/mu/lam layout (55-91).
+ *   mode TTO_OBCA_TRACK : MPCTrackingControlObs (python-files/mpc_control_obs.py:8-322)
+ *                         tracking cost with Q_f = Q (31-41), same OBCA rows (65-138), no final box.
+ * Both on top of trajectory_planning.py:28-36 (x_0 = x_init, Euler dynamics) and
+ * truck_trailer_model.py:8-72 (model, H-reps, body centres).
+ *
+ * Decision vector z (reference layout, trajectory_optimization.py:55-91):
+ *   stage k<N : [x_k(6), u_k(2), mu_k(8M), lam_k(8M)],  stage N : [x_N(6), mu_N(8M), lam_N(8M)]
+ *   n = N(8+16M) + 6 + 16M.  mu/lam slot i*8+[0:4] = truck vs obstacle i, i*8+[4:8] = trailer.
+ */
+#ifndef TT_OBCA_H
+#define TT_OBCA_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTO_MAXM 16
+enum { TTO_OBCA_PLAN = 0, TTO_OBCA_TRACK = 1 };
+
+typedef struct {
+    int N, M, mode;
+    double dt, L1, L2, Mh, W1, W2;  /* params dict (trajectory_animation.py:48-52) */
+    double Q[36], R[4];              /* row-major, symmetrised internally */
+    double xlb[6], xub[6], ulb[2], uub[2];  /* |b| >= 1e19 = free */
+    double obs[4 * TTO_MAXM];        /* cx, cy, w, h per obstacle (get_obstacles.py:20-28 format) */
+    double dmin;                     /* 0.2   trajectory_optimization.py:95 */
+    double eq_tol;                   /* 1e-5  range of the G'mu + R'A'lam rows (136-139) */
+    double fin_tol;                  /* 1e-2  final box (172-173); plan mode only */
+    double tfac;                     /* 100   terminal weight factor (180); track mode uses 1 */
+    double tol, acc_tol;             /* IPOPT tol / acceptable_tol (defaults 1e-8 / 1e-6) */
+    int max_iter, acc_iter;          /* 5000 (trajectory_optimization.py:198) / 15 */
+    int dual_init;                   /* 0: start from the guess's mu/lam (reference behaviour);
+                                        1: replace them by the separating-axis certificate of each
+                                        body/obstacle pair at the guess pose (see tt_obca.c) */
+} tto_obca_problem;
+
+/* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).
+ * z_guess (n) or NULL (plan: _generate_initial_trajectory_guess 209-225; track: reference copy +
+ * dual pattern, mpc_control_obs.py:216-239).  z_out (n).  Returns per-instance status
+ * (0 converged, 1 acceptable, 2 max_iter, 3 infeasible x_init, 4 non-finite / regularisation failed). */
+int tto_obca_solve(const tto_obca_problem* P, const double* x_init, const double* x_goal, const double* xref,
+                   const double* uref, const double* z_guess, double* z_out, int* iters, double* kkt);
+
+/* OpenMP over instances; arrays instance-major; x_goal/xref/uref/z_guess may be NULL per mode. */
+int tto_obca_solve_batch(const tto_obca_problem* P, int B, const double* x_init, const double* x_goal,
+                         const double* xref, const double* uref, const double* z_guess, double* z_out,
+                         int* status, int* iters, double* kkt, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -99,3 +99,93 @@ def split(z, N):
 
 
 os.environ.setdefault("OMP_PROC_BIND", "false")
+
+
+# ------------------------------------------------------------------------------------------------
+# OBCA NLPs (tt_obca.c): TrajectoryOptimization.plan / MPCTrackingControlObs.solve restated
+# ------------------------------------------------------------------------------------------------
+MAXM = 16
+OBCA_PLAN, OBCA_TRACK = 0, 1
+
+
+class TTOObcaProblem(C.Structure):
+    _fields_ = [("N", C.c_int), ("M", C.c_int), ("mode", C.c_int),
+                ("dt", C.c_double), ("L1", C.c_double), ("L2", C.c_double), ("Mh", C.c_double),
+                ("W1", C.c_double), ("W2", C.c_double),
+                ("Q", C.c_double * 36), ("R", C.c_double * 4), ("xlb", C.c_double * 6), ("xub", C.c_double * 6),
+                ("ulb", C.c_double * 2), ("uub", C.c_double * 2), ("obs", C.c_double * (4 * MAXM)),
+                ("dmin", C.c_double), ("eq_tol", C.c_double), ("fin_tol", C.c_double), ("tfac", C.c_double),
+                ("tol", C.c_double), ("acc_tol", C.c_double), ("max_iter", C.c_int), ("acc_iter", C.c_int),
+                ("dual_init", C.c_int)]
+
+
+def make_obca_problem(N, params, Q, R, xlb, xub, ulb, uub, obstacles, mode=OBCA_PLAN, tol=1e-8, acc_tol=1e-6,
+                      max_iter=5000, acc_iter=15, dual_init=1):
+    """obstacles: (M,4) array of (cx, cy, w, h) (get_obstacles.py format)."""
+    ob = np.asarray(obstacles, dtype=np.float64).reshape(-1, 4)
+    if not 1 <= ob.shape[0] <= MAXM:
+        raise ValueError("1 <= M <= 16 obstacles")
+    P = TTOObcaProblem()
+    P.N, P.M, P.mode = int(N), ob.shape[0], int(mode)
+    P.dt, P.L1, P.L2, P.Mh = params["dt"], params["L1"], params["L2"], params["M"]
+    P.W1, P.W2 = params["W1"], params["W2"]
+    P.Q[:] = list(np.asarray(Q, float).reshape(36))
+    P.R[:] = list(np.asarray(R, float).reshape(4))
+    P.xlb[:] = list(_fin(xlb)); P.xub[:] = list(_fin(xub))
+    P.ulb[:] = list(_fin(ulb)); P.uub[:] = list(_fin(uub))
+    P.obs[: ob.size] = list(ob.reshape(-1))
+    P.dmin, P.eq_tol, P.fin_tol = 0.2, 1e-5, 1e-2
+    P.tfac = 100.0 if mode == OBCA_PLAN else 1.0
+    P.tol, P.acc_tol, P.max_iter, P.acc_iter = tol, acc_tol, max_iter, acc_iter
+    P.dual_init = int(dual_init)
+    return P
+
+
+def obca_n(N, M):
+    return N * (8 + 16 * M) + 6 + 16 * M
+
+
+def obca_solve_batch(P, x0, x_goal=None, xref=None, uref=None, z_guess=None, nthreads=0):
+    """-> (z (B,n), status, iters, kkt).  plan mode needs x_goal (B,6); track mode xref/uref."""
+    L = lib()
+    if not hasattr(L, "_obca_ready"):
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int)
+        L.tto_obca_solve_batch.argtypes = [C.POINTER(TTOObcaProblem), C.c_int, dp, dp, dp, dp, dp, dp, ip, ip, dp,
+                                           C.c_int]
+        L.tto_obca_solve_batch.restype = C.c_int
+        L._obca_ready = True
+    N, M = P.N, P.M
+    n = obca_n(N, M)
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, 6)
+    B = x0.shape[0]
+    cv = lambda a, shp: None if a is None else np.ascontiguousarray(a, dtype=np.float64).reshape(shp)  # noqa: E731
+    xg = cv(x_goal, (B, 6))
+    xr = cv(xref, (B, N + 1, 6))
+    ur = cv(uref, (B, N, 2))
+    zg = cv(z_guess, (B, n))
+    z = np.zeros((B, n))
+    st = np.zeros(B, dtype=np.int32)
+    it = np.zeros(B, dtype=np.int32)
+    kk = np.zeros(B)
+    rc = L.tto_obca_solve_batch(C.byref(P), B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg), _ptr(z),
+                                st.ctypes.data_as(C.POINTER(C.c_int)), it.ctypes.data_as(C.POINTER(C.c_int)),
+                                _ptr(kk), int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"tto_obca_solve_batch failed: {rc}")
+    return z, st, it, kk
+
+
+def obca_split(z, N, M):
+    """_split_decision_variables (trajectory_optimization.py:277-309): (B,n) -> X (B,N+1,6), U (B,N,2),
+    mu (B,N+1,8M), lam (B,N+1,8M)."""
+    z = np.asarray(z).reshape(z.shape[0], -1)
+    B = z.shape[0]
+    st = 8 + 16 * M
+    body = z[:, : N * st].reshape(B, N, st)
+    last = z[:, N * st:]
+    X = np.concatenate([body[:, :, :6], last[:, None, :6]], axis=1)
+    U = body[:, :, 6:8].copy()
+    mu = np.concatenate([body[:, :, 8:8 + 8 * M], last[:, None, 6:6 + 8 * M]], axis=1)
+    lam = np.concatenate([body[:, :, 8 + 8 * M:], last[:, None, 6 + 8 * M:]], axis=1)
+    return X, U, mu, lam
