@@ -39,3 +39,43 @@ inline int max_horizon() { return (kMaxLdsBytes / 8 - kScratch) / kRowsPerStage 
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream);
 
 }  // namespace ttmpc
+
+namespace ttmpc {
+
+// ---------------- OBCA NLPs (tt_obca.hip) ----------------
+constexpr int kObcaMaxM = 16;
+constexpr int kObcaThreads = 256;  // one workgroup (4 waves) per instance
+constexpr int kObcaMaxFilter = 64;
+enum { OBCA_PLAN = 0, OBCA_TRACK = 1 };
+
+struct ObcaArgs {
+    int N, M, B, mode, max_iter, acc_iter, dual_init;
+    double dt, L1, L2, Mh, W1, W2, tol, acc_tol, dmin, eq_tol, fin_tol, tfac;
+    double Q[36], R[4];
+    double xlb[6], xub[6], ulb[2], uub[2];
+    double obs[4 * kObcaMaxM];      // cx, cy, w, h
+    const double* x0;               // [B][6]
+    const double* xgoal;            // [B][6]          (plan mode)
+    const double* xref;             // [B][N+1][6]     (track mode)
+    const double* uref;             // [B][N][2]       (track mode)
+    const double* zg;               // [B][n] reference layout, or nullptr
+    double* xout;                   // [B][N+1][6]
+    double* uout;                   // [B][N][2]
+    double* zout;                   // [B][n] or nullptr
+    int* status;                    // [B]
+    int* iters;                     // [B] or nullptr
+    double* kkt;                    // [B] or nullptr
+    double* ws;                     // per-instance workspace, obca_ws_doubles(N, M) each
+};
+
+// workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
+constexpr int kObcaStageFields = 188;
+constexpr int kObcaBlockFields = 76;
+inline size_t obca_ws_doubles(int N, int M) {
+    return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
+}
+inline size_t obca_n(int N, int M) { return (size_t)N * (8 + 16 * M) + 6 + 16 * M; }
+
+hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream);
+
+}  // namespace ttmpc

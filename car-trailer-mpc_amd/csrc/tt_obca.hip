@@ -1,0 +1,1057 @@
+// Batched OBCA trajectory optimisation / MPC+OBCA on gfx950 (MI355X / CDNA4).
+//
+// NLP (reference python-files/, restated; see oracle/c/tt_obca.c for the CPU statement):
+//   variables   x_k, u_k, mu_k (8M), lam_k (8M) >= 0             trajectory_optimization.py:55-91
+//   dynamics    x_0 = x_init, x_{k+1} = x_k + dt f(x_k, u_k)         trajectory_planning.py:28-36
+//   OBCA rows   per stage k, obstacle i, body b (truck/trailer):     trajectory_optimization.py:93-166
+//     d1 = g'mu - (A p(x) - b)'lam + d_min <= 0,  d2,d3 = G'mu + R(x)'A'lam in [-1e-5, 1e-5],
+//     d4 = ||A'lam|| - 1 <= 0                       (bodies: truck_trailer_model.py:31-72)
+//   plan  : goal cost, terminal 100 Q, |x_N - g| <= 1e-2               trajectory_optimization.py:168-183
+//   track : reference tracking cost, Q_f = Q                           mpc_control_obs.py:31-41
+//
+// Solver: the slack-form IPOPT restatement of the oracle (tol 1e-8, acceptable 1e-6 x 15, monotone mu,
+// bound_relax 1e-8, bound_push 1e-2, kappa_sigma 1e10, exact Hessian), IPOPT's filter line search with
+// up to 4 second-order corrections, Hessian regularisation with IPOPT's delta_w schedule.
+//
+// One workgroup (4 waves) per instance.  Work split:
+//   * stage-parallel phases (linearisation, optimality error, block elimination + stage Hessians,
+//     block step recovery, fraction-to-boundary, trial evaluation, updates): thread k owns stage k and
+//     its 2M OBCA blocks (obstacle x body).  Each block (8 duals, 4 rows) couples only to
+//     (X, Y, theta, psi) of its stage; its mu part is diagonal and its lam part a 4x4 SPD block, so
+//     the elimination is a 4x4 Cholesky + a 4x4 Schur complement T = D^-1 + Y'Y (never C'DC: D reaches
+//     1e10 on the +-1e-5 range rows and that product cancels catastrophically).
+//   * serial phases (Riccati backward sweep over the 6x6 stage blocks, forward sweep): wave 0, lane
+//     (i,j) owns entry (i,j) of the 6x6 products; P and PA tiles in LDS.
+// Workspace: per instance in HBM, stage fields [f][k] and block fields [f][j][k] so that the lanes of a
+// stage-parallel phase (consecutive k) read consecutive addresses.
+#include <math.h>
+
+#include "tt_kernel.hpp"
+
+namespace ttmpc {
+namespace {
+
+constexpr int T = kObcaThreads;
+constexpr double RELAX = 1e-8;
+constexpr double EPS = 2.220446049250313e-16;
+
+enum : int {
+    S_X = 0, S_U = 6, S_ZLX = 8, S_ZUX = 14, S_ZLU = 20, S_ZUU = 22, S_YC = 24,
+    S_GX = 30, S_GU = 36, S_C = 38, S_AJ = 44, S_WD = 53, S_QT = 60, S_QV = 81, S_RT = 87, S_RV = 90,
+    S_P = 92, S_PV = 113, S_K = 119, S_KF = 131, S_GI = 133, S_H = 136, S_DX = 148, S_DU = 160, S_YCP = 164,
+    S_CT = 176, S_CR = 182, S_END = 188
+};
+static_assert(S_END == kObcaStageFields, "stage field count");
+enum : int {
+    B_W = 0, B_ZW = 8, B_S = 16, B_VL = 20, B_VU = 24, B_YD = 28, B_D = 32, B_DW = 36, B_DS = 52, B_YP = 60,
+    B_DT = 68, B_DR = 72, B_END = 76
+};
+static_assert(B_END == kObcaBlockFields, "block field count");
+
+// packed symmetric 6x6 (upper) index
+__host__ __device__ constexpr int sy6(int i, int j) {
+    return i <= j ? i * 6 - (i * (i - 1)) / 2 + (j - i) : j * 6 - (j * (j - 1)) / 2 + (i - j);
+}
+// packed lower 4x4 index
+__host__ __device__ constexpr int lo4(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// dt*J nonzeros: 0:(0,2) 1:(0,5) 2:(1,2) 3:(1,5) 4:(2,4) 5:(2,5) 6:(3,3) 7:(3,4) 8:(3,5)   (A = I + dt J)
+__host__ __device__ constexpr int dj_idx(int r, int c) {
+    return (r == 0 && c == 2) ? 0 : (r == 0 && c == 5) ? 1 : (r == 1 && c == 2) ? 2 : (r == 1 && c == 5) ? 3
+         : (r == 2 && c == 4) ? 4 : (r == 2 && c == 5) ? 5 : (r == 3 && c == 3) ? 6 : (r == 3 && c == 4) ? 7
+         : (r == 3 && c == 5) ? 8 : -1;
+}
+// dynamics curvature nonzeros (symmetric): 0:(2,2) 1:(2,5) 2:(3,3) 3:(3,4) 4:(3,5) 5:(4,4) 6:(4,5)
+__host__ __device__ constexpr int wd_idx(int i, int j) {
+    return i > j ? wd_idx(j, i)
+         : (i == 2 && j == 2) ? 0 : (i == 2 && j == 5) ? 1 : (i == 3 && j == 3) ? 2 : (i == 3 && j == 4) ? 3
+         : (i == 3 && j == 5) ? 4 : (i == 4 && j == 4) ? 5 : (i == 4 && j == 5) ? 6 : -1;
+}
+
+// ---------------- wave / workgroup reductions (DPP inside 16-lane rows, readlane across rows) ----------
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)(b & 0xffffffffll), (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+enum { R_SUM = 0, R_MAX = 1, R_MIN = 2 };
+__device__ __forceinline__ double rop(int op, double a, double b) {
+    return op == R_SUM ? a + b : op == R_MAX ? fmax(a, b) : fmin(a, b);
+}
+__device__ __forceinline__ double wave_red(double v, int op) {
+    v = rop(op, v, dppd<0xB1>(v));
+    v = rop(op, v, dppd<0x4E>(v));
+    v = rop(op, v, dppd<0x141>(v));
+    v = rop(op, v, dppd<0x140>(v));
+    return rop(op, rop(op, readlane_d(v, 0), readlane_d(v, 16)), rop(op, readlane_d(v, 32), readlane_d(v, 48)));
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+struct Shared {
+    double red[4][12];
+    double P[36], PA[36];
+    // final-row (plan mode) state, owned by the thread of stage N
+    double sf[6], vLf[6], vUf[6], ydf[6], df[6], dsf[2][6], ydpf[2][6], dft[6], dfr[6], Df[6], rf[6];
+    double fth[kObcaMaxFilter], fph[kObcaMaxFilter];
+    int nf;
+    int flag;
+};
+
+// workgroup reduction of NV values with per-value op; result uniform in every thread, fixed order
+template <int NV>
+__device__ __forceinline__ void wg_reduce(Shared& sh, double (&v)[NV], const int (&op)[NV]) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double r[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) r[i] = wave_red(v[i], op[i]);
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh.red[wave][i] = r[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = rop(op[i], rop(op[i], sh.red[0][i], sh.red[1][i]), rop(op[i], sh.red[2][i], sh.red[3][i]));
+}
+
+// 1/x by v_rcp_f64 + two Newton steps
+__device__ __forceinline__ double frcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+// sum of logs as log(prod of mantissas) + (sum of exponents) ln 2
+struct LogSum {
+    double m = 1.0;
+    int e = 0;
+    int n = 0;
+    __device__ __forceinline__ void add(double s) {
+        int ex;
+        m *= frexp(s, &ex);
+        e += ex;
+        if (++n == 24) {  // renormalise before the mantissa product can underflow (0.5^24 >> DBL_MIN)
+            int e2;
+            m = frexp(m, &e2);
+            e += e2;
+            n = 0;
+        }
+    }
+    __device__ __forceinline__ double value() const { return log(m) + (double)e * 0.69314718055994530942; }
+};
+
+// ---------------- per-instance context ----------------
+struct Ctx {
+    const ObcaArgs* a;
+    double* ws;
+    int N, NP, nbk, tid, b;
+    double dt;
+    double xl[6], xu[6], ul[2], uu[2];
+    int hx, hu;             // bit i: finite lower (i) / upper (8+i) bound
+    double rlo, rhi;        // relaxed bounds of the range rows d2, d3
+    double fL, fU;          // final box
+    const double* tgt_x;    // plan: x_goal; track: xref of this instance
+    const double* tgt_u;    // track: uref
+    __device__ __forceinline__ double& S(int f, int k) const { return ws[(size_t)f * NP + k]; }
+    __device__ __forceinline__ double& B(int f, int j, int k) const {
+        return ws[(size_t)S_END * NP + ((size_t)f * nbk + j) * NP + k];
+    }
+    __device__ __forceinline__ bool hlx(int i) const { return (hx >> i) & 1; }
+    __device__ __forceinline__ bool hux(int i) const { return (hx >> (8 + i)) & 1; }
+    __device__ __forceinline__ bool hlu(int i) const { return (hu >> i) & 1; }
+    __device__ __forceinline__ bool huu(int i) const { return (hu >> (8 + i)) & 1; }
+    __device__ __forceinline__ bool plan() const { return a->mode == OBCA_PLAN; }
+    // row r of a block: lower bound finite only for the range rows 1, 2
+    __device__ __forceinline__ bool hrl(int r) const { return r == 1 || r == 2; }
+    __device__ __forceinline__ double rL(int r) const { return (r == 1 || r == 2) ? rlo : -INFINITY; }
+    __device__ __forceinline__ double rU(int r) const { return (r == 1 || r == 2) ? rhi : RELAX; }
+};
+
+// ---------------- model: truck_trailer_model.py:8-24 ----------------
+__device__ __forceinline__ void model_f(const ObcaArgs& a, const double* x, const double* u, double* fo) {
+    const double th = x[2], psi = x[3], phi = x[4], v = x[5];
+    const double t = tan(phi);
+    double sth, cth, sps, cps;
+    sincos(th, &sth, &cth);
+    sincos(psi, &sps, &cps);
+    fo[0] = v * cth;
+    fo[1] = v * sth;
+    fo[2] = v * t / a.L1;
+    fo[3] = -v * t / a.L1 * (1.0 + a.Mh / a.L2 * cps) - v * sps / a.L2;
+    fo[4] = u[1];
+    fo[5] = u[0];
+}
+
+// dt*J nonzeros (9) and the dynamics curvature -dt sum_i y_i d2 f_i (7 nonzeros)
+__device__ __forceinline__ void model_lin(const ObcaArgs& a, const double* x, const double* y, double* dj, double* wd) {
+    const double th = x[2], psi = x[3], phi = x[4], v = x[5];
+    const double L1 = a.L1, L2 = a.L2, M = a.Mh, dt = a.dt;
+    double sn, cs, sp, cp;
+    sincos(th, &sn, &cs);
+    sincos(psi, &sp, &cp);
+    const double t = tan(phi), cphi = cos(phi), c2 = 1.0 / (cphi * cphi), k = 1.0 + M / L2 * cp;
+    dj[0] = dt * (-v * sn);
+    dj[1] = dt * cs;
+    dj[2] = dt * (v * cs);
+    dj[3] = dt * sn;
+    dj[4] = dt * (v * c2 / L1);
+    dj[5] = dt * (t / L1);
+    dj[6] = dt * (v * t * M * sp / (L1 * L2) - v * cp / L2);
+    dj[7] = dt * (-v * c2 / L1 * k);
+    dj[8] = dt * (-t / L1 * k - sp / L2);
+    const double s = -dt;
+    wd[0] = s * (y[0] * (-v * cs) + y[1] * (-v * sn));
+    wd[1] = s * (y[0] * (-sn) + y[1] * cs);
+    wd[2] = s * (y[3] * (v * t * M * cp / (L1 * L2) + v * sp / L2));
+    wd[3] = s * (y[3] * (v * c2 * M * sp / (L1 * L2)));
+    wd[4] = s * (y[3] * (t * M * sp / (L1 * L2) - cp / L2));
+    wd[5] = s * (y[2] * (2 * v * t * c2 / L1) + y[3] * (-2 * v * t * c2 * k / L1));
+    wd[6] = s * (y[2] * (c2 / L1) + y[3] * (-c2 * k / L1));
+}
+
+// ---------------- OBCA block geometry (truck_trailer_model.py:31-72, trajectory_optimization.py:32-53) --------
+struct Geom {
+    double p0, p1, dpt0, dpt1, dpp0, dpp1, ppt0, ppt1, ptp0, ptp1, ppp0, ppp1, ca, sa, angp, hl, hw;
+};
+__device__ __forceinline__ void body_geom(const ObcaArgs& a, const double* xk, int body, Geom& g) {
+    double st, ct;
+    sincos(xk[2], &st, &ct);
+    if (body == 0) {
+        const double h1 = 0.5 * a.L1;
+        g.ca = ct; g.sa = st; g.angp = 0.0; g.hl = 0.5 * a.L1; g.hw = 0.5 * a.W1;
+        g.p0 = xk[0] + h1 * ct; g.p1 = xk[1] + h1 * st;
+        g.dpt0 = -h1 * st; g.dpt1 = h1 * ct;
+        g.dpp0 = 0.0; g.dpp1 = 0.0;
+        g.ppt0 = -h1 * ct; g.ppt1 = -h1 * st;
+        g.ptp0 = g.ptp1 = g.ppp0 = g.ppp1 = 0.0;
+    } else {
+        const double h2 = 0.5 * a.L2, M = a.Mh;
+        double sa, ca;
+        sincos(xk[2] + xk[3], &sa, &ca);
+        g.ca = ca; g.sa = sa; g.angp = 1.0; g.hl = 0.5 * a.L2; g.hw = 0.5 * a.W2;
+        g.p0 = xk[0] - M * ct - h2 * ca; g.p1 = xk[1] - M * st - h2 * sa;
+        g.dpt0 = M * st + h2 * sa; g.dpt1 = -M * ct - h2 * ca;
+        g.dpp0 = h2 * sa; g.dpp1 = -h2 * ca;
+        g.ppt0 = M * ct + h2 * ca; g.ppt1 = M * st + h2 * sa;
+        g.ptp0 = h2 * ca; g.ptp1 = h2 * sa;
+        g.ppp0 = h2 * ca; g.ppp1 = h2 * sa;
+    }
+}
+
+// constraint values of block j (obstacle j>>1, body j&1)
+__device__ __forceinline__ void blk_vals(const ObcaArgs& a, const double* xk, int j, const double* w, double* d) {
+    Geom g;
+    body_geom(a, xk, j & 1, g);
+    const double* ob = a.obs + 4 * (j >> 1);
+    const double ex = g.p0 - ob[0], ey = g.p1 - ob[1], hwo = 0.5 * ob[2], hho = 0.5 * ob[3];
+    const double aa = w[4] - w[6], cc = w[5] - w[7];
+    d[0] = g.hl * (w[0] + w[2]) + g.hw * (w[1] + w[3]) -
+           ((ex - hwo) * w[4] + (ey - hho) * w[5] + (-ex - hwo) * w[6] + (-ey - hho) * w[7]) + a.dmin;
+    d[1] = (w[0] - w[2]) + g.ca * aa + g.sa * cc;
+    d[2] = (w[1] - w[3]) - g.sa * aa + g.ca * cc;
+    d[3] = sqrt(aa * aa + cc * cc) - 1.0;
+}
+
+// Full block linearisation + elimination.  See the header comment and oracle/c/tt_obca.c:block_factor.
+struct Blk {
+    // linearisation
+    double d[4];
+    double jx0[4], e2, e3, angp;     // Jx rows 0..2 (row 3 = 0)
+    double jw0[8], ca, sa, an, cn;   // Jw row 0 + the rotation/normal data of rows 1..3
+    double hl, hw;
+    double hxx22, hxx23, hxx33;
+    double hxl[4][4];                // W_{x lam}: rows X,Y,theta,psi
+    // elimination
+    double dm[4];                    // Sigma_mu + dw (mu block is diagonal)
+    double LL[10];                   // chol of the lam block
+    double Yl[4][4];                 // L^-1 Jw_lam'  [a][r]
+    double Zl[4][4];                 // L^-1 W_lam x  [a][q]
+    double LT[10];                   // chol of T
+    double G[4][4];                  // Y_lam' Z - Jx  [r][q]
+    double D[4];
+};
+
+__device__ __forceinline__ bool chol4(double* L) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double s = L[lo4(j, j)];
+#pragma unroll
+        for (int k = 0; k < j; ++k) s -= L[lo4(j, k)] * L[lo4(j, k)];
+        if (!(s > 0.0)) return false;
+        const double r = sqrt(s), ir = frcp(r);
+        L[lo4(j, j)] = r;
+#pragma unroll
+        for (int i = j + 1; i < 4; ++i) {
+            double t = L[lo4(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; ++k) t -= L[lo4(i, k)] * L[lo4(j, k)];
+            L[lo4(i, j)] = t * ir;
+        }
+    }
+    return true;
+}
+__device__ __forceinline__ void fsub4(const double* L, double* b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        double t = b[i];
+#pragma unroll
+        for (int k = 0; k < i; ++k) t -= L[lo4(i, k)] * b[k];
+        b[i] = t / L[lo4(i, i)];
+    }
+}
+__device__ __forceinline__ void bsub4(const double* L, double* b) {
+#pragma unroll
+    for (int i = 3; i >= 0; --i) {
+        double t = b[i];
+#pragma unroll
+        for (int k = i + 1; k < 4; ++k) t -= L[lo4(k, i)] * b[k];
+        b[i] = t / L[lo4(i, i)];
+    }
+}
+
+__device__ __forceinline__ void blk_lin(const ObcaArgs& a, const double* xk, int j, const double* w, const double* y, Blk& k) {
+    Geom g;
+    body_geom(a, xk, j & 1, g);
+    const double* ob = a.obs + 4 * (j >> 1);
+    const double ex = g.p0 - ob[0], ey = g.p1 - ob[1], hwo = 0.5 * ob[2], hho = 0.5 * ob[3];
+    const double aa = w[4] - w[6], cc = w[5] - w[7];
+    double nr = sqrt(aa * aa + cc * cc);
+    k.d[0] = g.hl * (w[0] + w[2]) + g.hw * (w[1] + w[3]) -
+             ((ex - hwo) * w[4] + (ey - hho) * w[5] + (-ex - hwo) * w[6] + (-ey - hho) * w[7]) + a.dmin;
+    k.d[1] = (w[0] - w[2]) + g.ca * aa + g.sa * cc;
+    k.d[2] = (w[1] - w[3]) - g.sa * aa + g.ca * cc;
+    k.d[3] = nr - 1.0;
+    nr = fmax(nr, 1e-12);
+    const double inr = 1.0 / nr;
+    k.e2 = -g.sa * aa + g.ca * cc;
+    k.e3 = -g.ca * aa - g.sa * cc;
+    k.angp = g.angp;
+    k.jx0[0] = -aa; k.jx0[1] = -cc;
+    k.jx0[2] = -(aa * g.dpt0 + cc * g.dpt1);
+    k.jx0[3] = -(aa * g.dpp0 + cc * g.dpp1);
+    k.hl = g.hl; k.hw = g.hw;
+    k.jw0[0] = g.hl; k.jw0[1] = g.hw; k.jw0[2] = g.hl; k.jw0[3] = g.hw;
+    k.jw0[4] = -(ex - hwo); k.jw0[5] = -(ey - hho); k.jw0[6] = ex + hwo; k.jw0[7] = ey + hho;
+    k.ca = g.ca; k.sa = g.sa; k.an = aa * inr; k.cn = cc * inr;
+    const double y1 = y[0], y2 = y[1], y3 = y[2], y4 = y[3];
+    const double rot = y2 * (-g.ca * aa - g.sa * cc) + y3 * (g.sa * aa - g.ca * cc);
+    k.hxx22 = -y1 * (aa * g.ppt0 + cc * g.ppt1) + rot;
+    k.hxx23 = -y1 * (aa * g.ptp0 + cc * g.ptp1) + rot * g.angp;
+    k.hxx33 = -y1 * (aa * g.ppp0 + cc * g.ppp1) + rot * g.angp;
+    const double r0 = -y2 * g.sa - y3 * g.ca, r1 = y2 * g.ca - y3 * g.sa;
+    k.hxl[0][0] = -y1; k.hxl[0][1] = 0.0; k.hxl[0][2] = y1; k.hxl[0][3] = 0.0;
+    k.hxl[1][0] = 0.0; k.hxl[1][1] = -y1; k.hxl[1][2] = 0.0; k.hxl[1][3] = y1;
+    k.hxl[2][0] = -y1 * g.dpt0 + r0; k.hxl[2][1] = -y1 * g.dpt1 + r1;
+    k.hxl[2][2] = y1 * g.dpt0 - r0;  k.hxl[2][3] = y1 * g.dpt1 - r1;
+    k.hxl[3][0] = -y1 * g.dpp0 + g.angp * r0; k.hxl[3][1] = -y1 * g.dpp1 + g.angp * r1;
+    k.hxl[3][2] = y1 * g.dpp0 - g.angp * r0;  k.hxl[3][3] = y1 * g.dpp1 - g.angp * r1;
+    // lam-lam block y4 T'H4T (into LL, before the diagonal is added)
+    const double n3 = nr * nr * nr, haa = y4 * cc * cc / n3, hac = -y4 * aa * cc / n3, hcc = y4 * aa * aa / n3;
+    // T = [[1,0,-1,0],[0,1,0,-1]]: entries H[i][k] = T0i(haa T0k + hac T1k) + T1i(hac T0k + hcc T1k)
+    const double T0[4] = {1, 0, -1, 0}, T1[4] = {0, 1, 0, -1};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q <= i; ++q)
+            k.LL[lo4(i, q)] = T0[i] * (haa * T0[q] + hac * T1[q]) + T1[i] * (hac * T0[q] + hcc * T1[q]);
+}
+
+// Jx[r][q] (rows 0..3, cols X,Y,theta,psi)
+__device__ __forceinline__ double jx(const Blk& k, int r, int q) {
+    if (r == 0) return k.jx0[q];
+    if (r == 1) return q == 2 ? k.e2 : q == 3 ? k.e2 * k.angp : 0.0;
+    if (r == 2) return q == 2 ? k.e3 : q == 3 ? k.e3 * k.angp : 0.0;
+    return 0.0;
+}
+// Jw[r][4 + a] (lam columns)
+__device__ __forceinline__ double jwl(const Blk& k, int r, int a) {
+    if (r == 0) return k.jw0[4 + a];
+    if (r == 1) { const double v[4] = {k.ca, k.sa, -k.ca, -k.sa}; return v[a]; }
+    if (r == 2) { const double v[4] = {-k.sa, k.ca, k.sa, -k.ca}; return v[a]; }
+    const double v[4] = {k.an, k.cn, -k.an, -k.cn};
+    return v[a];
+}
+// Jw[r][a] (mu columns)
+__device__ __forceinline__ double jwm(const Blk& k, int r, int a) {
+    if (r == 0) return k.jw0[a];
+    if (r == 1) return a == 0 ? 1.0 : a == 2 ? -1.0 : 0.0;
+    if (r == 2) return a == 1 ? 1.0 : a == 3 ? -1.0 : 0.0;
+    return 0.0;
+}
+
+// elimination of a linearised block: returns false when the lam block is not positive definite.
+// sig_w: Sigma of the 8 duals; D: Sigma_s + dw of the 4 rows.  Adds the Schur complement into the
+// stage Hessian contribution C (10 packed lower entries over X,Y,theta,psi).
+__device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double dw, double* C) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        k.dm[i] = sig_w[i] + dw;
+        k.LL[lo4(i, i)] += sig_w[4 + i] + dw;
+    }
+    if (!chol4(k.LL)) return false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double col[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) col[a] = jwl(k, r, a);
+        fsub4(k.LL, col);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) k.Yl[a][r] = col[a];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double col[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) col[a] = k.hxl[q][a];
+        fsub4(k.LL, col);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) k.Zl[a][q] = col[a];
+    }
+    double idm[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) idm[a] = frcp(k.dm[a]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int s = 0; s <= r; ++s) {
+            double t = (r == s) ? frcp(k.D[r]) : 0.0;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) t += jwm(k, r, a) * jwm(k, s, a) * idm[a] + k.Yl[a][r] * k.Yl[a][s];
+            k.LT[lo4(r, s)] = t;
+        }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            double g = -jx(k, r, q);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) g += k.Yl[a][r] * k.Zl[a][q];
+            k.G[r][q] = g;
+        }
+    if (!chol4(k.LT)) return false;
+    double Wm[4][4];  // LT^-1 G
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double col[4] = {k.G[0][q], k.G[1][q], k.G[2][q], k.G[3][q]};
+        fsub4(k.LT, col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Wm[r][q] = col[r];
+    }
+    const double hxx[4][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, k.hxx22, k.hxx23}, {0, 0, k.hxx23, k.hxx33}};
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q <= p; ++q) {
+            double t = hxx[p][q];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) t += Wm[a][p] * Wm[a][q] - k.Zl[a][p] * k.Zl[a][q];
+            C[lo4(p, q)] += t;
+        }
+    return true;
+}
+
+// right-hand side of a factored block.  fw: barrier gradient of the 8 duals; rd: row residual
+// (d - s) + D^-1 grad phi_s.  Returns zf (L^-1-scaled dual gradient: mu part fw/dm, lam part LL^-1 fw),
+// t = T^-1 h, and adds the gradient contribution into q4.
+__device__ __forceinline__ void blk_rhs(const Blk& k, const double* fw, const double* rd, double* zf, double* t, double* q4) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) zf[a] = fw[a] / k.dm[a];
+    double zl[4] = {fw[4], fw[5], fw[6], fw[7]};
+    fsub4(k.LL, zl);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) zf[4 + a] = zl[a];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double h = rd[r];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) h -= jwm(k, r, a) * zf[a] + k.Yl[a][r] * zl[a];
+        t[r] = h;
+    }
+    fsub4(k.LT, t);
+    bsub4(k.LT, t);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        double g = 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) g -= k.Zl[a][p] * zl[a];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g -= k.G[r][p] * t[r];
+        q4[p] += g;
+    }
+}
+
+// recovery: y+ = t - T^-1 G dx^, dw_mu = -(fw_mu + Jw_mu' y+)/dm, dw_lam = -L^-T (zl + Z dx^ + Y y+)
+__device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, const double* zf, const double* t,
+                                            const double* dxh, double* yp, double* dwv) {
+    double g4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += k.G[r][q] * dxh[q];
+        g4[r] = s;
+    }
+    fsub4(k.LT, g4);
+    bsub4(k.LT, g4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) yp[r] = t[r] - g4[r];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        double s = fw[a];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += jwm(k, r, a) * yp[r];
+        dwv[a] = -s / k.dm[a];
+    }
+    double v[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        double s = zf[4 + a];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s += k.Zl[a][q] * dxh[q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s += k.Yl[a][r] * yp[r];
+        v[a] = s;
+    }
+    bsub4(k.LL, v);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dwv[4 + a] = -v[a];
+}
+
+// separating-axis dual certificate (see oracle/c/tt_obca.c:dual_certificate)
+__device__ __forceinline__ void dual_certificate(const ObcaArgs& a, const double* xk, int j, double* w) {
+    Geom g;
+    body_geom(a, xk, j & 1, g);
+    const double* ob = a.obs + 4 * (j >> 1);
+    double best = -INFINITY, b0 = 1.0, b1 = 0.0;
+    for (int c = 0; c < 8; ++c) {
+        const double s = (c & 1) ? -1.0 : 1.0;
+        double n0, n1;
+        if (c < 4) { n0 = (c < 2) ? s : 0.0; n1 = (c < 2) ? 0.0 : s; }
+        else if (c < 6) { n0 = s * g.ca; n1 = s * g.sa; }
+        else { n0 = -s * g.sa; n1 = s * g.ca; }
+        const double mx = -(g.ca * n0 + g.sa * n1), my = -(-g.sa * n0 + g.ca * n1);
+        const double hB = g.hl * fabs(mx) + g.hw * fabs(my);
+        const double hO = n0 * ob[0] + n1 * ob[1] + 0.5 * ob[2] * fabs(n0) + 0.5 * ob[3] * fabs(n1);
+        const double gap = n0 * g.p0 + n1 * g.p1 - hB - hO;
+        if (gap > best) { best = gap; b0 = n0; b1 = n1; }
+    }
+    const double sc = 0.99;
+    const double mx = -(g.ca * b0 + g.sa * b1), my = -(-g.sa * b0 + g.ca * b1);
+    w[0] = sc * fmax(mx, 0.0); w[1] = sc * fmax(my, 0.0); w[2] = sc * fmax(-mx, 0.0); w[3] = sc * fmax(-my, 0.0);
+    w[4] = sc * fmax(b0, 0.0); w[5] = sc * fmax(b1, 0.0); w[6] = sc * fmax(-b0, 0.0); w[7] = sc * fmax(-b1, 0.0);
+}
+
+__device__ __forceinline__ double push_into(double v, double lo, double hi, bool hl, bool hu) {
+    const double k1 = 1e-2, k2 = 1e-2;
+    if (hl && hu) {
+        const double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
+        const double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
+        return fmin(fmax(v, lo + pl), hi - pu);
+    }
+    if (hl) return fmax(v, lo + k1 * fmax(1.0, fabs(lo)));
+    if (hu) return fmin(v, hi - k1 * fmax(1.0, fabs(hi)));
+    return v;
+}
+
+__device__ __forceinline__ void clamp_mult(double& z, double sl, double mu) {
+    const double ks = 1e10;
+    z = fmax(fmin(z, ks * mu / sl), mu / (ks * sl));
+}
+
+// fraction to the boundary helpers
+__device__ __forceinline__ void ftb_lo(double v, double lo, double d, double tau, double& a) {
+    if (d < 0.0) a = fmin(a, -tau * (v - lo) / d);
+}
+__device__ __forceinline__ void ftb_hi(double v, double hi, double d, double tau, double& a) {
+    if (d > 0.0) a = fmin(a, tau * (hi - v) / d);
+}
+
+// ---------------- stage pieces ----------------
+__device__ __forceinline__ void load_x(const Ctx& c, int k, double* x) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = c.S(S_X + i, k);
+}
+__device__ __forceinline__ double stage_cost(const Ctx& c, int k, const double* x, const double* u) {
+    const ObcaArgs& a = *c.a;
+    const double* tg = c.plan() ? c.tgt_x : c.tgt_x + 6 * k;
+    const double sc = (k == c.N && c.plan()) ? a.tfac : 1.0;
+    double e[6], F = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) e[i] = x[i] - tg[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double t = 0.0;
+#pragma unroll
+        for (int j2 = 0; j2 < 6; ++j2) t += 0.5 * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]) * e[j2];
+        F += sc * e[i] * t;
+    }
+    if (k < c.N) {
+        double r0 = u[0] - (c.plan() ? 0.0 : c.tgt_u[2 * k]), r1 = u[1] - (c.plan() ? 0.0 : c.tgt_u[2 * k + 1]);
+        const double R01 = 0.5 * (a.R[1] + a.R[2]);
+        F += r0 * (a.R[0] * r0 + R01 * r1) + r1 * (R01 * r0 + a.R[3] * r1);
+    }
+    return F;
+}
+
+// barrier term sum(log slack) of stage k at a point (x, u, w[j][8], s[j][4]) accumulated into ls;
+// returns false if any slack is not positive
+struct StagePt {
+    double x[6], u[2];
+};
+
+// ---------------- the kernel ----------------
+__global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
+    __shared__ Shared sh;
+    const ObcaArgs& a = args;
+    Ctx c;
+    c.a = &args;
+    c.b = blockIdx.x;
+    c.N = a.N;
+    c.NP = a.N + 1;
+    c.nbk = 2 * a.M;
+    c.tid = threadIdx.x;
+    c.ws = a.ws + (size_t)c.b * obca_ws_doubles(a.N, a.M);
+    c.dt = a.dt;
+    const int N = c.N, NBK = c.nbk, tid = c.tid;
+    const bool plan = a.mode == OBCA_PLAN;
+    c.tgt_x = plan ? a.xgoal + 6 * (size_t)c.b : a.xref + (size_t)c.b * 6 * (N + 1);
+    c.tgt_u = plan ? nullptr : a.uref + (size_t)c.b * 2 * N;
+    const double* xinit = a.x0 + 6 * (size_t)c.b;
+    c.hx = 0;
+    c.hu = 0;
+    for (int i = 0; i < 6; ++i) {
+        const bool l = isfinite(a.xlb[i]) && a.xlb[i] > -1e19, u = isfinite(a.xub[i]) && a.xub[i] < 1e19;
+        c.hx |= (l ? 1 : 0) << i;
+        c.hx |= (u ? 1 : 0) << (8 + i);
+        c.xl[i] = l ? a.xlb[i] - RELAX * fmax(1.0, fabs(a.xlb[i])) : -INFINITY;
+        c.xu[i] = u ? a.xub[i] + RELAX * fmax(1.0, fabs(a.xub[i])) : INFINITY;
+    }
+    for (int i = 0; i < 2; ++i) {
+        const bool l = isfinite(a.ulb[i]) && a.ulb[i] > -1e19, u = isfinite(a.uub[i]) && a.uub[i] < 1e19;
+        c.hu |= (l ? 1 : 0) << i;
+        c.hu |= (u ? 1 : 0) << (8 + i);
+        c.ul[i] = l ? a.ulb[i] - RELAX * fmax(1.0, fabs(a.ulb[i])) : -INFINITY;
+        c.uu[i] = u ? a.uub[i] + RELAX * fmax(1.0, fabs(a.uub[i])) : INFINITY;
+    }
+    c.rlo = -a.eq_tol - RELAX;
+    c.rhi = a.eq_tol + RELAX;
+    c.fL = -a.fin_tol - RELAX;
+    c.fU = a.fin_tol + RELAX;
+    const int st = 8 + 16 * a.M;  // reference z stride per stage
+    const size_t nz = obca_n(N, a.M);
+    const double* zg = a.zg ? a.zg + (size_t)c.b * nz : nullptr;
+
+    // ---------------- initial point ----------------
+    bool infeasible = false;
+    for (int i = 0; i < 6; ++i)
+        if (!isfinite(xinit[i]) || (c.hlx(i) && xinit[i] < c.xl[i]) || (c.hux(i) && xinit[i] > c.xu[i])) infeasible = true;
+    if (tid == 0) sh.nf = 0;
+    for (int k = tid; k <= N; k += T) {
+        double x[6], u[2] = {0.0, 0.0};
+        for (int i = 0; i < 6; ++i) {
+            if (zg) x[i] = zg[(size_t)k * st + i];
+            else if (plan) { const double t = (double)k / N; x[i] = k < N ? (1 - t) * xinit[i] + t * c.tgt_x[i] : c.tgt_x[i]; }
+            else x[i] = c.tgt_x[6 * k + i];
+        }
+        if (k < N) {
+            for (int i = 0; i < 2; ++i) u[i] = zg ? zg[(size_t)k * st + 6 + i] : (plan ? 0.0 : c.tgt_u[2 * k + i]);
+        }
+        const int o = k < N ? 8 : 6;
+        for (int j = 0; j < NBK; ++j) {
+            double w[8];
+            const int ob = j >> 1, bd = j & 1;
+            for (int e = 0; e < 4; ++e) {
+                if (zg) {
+                    w[e] = zg[(size_t)k * st + o + ob * 8 + 4 * bd + e];
+                    w[4 + e] = zg[(size_t)k * st + o + 8 * a.M + ob * 8 + 4 * bd + e];
+                } else {
+                    w[e] = 100.0;
+                    const double pat[4] = {100.0, 105.0, 110.0, 115.0};
+                    w[4 + e] = pat[e];
+                }
+            }
+            if (a.dual_init) dual_certificate(a, x, j, w);
+            for (int e = 0; e < 8; ++e) {
+                w[e] = push_into(w[e], -RELAX, INFINITY, true, false);
+                c.B(B_W + e, j, k) = w[e];
+                c.B(B_ZW + e, j, k) = 1.0;
+            }
+        }
+        if (!infeasible) {
+            for (int i = 0; i < 6; ++i) x[i] = push_into(x[i], c.xl[i], c.xu[i], c.hlx(i), c.hux(i));
+            if (k < N)
+                for (int i = 0; i < 2; ++i) u[i] = push_into(u[i], c.ul[i], c.uu[i], c.hlu(i), c.huu(i));
+        }
+        for (int i = 0; i < 6; ++i) {
+            c.S(S_X + i, k) = x[i];
+            c.S(S_ZLX + i, k) = c.hlx(i) ? 1.0 : 0.0;
+            c.S(S_ZUX + i, k) = c.hux(i) ? 1.0 : 0.0;
+            c.S(S_YC + i, k) = 0.0;
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) {
+                c.S(S_U + i, k) = u[i];
+                c.S(S_ZLU + i, k) = c.hlu(i) ? 1.0 : 0.0;
+                c.S(S_ZUU + i, k) = c.huu(i) ? 1.0 : 0.0;
+            }
+        // slacks = d(x0) pushed into the row bounds; multipliers 1 / 0
+        for (int j = 0; j < NBK; ++j) {
+            double w[8], d[4];
+            for (int e = 0; e < 8; ++e) w[e] = c.B(B_W + e, j, k);
+            blk_vals(a, x, j, w, d);
+            for (int r = 0; r < 4; ++r) {
+                c.B(B_S + r, j, k) = push_into(d[r], c.rL(r), c.rU(r), c.hrl(r), true);
+                c.B(B_VL + r, j, k) = c.hrl(r) ? 1.0 : 0.0;
+                c.B(B_VU + r, j, k) = 1.0;
+                c.B(B_YD + r, j, k) = 0.0;
+            }
+        }
+        if (k == N && plan)
+            for (int i = 0; i < 6; ++i) {
+                sh.sf[i] = push_into(x[i] - c.tgt_x[i], c.fL, c.fU, true, true);
+                sh.vLf[i] = sh.vUf[i] = 1.0;
+                sh.ydf[i] = 0.0;
+            }
+    }
+    __syncthreads();
+
+    int status = 2, iter = 0;
+    double E0 = INFINITY;
+    if (infeasible) {
+        status = 3;
+    } else {
+        // constants for the optimality-error scaling
+        int nxb = 0, nub = 0;
+        for (int i = 0; i < 6; ++i) nxb += c.hlx(i) + c.hux(i);
+        for (int i = 0; i < 2; ++i) nub += c.hlu(i) + c.huu(i);
+        const double n_bounds = (double)(N + 1) * nxb + (double)N * nub + (double)(N + 1) * NBK * 14 + (plan ? 12 : 0);
+        const double n_rows = 6.0 * (N + 1) + 4.0 * (N + 1) * NBK + (plan ? 6 : 0);
+        double mu = 0.1, tau = fmax(0.99, 1.0 - mu), dw_last = 0.0, th_max = 0.0, th_min = 0.0;
+        int acc_count = 0, buf = 0;
+        const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+        for (iter = 0;; ++iter) {
+            // ======== linearise + optimality error + theta/phi at the iterate ========
+            // (values and Jacobians of the dynamics; OBCA row values; stationarity residuals)
+            double red[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dinf, pinf, c0, sy+sz, sz, theta, phi, bad
+            for (int k = tid; k <= N; k += T) {
+                double x[6], u[2] = {0.0, 0.0}, gl[6];
+                load_x(c, k, x);
+                if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
+                // cost gradient
+                {
+                    const double* tg = plan ? c.tgt_x : c.tgt_x + 6 * k;
+                    const double sc = (k == N && plan) ? a.tfac : 1.0;
+                    for (int i = 0; i < 6; ++i) {
+                        double g = 0.0;
+                        for (int j2 = 0; j2 < 6; ++j2) g += 0.5 * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]) * (x[j2] - tg[j2]);
+                        gl[i] = 2.0 * sc * g;
+                        c.S(S_GX + i, k) = gl[i];
+                    }
+                    if (k < N) {
+                        const double r0 = u[0] - (plan ? 0.0 : c.tgt_u[2 * k]), r1 = u[1] - (plan ? 0.0 : c.tgt_u[2 * k + 1]);
+                        const double R01 = 0.5 * (a.R[1] + a.R[2]);
+                        c.S(S_GU, k) = 2.0 * (a.R[0] * r0 + R01 * r1);
+                        c.S(S_GU + 1, k) = 2.0 * (R01 * r0 + a.R[3] * r1);
+                    }
+                }
+                // dynamics residual c_k (k >= 1 reads the previous stage)
+                double ck[6];
+                if (k == 0) {
+                    for (int i = 0; i < 6; ++i) ck[i] = x[i] - xinit[i];
+                } else {
+                    double xp[6], up[2] = {c.S(S_U, k - 1), c.S(S_U + 1, k - 1)}, fo[6];
+                    load_x(c, k - 1, xp);
+                    model_f(a, xp, up, fo);
+                    for (int i = 0; i < 6; ++i) ck[i] = x[i] - (xp[i] + a.dt * fo[i]);
+                }
+                for (int i = 0; i < 6; ++i) {
+                    c.S(S_C + i, k) = ck[i];
+                    red[1] = fmax(red[1], fabs(ck[i]));
+                    red[5] += fabs(ck[i]);
+                }
+                double yk[6], yn[6] = {0, 0, 0, 0, 0, 0};
+                for (int i = 0; i < 6; ++i) yk[i] = c.S(S_YC + i, k);
+                if (k < N) {
+                    for (int i = 0; i < 6; ++i) yn[i] = c.S(S_YC + i, k + 1);
+                    double dj[9], wd[7];
+                    model_lin(a, x, yn, dj, wd);
+                    for (int i = 0; i < 9; ++i) c.S(S_AJ + i, k) = dj[i];
+                    for (int i = 0; i < 7; ++i) c.S(S_WD + i, k) = wd[i];
+                    // gl += y_k - A'y_{k+1}   (A = I + dJ)
+                    for (int i = 0; i < 6; ++i) gl[i] += yk[i] - yn[i];
+                    gl[2] -= dj[0] * yn[0] + dj[2] * yn[1];
+                    gl[3] -= dj[6] * yn[3];
+                    gl[4] -= dj[4] * yn[2] + dj[7] * yn[3];
+                    gl[5] -= dj[1] * yn[0] + dj[3] * yn[1] + dj[5] * yn[2] + dj[8] * yn[3];
+                } else {
+                    for (int i = 0; i < 6; ++i) gl[i] += yk[i];
+                }
+                for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
+                // blocks
+                LogSum lsum;
+                for (int j = 0; j < NBK; ++j) {
+                    double w[8], y[4], zw[8];
+                    for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); }
+                    for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
+                    Blk bk;
+                    blk_lin(a, x, j, w, y, bk);
+                    for (int r = 0; r < 4; ++r) c.B(B_D + r, j, k) = bk.d[r];
+                    // x stationarity: Jx' y
+                    for (int q = 0; q < 4; ++q) {
+                        double s = 0.0;
+                        for (int r = 0; r < 3; ++r) s += jx(bk, r, q) * y[r];
+                        gl[q] += s;
+                    }
+                    // dual stationarity: Jw' y - zw
+                    for (int e = 0; e < 8; ++e) {
+                        double t = -zw[e];
+                        for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * y[r];
+                        red[0] = fmax(red[0], fabs(t));
+                        const double sl = w[e] + RELAX;
+                        red[2] = fmax(red[2], fabs(zw[e] * sl));
+                        red[3] += zw[e];
+                        red[4] += zw[e];
+                        lsum.add(sl);
+                    }
+                    for (int r = 0; r < 4; ++r) {
+                        const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+                        red[0] = fmax(red[0], fabs(-y[r] - vl + vu));
+                        red[1] = fmax(red[1], fabs(bk.d[r] - s));
+                        red[5] += fabs(bk.d[r] - s);
+                        red[3] += fabs(y[r]) + vu;
+                        red[4] += vu;
+                        red[2] = fmax(red[2], fabs(vu * (c.rU(r) - s)));
+                        lsum.add(c.rU(r) - s);
+                        if (c.hrl(r)) {
+                            red[2] = fmax(red[2], fabs(vl * (s - c.rL(r))));
+                            red[3] += vl;
+                            red[4] += vl;
+                            lsum.add(s - c.rL(r));
+                        }
+                    }
+                }
+                if (k == N && plan) {
+                    for (int i = 0; i < 6; ++i) {
+                        gl[i] += sh.ydf[i];
+                        const double dfi = x[i] - c.tgt_x[i];
+                        sh.df[i] = dfi;
+                        red[0] = fmax(red[0], fabs(-sh.ydf[i] - sh.vLf[i] + sh.vUf[i]));
+                        red[1] = fmax(red[1], fabs(dfi - sh.sf[i]));
+                        red[5] += fabs(dfi - sh.sf[i]);
+                        const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
+                        red[2] = fmax(red[2], fmax(fabs(sh.vLf[i] * sl), fabs(sh.vUf[i] * su)));
+                        red[3] += fabs(sh.ydf[i]) + sh.vLf[i] + sh.vUf[i];
+                        red[4] += sh.vLf[i] + sh.vUf[i];
+                        lsum.add(sl);
+                        lsum.add(su);
+                    }
+                }
+                for (int i = 0; i < 6; ++i) {
+                    const double zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
+                    gl[i] += -zl + zu;
+                    red[0] = fmax(red[0], fabs(gl[i]));
+                    if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
+                    if (c.hux(i)) { const double sl = c.xu[i] - x[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
+                }
+                if (k < N)
+                    for (int i = 0; i < 2; ++i) {
+                        const double zl = c.S(S_ZLU + i, k), zu = c.S(S_ZUU + i, k);
+                        const double t = c.S(S_GU + i, k) - a.dt * yn[i == 0 ? 5 : 4] - zl + zu;
+                        red[0] = fmax(red[0], fabs(t));
+                        if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
+                        if (c.huu(i)) { const double sl = c.uu[i] - u[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
+                    }
+                red[6] += stage_cost(c, k, x, u);
+                red[7] += lsum.value();  // sum of log slacks (barrier = -mu * this)
+                if (!isfinite(red[0]) || !isfinite(red[1])) red[0] = INFINITY;
+            }
+            {
+                const int ops[8] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM};
+                wg_reduce(sh, red, ops);
+            }
+            const double dinf = red[0], pinf = red[1], c0 = red[2], syz = red[3], szz = red[4];
+            const double th0 = red[5], cost0 = red[6], logs0 = red[7];
+            if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; break; }
+            const double smax = 100.0;
+            const double sd = fmax(smax, syz / (n_rows + n_bounds)) / smax;
+            const double sc = fmax(smax, szz / n_bounds) / smax;
+            E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
+            if (E0 <= a.tol) { status = 0; break; }
+            if (E0 <= a.acc_tol) {
+                if (++acc_count >= a.acc_iter) { status = 1; break; }
+            } else {
+                acc_count = 0;
+            }
+            if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; break; }
+            // ======== barrier update (monotone) ========
+            for (;;) {
+                if (!(mu > a.tol / 10.0 * 1.0000001)) break;
+                // complementarity vs mu
+                double cm[1] = {0.0};
+                for (int k = tid; k <= N; k += T) {
+                    double m = 0.0;
+                    for (int i = 0; i < 6; ++i) {
+                        const double xv = c.S(S_X + i, k);
+                        if (c.hlx(i)) m = fmax(m, fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
+                        if (c.hux(i)) m = fmax(m, fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
+                    }
+                    if (k < N)
+                        for (int i = 0; i < 2; ++i) {
+                            const double uv = c.S(S_U + i, k);
+                            if (c.hlu(i)) m = fmax(m, fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
+                            if (c.huu(i)) m = fmax(m, fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
+                        }
+                    for (int j = 0; j < NBK; ++j) {
+                        for (int e = 0; e < 8; ++e) m = fmax(m, fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
+                        for (int r = 0; r < 4; ++r) {
+                            const double s = c.B(B_S + r, j, k);
+                            m = fmax(m, fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
+                            if (c.hrl(r)) m = fmax(m, fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
+                        }
+                    }
+                    if (k == N && plan)
+                        for (int i = 0; i < 6; ++i)
+                            m = fmax(m, fmax(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu), fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu)));
+                    cm[0] = fmax(cm[0], m);
+                }
+                const int ops[1] = {R_MAX};
+                wg_reduce(sh, cm, ops);
+                const double Emu = fmax(fmax(dinf / sd, pinf), cm[0] / sc);
+                if (Emu <= kappa_eps * mu) {
+                    mu = fmax(a.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
+                    tau = fmax(0.99, 1.0 - mu);
+                    if (tid == 0) sh.nf = 0;  // IPOPT resets the filter on every barrier update
+                } else {
+                    break;
+                }
+            }
+            // residual arrays of the Newton right-hand side: c, d - s, d_f - s_f
+            for (int k = tid; k <= N; k += T) {
+                for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = c.S(S_C + i, k);
+                for (int j = 0; j < NBK; ++j)
+                    for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = c.B(B_D + r, j, k) - c.B(B_S + r, j, k);
+                if (k == N && plan)
+                    for (int i = 0; i < 6; ++i) sh.dfr[i] = sh.df[i] - sh.sf[i];
+            }
+            // ======== Newton step with inertia correction ========
+            double dw = 0.0;
+            bool ok = false;
+            for (int attempt = 0; attempt < 40; ++attempt) {
+                __syncthreads();
+                // --- stage Hessians + gradients (block eliminations) ---
+                double fail[1] = {0.0};
+                for (int k = tid; k <= N; k += T) {
+                    double x[6];
+                    load_x(c, k, x);
+                    double Qs[21], qv[6];
+                    const double sc = (k == N && plan) ? a.tfac : 1.0;
+                    for (int i = 0; i < 6; ++i)
+                        for (int j2 = i; j2 < 6; ++j2) Qs[sy6(i, j2)] = sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
+                    if (k < N) {
+                        for (int i = 0; i < 6; ++i)
+                            for (int j2 = i; j2 < 6; ++j2) {
+                                const int wi = wd_idx(i, j2);
+                                if (wi >= 0) Qs[sy6(i, j2)] += c.S(S_WD + wi, k);
+                            }
+                    }
+                    for (int i = 0; i < 6; ++i) {
+                        const double xv = x[i], zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
+                        double sg = dw, g = c.S(S_GX + i, k);
+                        if (c.hlx(i)) { sg += zl / (xv - c.xl[i]); g -= mu / (xv - c.xl[i]); }
+                        if (c.hux(i)) { sg += zu / (c.xu[i] - xv); g += mu / (c.xu[i] - xv); }
+                        Qs[sy6(i, i)] += sg;
+                        qv[i] = g;
+                    }
+                    double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
+                    for (int j = 0; j < NBK; ++j) {
+                        double w[8], y[4], sw[8], fw[8], rd[4];
+                        for (int e = 0; e < 8; ++e) {
+                            w[e] = c.B(B_W + e, j, k);
+                            const double sl = w[e] + RELAX;
+                            sw[e] = c.B(B_ZW + e, j, k) / sl;
+                            fw[e] = -mu / sl;
+                        }
+                        for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
+                        Blk bk;
+                        blk_lin(a, x, j, w, y, bk);
+                        for (int r = 0; r < 4; ++r) {
+                            const double s = c.B(B_S + r, j, k), vu = c.B(B_VU + r, j, k);
+                            double sg = vu / (c.rU(r) - s), gs = mu / (c.rU(r) - s);
+                            if (c.hrl(r)) { const double vl = c.B(B_VL + r, j, k); sg += vl / (s - c.rL(r)); gs -= mu / (s - c.rL(r)); }
+                            bk.D[r] = sg + dw;
+                            rd[r] = c.B(B_DR + r, j, k) + gs / bk.D[r];
+                        }
+                        if (!blk_factor(bk, sw, dw, C4)) { fail[0] = 1.0; continue; }
+                        double zf[8], t4[4];
+                        blk_rhs(bk, fw, rd, zf, t4, q4);
+                    }
+                    for (int p = 0; p < 4; ++p) {
+                        for (int q = 0; q <= p; ++q) Qs[sy6(q, p)] += C4[lo4(p, q)];
+                        qv[p] += q4[p];
+                    }
+                    if (k == N && plan)
+                        for (int i = 0; i < 6; ++i) {
+                            const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
+                            const double Df = sh.vLf[i] / sl + sh.vUf[i] / su + dw;
+                            const double gs = -mu / sl + mu / su;
+                            sh.Df[i] = Df;
+                            sh.rf[i] = sh.dfr[i] + gs / Df;
+                            Qs[sy6(i, i)] += Df;
+                            qv[i] += Df * sh.rf[i];
+                        }
+                    for (int i = 0; i < 21; ++i) c.S(S_QT + i, k) = Qs[i];
+                    for (int i = 0; i < 6; ++i) c.S(S_QV + i, k) = qv[i];
+                    if (k < N) {
+                        const double u0 = c.S(S_U, k), u1 = c.S(S_U + 1, k);
+                        double R0 = 2.0 * a.R[0] + dw, R1 = a.R[1] + a.R[2], R3 = 2.0 * a.R[3] + dw;
+                        double g0 = c.S(S_GU, k), g1 = c.S(S_GU + 1, k);
+                        if (c.hlu(0)) { R0 += c.S(S_ZLU, k) / (u0 - c.ul[0]); g0 -= mu / (u0 - c.ul[0]); }
+                        if (c.huu(0)) { R0 += c.S(S_ZUU, k) / (c.uu[0] - u0); g0 += mu / (c.uu[0] - u0); }
+                        if (c.hlu(1)) { R3 += c.S(S_ZLU + 1, k) / (u1 - c.ul[1]); g1 -= mu / (u1 - c.ul[1]); }
+                        if (c.huu(1)) { R3 += c.S(S_ZUU + 1, k) / (c.uu[1] - u1); g1 += mu / (c.uu[1] - u1); }
+                        c.S(S_RT, k) = R0;
+                        c.S(S_RT + 1, k) = R1;
+                        c.S(S_RT + 2, k) = R3;
+                        c.S(S_RV, k) = g0;
+                        c.S(S_RV + 1, k) = g1;
+                    }
+                }
+                {
+                    const int ops[1] = {R_MAX};
+                    wg_reduce(sh, fail, ops);
+                }
+                bool good = fail[0] == 0.0;
+                // --- Riccati backward sweep (wave 0) ---
+                if (good) {
+                    if (tid < 64) riccati(c, sh, true);
+                    __syncthreads();
+                    good = sh.flag == 0;
+                }
+                if (good) { ok = true; break; }
+                dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
+                if (dw > 1e40) break;
+            }
+            if (!ok) { status = 4; break; }
+            if (dw > 0) dw_last = dw;
+            // NOTE: continued in part 2
+        }
+    }
+}
+
+}  // namespace
+}  // namespace ttmpc

@@ -1341,10 +1341,11 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
                 memcpy(o, W->dw, nw_ * 8); o += nw_; memcpy(o, W->ds, ns_ * 8); o += ns_;
                 memcpy(o, W->ycp, nx_ * 8); o += nx_; memcpy(o, W->ydp, ns_ * 8); o += ns_;
                 memcpy(o, W->dsf, 48); o += 6; memcpy(o, W->ydpf, 48);
+                /* c_soc(0) = alpha r(x) + r(x + alpha d), c_soc(p+1) = a_soc(p) c_soc(p) + r(x + a_soc(p) d_soc(p)) */
                 double frs[6] = {0}, a_soc = alpha, th_old = th0;
-                for (size_t i = 0; i < nx_; ++i) W->cr[i] = alpha * W->c[i];
-                for (size_t i = 0; i < ns_; ++i) W->dr[i] = alpha * (W->d[i] - W->s[i]);
-                if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = alpha * (W->df[i] - W->sf[i]);
+                for (size_t i = 0; i < nx_; ++i) W->cr[i] = W->c[i];
+                for (size_t i = 0; i < ns_; ++i) W->dr[i] = W->d[i] - W->s[i];
+                if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = W->df[i] - W->sf[i];
                 int soc_ok = 0;
                 for (int p = 0; p < 4; ++p) {
                     if (p > 0 && tht > 0.99 * th_old) break;
