@@ -19,6 +19,11 @@ namespace {
 struct Handle {
     tt_config cfg;
     double Q[36], R[4], xlb[6], xub[6], ulb[2], uub[2];
+    double obs[4 * ttmpc::kObcaMaxM] = {};
+    // OBCA variants: per-instance solver workspace + host-call staging buffers
+    size_t ocap = 0;
+    double* d_ows = nullptr;
+    double *d_oxg = nullptr, *d_ozg = nullptr, *d_ozo = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
     size_t cap = 0;  // instances the workspace holds
@@ -58,10 +63,39 @@ void free_ws(Handle* h) {
     h->cap = 0;
 }
 
+bool is_obca(const tt_config& c) { return c.variant == TT_VARIANT_TRACK_OBCA || c.variant == TT_VARIANT_OBCA_PLAN; }
+
+void free_ows(Handle* h) {
+    double** dp[] = {&h->d_ows, &h->d_oxg, &h->d_ozg, &h->d_ozo};
+    for (double** p : dp) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    h->ocap = 0;
+}
+
+// OBCA solver workspace for B instances (HBM: ~1.8 MB per instance at N=200, M=6)
+int ensure_ows(Handle* h, int B) {
+    if ((size_t)B <= h->ocap) return 0;
+    free_ows(h);
+    const size_t b = (size_t)B, N = h->cfg.N, M = h->cfg.M, n = ttmpc::obca_n(h->cfg.N, h->cfg.M);
+    hipError_t e = hipMalloc((void**)&h->d_ows, b * ttmpc::obca_ws_doubles(h->cfg.N, h->cfg.M) * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_oxg, b * 6 * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_ozg, b * n * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_ozo, b * n * 8);
+    (void)N; (void)M;
+    if (e != hipSuccess) {
+        free_ows(h);
+        return fail(h, -ENOMEM, "OBCA workspace allocation failed for B=%s", std::to_string(B).c_str());
+    }
+    h->ocap = b;
+    return 0;
+}
+
 int ensure_ws(Handle* h, int B) {
     if ((size_t)B <= h->cap) return 0;
     free_ws(h);
-    const size_t N = h->cfg.N, nz = 8 * N + 6;
+    const size_t N = h->cfg.N, nz = is_obca(h->cfg) ? ttmpc::obca_n(h->cfg.N, h->cfg.M) : 8 * N + 6;
     const size_t cap = (size_t)B;
     hipError_t e = hipSuccess;
 #define ALLOC(p, bytes) \
@@ -88,7 +122,8 @@ int ensure_ws(Handle* h, int B) {
 void defaults(tt_config& c) {
     const bool relaxed = c.variant == TT_VARIANT_NMPC || c.variant == TT_VARIANT_FUZZY;
     // IPOPT options of the reference classes: mpc_control.py:35-39 (defaults tol 1e-8, acceptable
-    // 1e-6 x 15), mpc_control_nmpc.py:36-45 / mpc_control_fuzzy.py:47-58 (tol 1e-3, acc 1e-2 x 5)
+    // 1e-6 x 15), mpc_control_nmpc.py:36-45 / mpc_control_fuzzy.py:47-58 (tol 1e-3, acc 1e-2 x 5),
+    // mpc_control_obs.py:189-193 / trajectory_optimization.py:196-199 (max_iter 5000, IPOPT defaults)
     if (c.tol <= 0) c.tol = relaxed ? 1e-3 : 1e-8;
     if (c.acc_tol <= 0) c.acc_tol = relaxed ? 1e-2 : 1e-6;
     if (c.max_iter <= 0) c.max_iter = relaxed ? 2000 : 5000;
@@ -123,19 +158,28 @@ extern "C" {
 
 int tt_create(const tt_config* cfg, const double* Q, const double* R, const double* xlb, const double* xub,
               const double* ulb, const double* uub, const double* obstacles, int device, void** handle) {
-    (void)obstacles;
     if (!handle) return fail(nullptr, -EINVAL, "handle pointer is NULL%s");
     *handle = nullptr;
     if (!cfg || !Q || !R || !xlb || !xub || !ulb || !uub) return fail(nullptr, -EINVAL, "NULL argument%s");
     if (cfg->nx != 6 || cfg->nu != 2)
         return fail(nullptr, -EINVAL, "truck-trailer model has nx=6, nu=2 (truck_trailer_model.py:4-5)%s");
-    if (cfg->variant == TT_VARIANT_TRACK_OBCA || cfg->variant == TT_VARIANT_OBCA_PLAN)
-        return fail(nullptr, -ENOSYS, "OBCA variants are not in this build%s");
-    if (cfg->variant != TT_VARIANT_TRACK && cfg->variant != TT_VARIANT_NMPC && cfg->variant != TT_VARIANT_FUZZY)
+    const bool obca = is_obca(*cfg);
+    if (!obca && cfg->variant != TT_VARIANT_TRACK && cfg->variant != TT_VARIANT_NMPC && cfg->variant != TT_VARIANT_FUZZY)
         return fail(nullptr, -EINVAL, "unknown variant%s");
-    if (cfg->N < 1 || cfg->N > ttmpc::max_horizon())
+    if (obca) {
+        // mpc_control_obs.py:149 / trajectory_optimization.py:25-26 need at least one obstacle
+        if (cfg->M < 1 || cfg->M > ttmpc::kObcaMaxM)
+            return fail(nullptr, -EINVAL, "OBCA variants need 1 <= M <= %s obstacles",
+                        std::to_string(ttmpc::kObcaMaxM).c_str());
+        if (!obstacles) return fail(nullptr, -EINVAL, "OBCA variants need the obstacle list (M x [cx, cy, w, h])%s");
+        if (cfg->N < 1 || cfg->N > 100000) return fail(nullptr, -EINVAL, "horizon must be in [1, 100000]%s");
+        if (!(cfg->W1 > 0) || !(cfg->W2 > 0)) return fail(nullptr, -EINVAL, "params W1, W2 must be > 0%s");
+        for (int i = 0; i < 4 * cfg->M; ++i)
+            if (!isfinite(obstacles[i])) return fail(nullptr, -EINVAL, "non-finite obstacle entry%s");
+    } else if (cfg->N < 1 || cfg->N > ttmpc::max_horizon()) {
         return fail(nullptr, -EINVAL, "horizon must be in [1, %s] (LDS-resident instance)",
                     std::to_string(ttmpc::max_horizon()).c_str());
+    }
     if (!(cfg->dt > 0) || !(cfg->L1 > 0) || !(cfg->L2 > 0) || !isfinite(cfg->Mh))
         return fail(nullptr, -EINVAL, "params dt, L1, L2 must be > 0 and M finite%s");
     for (int i = 0; i < 6; ++i)
@@ -158,6 +202,7 @@ int tt_create(const tt_config* cfg, const double* Q, const double* R, const doub
     memcpy(h->xub, xub, sizeof h->xub);
     memcpy(h->ulb, ulb, sizeof h->ulb);
     memcpy(h->uub, uub, sizeof h->uub);
+    if (obca) memcpy(h->obs, obstacles, sizeof(double) * 4 * cfg->M);
     h->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -180,6 +225,11 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
     if (B > (1 << 30)) return fail(h, -EINVAL, "B too large%s");
     if (!d_x0 || !d_xref || !d_uref || !d_x_out || !d_u_out || !d_status)
         return fail(h, -EINVAL, "NULL device buffer%s");
+    if (h->cfg.variant == TT_VARIANT_OBCA_PLAN)
+        return fail(h, -EINVAL, "plan handles solve through tt_plan_batch / tt_obca_solve_batch%s");
+    if (h->cfg.variant == TT_VARIANT_TRACK_OBCA)
+        return tt_obca_solve_batch_device(handle, B, d_x0, nullptr, d_xref, d_uref, d_z_guess, d_x_out, d_u_out,
+                                          nullptr, d_status, d_iters, d_kkt_res, stream);
     if (h->cfg.variant == TT_VARIANT_FUZZY && !d_wq_wr)
         return fail(h, -EINVAL, "fuzzy variant needs per-instance weights (mpc_control_fuzzy.py:54-58)%s");
     hipError_t e = hipSetDevice(h->device);
@@ -213,7 +263,7 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     int rc = ensure_ws(h, B);
     if (rc) return rc;
-    const size_t N = h->cfg.N, nz = 8 * N + 6, b = (size_t)B;
+    const size_t N = h->cfg.N, nz = is_obca(h->cfg) ? ttmpc::obca_n(h->cfg.N, h->cfg.M) : 8 * N + 6, b = (size_t)B;
     hipStream_t s = h->stream;
 #define H2D(d, hp, bytes) \
     if (e == hipSuccess) e = hipMemcpyAsync((d), (hp), (bytes), hipMemcpyHostToDevice, s)
@@ -261,10 +311,124 @@ int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_x
 }
 #endif
 
+int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
+                               const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
+                               double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
+    if (!is_obca(h->cfg)) return fail(h, -EINVAL, "handle is not an OBCA variant%s");
+    if (B < 0) return fail(h, -EINVAL, "B must be >= 0%s");
+    if (B == 0) return 0;
+    if (B > (1 << 24)) return fail(h, -EINVAL, "B too large%s");
+    const bool plan = h->cfg.variant == TT_VARIANT_OBCA_PLAN;
+    if (!d_x0 || !d_x_out || !d_u_out || !d_status) return fail(h, -EINVAL, "NULL device buffer%s");
+    if (plan && !d_xgoal) return fail(h, -EINVAL, "plan variant needs the goal states%s");
+    if (!plan && (!d_xref || !d_uref)) return fail(h, -EINVAL, "MPC+OBCA variant needs reference states/inputs%s");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    int rc = ensure_ows(h, B);
+    if (rc) return rc;
+    ttmpc::ObcaArgs a;
+    memset(&a, 0, sizeof a);
+    a.N = h->cfg.N;
+    a.M = h->cfg.M;
+    a.B = B;
+    a.mode = plan ? ttmpc::OBCA_PLAN : ttmpc::OBCA_TRACK;
+    a.max_iter = h->cfg.max_iter;
+    a.acc_iter = h->cfg.acc_iter;
+    a.dual_init = h->cfg.dual_init;
+    a.dt = h->cfg.dt;
+    a.L1 = h->cfg.L1;
+    a.L2 = h->cfg.L2;
+    a.Mh = h->cfg.Mh;
+    a.W1 = h->cfg.W1;
+    a.W2 = h->cfg.W2;
+    a.tol = h->cfg.tol;
+    a.acc_tol = h->cfg.acc_tol;
+    a.dmin = 0.2;      // trajectory_optimization.py:95, mpc_control_obs.py:67
+    a.eq_tol = 1e-5;   // trajectory_optimization.py:136-139
+    a.fin_tol = 1e-2;  // trajectory_optimization.py:172-173
+    a.tfac = plan ? 100.0 : 1.0;  // trajectory_optimization.py:180 / mpc_control_obs.py:39
+    memcpy(a.Q, h->Q, sizeof a.Q);
+    memcpy(a.R, h->R, sizeof a.R);
+    memcpy(a.xlb, h->xlb, sizeof a.xlb);
+    memcpy(a.xub, h->xub, sizeof a.xub);
+    memcpy(a.ulb, h->ulb, sizeof a.ulb);
+    memcpy(a.uub, h->uub, sizeof a.uub);
+    memcpy(a.obs, h->obs, sizeof a.obs);
+    a.x0 = d_x0;
+    a.xgoal = d_xgoal;
+    a.xref = d_xref;
+    a.uref = d_uref;
+    a.zg = d_z_guess;
+    a.xout = d_x_out;
+    a.uout = d_u_out;
+    a.zout = d_z_out;
+    a.status = d_status;
+    a.iters = d_iters;
+    a.kkt = d_kkt_res;
+    a.ws = h->d_ows;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+    e = ttmpc::launch_obca(a, s);
+    if (e != hipSuccess) return hip_fail(h, e, "OBCA kernel launch");
+    return 0;
+}
+
+int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
+                        const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
+                        int* status, int* iters, double* kkt_res) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
+    if (!is_obca(h->cfg)) return fail(h, -EINVAL, "handle is not an OBCA variant%s");
+    if (B < 0) return fail(h, -EINVAL, "B must be >= 0%s");
+    if (B == 0) return 0;
+    const bool plan = h->cfg.variant == TT_VARIANT_OBCA_PLAN;
+    if (!x0 || !status || (plan && !xgoal) || (!plan && (!xref || !uref)))
+        return fail(h, -EINVAL, "NULL host buffer%s");
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    int rc = ensure_ws(h, B);
+    if (rc == 0) rc = ensure_ows(h, B);
+    if (rc) return rc;
+    const size_t N = h->cfg.N, nz = ttmpc::obca_n(h->cfg.N, h->cfg.M), b = (size_t)B;
+    hipStream_t s = h->stream;
+#define H2D(d, hp, bytes) \
+    if (e == hipSuccess) e = hipMemcpyAsync((d), (hp), (bytes), hipMemcpyHostToDevice, s)
+#define D2H(hp, d, bytes) \
+    if (e == hipSuccess) e = hipMemcpyAsync((hp), (d), (bytes), hipMemcpyDeviceToHost, s)
+    H2D(h->d_x0, x0, b * 6 * 8);
+    if (plan) H2D(h->d_oxg, xgoal, b * 6 * 8);
+    if (!plan) {
+        H2D(h->d_xref, xref, b * (N + 1) * 6 * 8);
+        H2D(h->d_uref, uref, b * N * 2 * 8);
+    }
+    if (z_guess) H2D(h->d_ozg, z_guess, b * nz * 8);
+    if (e != hipSuccess) return hip_fail(h, e, "H2D copy");
+    rc = tt_obca_solve_batch_device(h, B, h->d_x0, plan ? h->d_oxg : nullptr, plan ? nullptr : h->d_xref,
+                                    plan ? nullptr : h->d_uref, z_guess ? h->d_ozg : nullptr, h->d_xo, h->d_uo,
+                                    z_out ? h->d_ozo : nullptr, h->d_st, h->d_it, h->d_kkt, s);
+    if (rc) return rc;
+    if (x_out) D2H(x_out, h->d_xo, b * (N + 1) * 6 * 8);
+    if (u_out) D2H(u_out, h->d_uo, b * N * 2 * 8);
+    if (z_out) D2H(z_out, h->d_ozo, b * nz * 8);
+    D2H(status, h->d_st, b * 4);
+    if (iters) D2H(iters, h->d_it, b * 4);
+    if (kkt_res) D2H(kkt_res, h->d_kkt, b * 8);
+#undef H2D
+#undef D2H
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(h, e, "OBCA solve");
+    return 0;
+}
+
 int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess, double* x_out,
                   double* u_out, int* status, int* iters) {
-    (void)B; (void)x0; (void)xgoal; (void)z_guess; (void)x_out; (void)u_out; (void)status; (void)iters;
-    return fail(static_cast<Handle*>(handle), -ENOSYS, "tt_plan_batch (OBCA) is not in this build%s");
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
+    if (h->cfg.variant != TT_VARIANT_OBCA_PLAN) return fail(h, -EINVAL, "tt_plan_batch needs a TT_VARIANT_OBCA_PLAN handle%s");
+    if (!x_out || !u_out) return fail(h, -EINVAL, "NULL host buffer%s");
+    return tt_obca_solve_batch(handle, B, x0, xgoal, nullptr, nullptr, z_guess, x_out, u_out, nullptr, status, iters,
+                               nullptr);
 }
 
 void tt_destroy(void* handle) {
@@ -272,6 +436,7 @@ void tt_destroy(void* handle) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     free_ws(h);
+    free_ows(h);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -283,6 +448,10 @@ const char* tt_last_error(void* handle) {
 
 int tt_lds_bytes(int N) { return ttmpc::lds_bytes(N); }
 int tt_max_horizon(void) { return ttmpc::max_horizon(); }
-const char* tt_version(void) { return "ttmpc 0.1 (gfx950, wave-per-instance Riccati IPM)"; }
+const char* tt_version(void) { return "ttmpc 0.2 (gfx950: wave-per-instance Riccati IPM; workgroup-per-instance OBCA IPM)"; }
+long long tt_obca_n(int N, int M) { return (N < 1 || M < 1) ? -EINVAL : (long long)ttmpc::obca_n(N, M); }
+long long tt_obca_workspace_bytes(int N, int M) {
+    return (N < 1 || M < 1) ? -EINVAL : (long long)(8 * ttmpc::obca_ws_doubles(N, M));
+}
 
 }  // extern "C"

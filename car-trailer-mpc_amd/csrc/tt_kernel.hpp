@@ -71,10 +71,10 @@ struct ObcaArgs {
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
 constexpr int kObcaStageFields = 188;
 constexpr int kObcaBlockFields = 76;
-inline size_t obca_ws_doubles(int N, int M) {
+__host__ __device__ inline size_t obca_ws_doubles(int N, int M) {
     return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
 }
-inline size_t obca_n(int N, int M) { return (size_t)N * (8 + 16 * M) + 6 + 16 * M; }
+__host__ __device__ inline size_t obca_n(int N, int M) { return (size_t)N * (8 + 16 * M) + 6 + 16 * M; }
 
 hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream);
 

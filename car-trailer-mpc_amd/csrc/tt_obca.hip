@@ -56,17 +56,7 @@ __host__ __device__ constexpr int sy6(int i, int j) {
 __host__ __device__ constexpr int lo4(int i, int j) { return i * (i + 1) / 2 + j; }
 
 // dt*J nonzeros: 0:(0,2) 1:(0,5) 2:(1,2) 3:(1,5) 4:(2,4) 5:(2,5) 6:(3,3) 7:(3,4) 8:(3,5)   (A = I + dt J)
-__host__ __device__ constexpr int dj_idx(int r, int c) {
-    return (r == 0 && c == 2) ? 0 : (r == 0 && c == 5) ? 1 : (r == 1 && c == 2) ? 2 : (r == 1 && c == 5) ? 3
-         : (r == 2 && c == 4) ? 4 : (r == 2 && c == 5) ? 5 : (r == 3 && c == 3) ? 6 : (r == 3 && c == 4) ? 7
-         : (r == 3 && c == 5) ? 8 : -1;
-}
 // dynamics curvature nonzeros (symmetric): 0:(2,2) 1:(2,5) 2:(3,3) 3:(3,4) 4:(3,5) 5:(4,4) 6:(4,5)
-__host__ __device__ constexpr int wd_idx(int i, int j) {
-    return i > j ? wd_idx(j, i)
-         : (i == 2 && j == 2) ? 0 : (i == 2 && j == 5) ? 1 : (i == 3 && j == 3) ? 2 : (i == 3 && j == 4) ? 3
-         : (i == 3 && j == 5) ? 4 : (i == 4 && j == 4) ? 5 : (i == 4 && j == 5) ? 6 : -1;
-}
 
 // ---------------- wave / workgroup reductions (DPP inside 16-lane rows, readlane across rows) ----------
 template <int CTRL>
@@ -373,22 +363,21 @@ __device__ __forceinline__ void blk_lin(const ObcaArgs& a, const double* xk, int
 
 // Jx[r][q] (rows 0..3, cols X,Y,theta,psi)
 __device__ __forceinline__ double jx(const Blk& k, int r, int q) {
-    if (r == 0) return k.jx0[q];
+    if (r == 0) return q == 0 ? k.jx0[0] : q == 1 ? k.jx0[1] : q == 2 ? k.jx0[2] : k.jx0[3];
     if (r == 1) return q == 2 ? k.e2 : q == 3 ? k.e2 * k.angp : 0.0;
     if (r == 2) return q == 2 ? k.e3 : q == 3 ? k.e3 * k.angp : 0.0;
     return 0.0;
 }
 // Jw[r][4 + a] (lam columns)
 __device__ __forceinline__ double jwl(const Blk& k, int r, int a) {
-    if (r == 0) return k.jw0[4 + a];
-    if (r == 1) { const double v[4] = {k.ca, k.sa, -k.ca, -k.sa}; return v[a]; }
-    if (r == 2) { const double v[4] = {-k.sa, k.ca, k.sa, -k.ca}; return v[a]; }
-    const double v[4] = {k.an, k.cn, -k.an, -k.cn};
-    return v[a];
+    if (r == 0) return a == 0 ? k.jw0[4] : a == 1 ? k.jw0[5] : a == 2 ? k.jw0[6] : k.jw0[7];
+    if (r == 1) return a == 0 ? k.ca : a == 1 ? k.sa : a == 2 ? -k.ca : -k.sa;
+    if (r == 2) return a == 0 ? -k.sa : a == 1 ? k.ca : a == 2 ? k.sa : -k.ca;
+    return a == 0 ? k.an : a == 1 ? k.cn : a == 2 ? -k.an : -k.cn;
 }
 // Jw[r][a] (mu columns)
 __device__ __forceinline__ double jwm(const Blk& k, int r, int a) {
-    if (r == 0) return k.jw0[a];
+    if (r == 0) return a == 0 ? k.jw0[0] : a == 1 ? k.jw0[1] : a == 2 ? k.jw0[2] : k.jw0[3];
     if (r == 1) return a == 0 ? 1.0 : a == 2 ? -1.0 : 0.0;
     if (r == 2) return a == 1 ? 1.0 : a == 3 ? -1.0 : 0.0;
     return 0.0;
@@ -538,6 +527,7 @@ __device__ __forceinline__ void dual_certificate(const ObcaArgs& a, const double
     body_geom(a, xk, j & 1, g);
     const double* ob = a.obs + 4 * (j >> 1);
     double best = -INFINITY, b0 = 1.0, b1 = 0.0;
+#pragma unroll
     for (int c = 0; c < 8; ++c) {
         const double s = (c & 1) ? -1.0 : 1.0;
         double n0, n1;
@@ -608,14 +598,808 @@ __device__ __forceinline__ double stage_cost(const Ctx& c, int k, const double* 
     return F;
 }
 
-// barrier term sum(log slack) of stage k at a point (x, u, w[j][8], s[j][4]) accumulated into ls;
-// returns false if any slack is not positive
-struct StagePt {
-    double x[6], u[2];
-};
+
+// barrier gradients of the block rows
+__device__ __forceinline__ double sig_row(const Ctx& c, int r, double s, double vl, double vu) {
+    double sg = vu / (c.rU(r) - s);
+    if (c.hrl(r)) sg += vl / (s - c.rL(r));
+    return sg;
+}
+__device__ __forceinline__ double grad_row(const Ctx& c, int r, double s, double mu) {
+    double g = mu / (c.rU(r) - s);
+    if (c.hrl(r)) g -= mu / (s - c.rL(r));
+    return g;
+}
+
+// linearise + factor + rhs of one block at the current iterate; returns false if not positive definite
+__device__ __forceinline__ bool block_setup(const Ctx& c, int j, int k, const double* x, double mu, double dw, Blk& bk,
+                                            double* fw, double* zf, double* t4, double* C4, double* q4) {
+    double w[8], y[4], sw[8], rd[4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        w[e] = c.B(B_W + e, j, k);
+        const double sl = w[e] + RELAX;
+        sw[e] = c.B(B_ZW + e, j, k) / sl;
+        fw[e] = -mu / sl;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
+    blk_lin(*c.a, x, j, w, y, bk);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double s = c.B(B_S + r, j, k);
+        bk.D[r] = sig_row(c, r, s, c.B(B_VL + r, j, k), c.B(B_VU + r, j, k)) + dw;
+        rd[r] = c.B(B_DR + r, j, k) + grad_row(c, r, s, mu) / bk.D[r];
+    }
+    if (!blk_factor(bk, sw, dw, C4)) return false;
+    blk_rhs(bk, fw, rd, zf, t4, q4);
+    return true;
+}
+
+// ======== phase: stage Hessians + gradients (all threads) -> fail flag (uniform) ========
+__device__ __noinline__ bool phase_factor(const Ctx& c, Shared& sh, double mu, double dw) {
+    const ObcaArgs& a = *c.a;
+    const int N = c.N;
+    const bool plan = c.plan();
+    double fail[1] = {0.0};
+    for (int k = c.tid; k <= N; k += T) {
+        double x[6];
+        load_x(c, k, x);
+        double Qs[21], qv[6];
+        const double sc = (k == N && plan) ? a.tfac : 1.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            for (int j2 = i; j2 < 6; ++j2) Qs[sy6(i, j2)] = sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
+        if (k < N) {
+            Qs[sy6(2, 2)] += c.S(S_WD + 0, k);
+            Qs[sy6(2, 5)] += c.S(S_WD + 1, k);
+            Qs[sy6(3, 3)] += c.S(S_WD + 2, k);
+            Qs[sy6(3, 4)] += c.S(S_WD + 3, k);
+            Qs[sy6(3, 5)] += c.S(S_WD + 4, k);
+            Qs[sy6(4, 4)] += c.S(S_WD + 5, k);
+            Qs[sy6(4, 5)] += c.S(S_WD + 6, k);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double xv = x[i];
+            double sg = dw, g = c.S(S_GX + i, k);
+            if (c.hlx(i)) { sg += c.S(S_ZLX + i, k) / (xv - c.xl[i]); g -= mu / (xv - c.xl[i]); }
+            if (c.hux(i)) { sg += c.S(S_ZUX + i, k) / (c.xu[i] - xv); g += mu / (c.xu[i] - xv); }
+            Qs[sy6(i, i)] += sg;
+            qv[i] = g;
+        }
+        double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
+        for (int j = 0; j < c.nbk; ++j) {
+            Blk bk;
+            double fw[8], zf[8], t4[4];
+            if (!block_setup(c, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            for (int q = 0; q <= p; ++q) Qs[sy6(q, p)] += C4[lo4(p, q)];
+            qv[p] += q4[p];
+        }
+        if (k == N && plan)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
+                const double Df = sh.vLf[i] / sl + sh.vUf[i] / su + dw;
+                sh.Df[i] = Df;
+                sh.rf[i] = sh.dfr[i] + (-mu / sl + mu / su) / Df;
+                Qs[sy6(i, i)] += Df;
+                qv[i] += Df * sh.rf[i];
+            }
+#pragma unroll
+        for (int i = 0; i < 21; ++i) c.S(S_QT + i, k) = Qs[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c.S(S_QV + i, k) = qv[i];
+        if (k < N) {
+            const double u0 = c.S(S_U, k), u1 = c.S(S_U + 1, k);
+            double R0 = 2.0 * a.R[0] + dw, R1 = a.R[1] + a.R[2], R3 = 2.0 * a.R[3] + dw;
+            double g0 = c.S(S_GU, k), g1 = c.S(S_GU + 1, k);
+            if (c.hlu(0)) { R0 += c.S(S_ZLU, k) / (u0 - c.ul[0]); g0 -= mu / (u0 - c.ul[0]); }
+            if (c.huu(0)) { R0 += c.S(S_ZUU, k) / (c.uu[0] - u0); g0 += mu / (c.uu[0] - u0); }
+            if (c.hlu(1)) { R3 += c.S(S_ZLU + 1, k) / (u1 - c.ul[1]); g1 -= mu / (u1 - c.ul[1]); }
+            if (c.huu(1)) { R3 += c.S(S_ZUU + 1, k) / (c.uu[1] - u1); g1 += mu / (c.uu[1] - u1); }
+            c.S(S_RT, k) = R0;
+            c.S(S_RT + 1, k) = R1;
+            c.S(S_RT + 2, k) = R3;
+            c.S(S_RV, k) = g0;
+            c.S(S_RV + 1, k) = g1;
+        }
+    }
+    const int ops[1] = {R_MAX};
+    wg_reduce(sh, fail, ops);
+    return fail[0] == 0.0;
+}
+
+// ======== phase: Riccati backward sweep (wave 0).  Sets sh.flag = 1 if an input block is not PD ========
+// P_N = Q~_N; G = R~ + B'PB, H = B'PA, K = -G^-1 H, P_k = Q~_k + A'PA + H'K   (B = dt [e5 e4])
+// vector: p' = p_{k+1} - P_{k+1} c_{k+1}, kff = -G^-1 (r~ + B'p'), p_k = q~_k + A'p' + H'kff
+__device__ __noinline__ void riccati(const Ctx& c, Shared& sh) {
+    const int lane = threadIdx.x, N = c.N;
+    const double dt = c.dt;
+    const int i = lane / 6, j = lane % 6;
+    const bool act = lane < 36;
+    if (act) sh.P[lane] = c.S(S_QT + sy6(i, j), N);
+    if (act && i <= j) c.S(S_P + sy6(i, j), N) = sh.P[lane];
+    double pv = lane < 6 ? c.S(S_QV + lane, N) : 0.0;
+    if (lane < 6) c.S(S_PV + lane, N) = pv;
+    int fail = 0;
+    wave_sync();
+    for (int k = N - 1; k >= 0; --k) {
+        double dj[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) dj[q] = c.S(S_AJ + q, k);
+        double e[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = c.S(S_CR + q, k + 1);
+        // PA = P + P dJ   (column j of dJ: 2:{0,1} 3:{3} 4:{2,3} 5:{0,1,2,3})
+        double pa = 0.0, pp = 0.0;
+        if (act) {
+            const double* Pr = sh.P + 6 * i;
+            pa = Pr[j];
+            if (j == 2) pa += Pr[0] * dj[0] + Pr[1] * dj[2];
+            else if (j == 3) pa += Pr[3] * dj[6];
+            else if (j == 4) pa += Pr[2] * dj[4] + Pr[3] * dj[7];
+            else if (j == 5) pa += Pr[0] * dj[1] + Pr[1] * dj[3] + Pr[2] * dj[5] + Pr[3] * dj[8];
+            sh.PA[lane] = pa;
+        }
+        if (lane < 6) {
+            pp = pv;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) pp -= sh.P[6 * lane + q] * e[q];
+        }
+        wave_sync();
+        const double R0 = c.S(S_RT, k), R1 = c.S(S_RT + 1, k), R3 = c.S(S_RT + 2, k);
+        const double G00 = R0 + dt * dt * sh.P[35], G01 = R1 + dt * dt * sh.P[34], G11 = R3 + dt * dt * sh.P[28];
+        const double g00 = G00, det = G00 * G11 - G01 * G01;
+        if (!(g00 > 0.0) || !(det > 0.0)) fail = 1;
+        const double idet = 1.0 / det;
+        const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
+        // H rows: H0[j] = dt PA[5][j], H1[j] = dt PA[4][j]
+        double Pk = 0.0;
+        if (act && i <= j) {
+            const double* PAc = sh.PA;
+            double at = PAc[6 * i + j];
+            // A'PA = PA + dJ' PA: column i of dJ
+            if (i == 2) at += dj[0] * PAc[0 * 6 + j] + dj[2] * PAc[1 * 6 + j];
+            else if (i == 3) at += dj[6] * PAc[3 * 6 + j];
+            else if (i == 4) at += dj[4] * PAc[2 * 6 + j] + dj[7] * PAc[3 * 6 + j];
+            else if (i == 5) at += dj[1] * PAc[0 * 6 + j] + dj[3] * PAc[1 * 6 + j] + dj[5] * PAc[2 * 6 + j] + dj[8] * PAc[3 * 6 + j];
+            const double H0i = dt * PAc[30 + i], H1i = dt * PAc[24 + i], H0j = dt * PAc[30 + j], H1j = dt * PAc[24 + j];
+            const double K0j = -(Gi00 * H0j + Gi01 * H1j), K1j = -(Gi01 * H0j + Gi11 * H1j);
+            Pk = c.S(S_QT + sy6(i, j), k) + at + H0i * K0j + H1i * K1j;
+        }
+        // vector part
+        const double pp5 = readlane_d(pp, 5), pp4 = readlane_d(pp, 4);
+        double ppl[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, q);
+        const double g0 = c.S(S_RV, k) + dt * pp5, g1 = c.S(S_RV + 1, k) + dt * pp4;
+        const double kf0 = -(Gi00 * g0 + Gi01 * g1), kf1 = -(Gi01 * g0 + Gi11 * g1);
+        double pnew = 0.0;
+        if (lane < 6) {
+            const int r = lane;
+            double at = ppl[r];
+            if (r == 2) at += dj[0] * ppl[0] + dj[2] * ppl[1];
+            else if (r == 3) at += dj[6] * ppl[3];
+            else if (r == 4) at += dj[4] * ppl[2] + dj[7] * ppl[3];
+            else if (r == 5) at += dj[1] * ppl[0] + dj[3] * ppl[1] + dj[5] * ppl[2] + dj[8] * ppl[3];
+            pnew = c.S(S_QV + r, k) + at + dt * sh.PA[30 + r] * kf0 + dt * sh.PA[24 + r] * kf1;
+        }
+        // K, H stored for the forward sweep
+        if (lane < 6) {
+            const double H0 = dt * sh.PA[30 + lane], H1 = dt * sh.PA[24 + lane];
+            c.S(S_H + lane, k) = H0;
+            c.S(S_H + 6 + lane, k) = H1;
+            c.S(S_K + lane, k) = -(Gi00 * H0 + Gi01 * H1);
+            c.S(S_K + 6 + lane, k) = -(Gi01 * H0 + Gi11 * H1);
+        }
+        if (lane == 0) {
+            c.S(S_KF, k) = kf0;
+            c.S(S_KF + 1, k) = kf1;
+            c.S(S_GI, k) = Gi00;
+            c.S(S_GI + 1, k) = Gi01;
+            c.S(S_GI + 2, k) = Gi11;
+        }
+        wave_sync();
+        if (act && i <= j) {
+            sh.P[6 * i + j] = Pk;
+            sh.P[6 * j + i] = Pk;
+            c.S(S_P + sy6(i, j), k) = Pk;
+        }
+        pv = pnew;
+        if (lane < 6) c.S(S_PV + lane, k) = pv;
+        wave_sync();
+    }
+    if (lane == 0) sh.flag = fail;
+}
+
+// ======== phase: forward sweep (wave 0) into step buffer buf ========
+__device__ __noinline__ void forward(const Ctx& c, int buf) {
+    const int lane = threadIdx.x, N = c.N;
+    const double dt = c.dt;
+    double dx = lane < 6 ? -c.S(S_CR + lane, 0) : 0.0;
+    for (int k = 0;; ++k) {
+        double dxv[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) dxv[q] = readlane_d(dx, q);
+        if (lane < 6) {
+            double t = c.S(S_PV + lane, k);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) t += c.S(S_P + sy6(lane, q), k) * dxv[q];
+            c.S(S_YCP + 6 * buf + lane, k) = -t;
+            c.S(S_DX + 6 * buf + lane, k) = dx;
+        }
+        if (k == N) break;
+        double du0 = c.S(S_KF, k), du1 = c.S(S_KF + 1, k);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            du0 += c.S(S_K + q, k) * dxv[q];
+            du1 += c.S(S_K + 6 + q, k) * dxv[q];
+        }
+        if (lane == 0) {
+            c.S(S_DU + 2 * buf, k) = du0;
+            c.S(S_DU + 2 * buf + 1, k) = du1;
+        }
+        if (lane < 6) {
+            const int r = lane;
+            double t = dx - c.S(S_CR + r, k + 1);
+            if (r == 0) t += c.S(S_AJ + 0, k) * dxv[2] + c.S(S_AJ + 1, k) * dxv[5];
+            else if (r == 1) t += c.S(S_AJ + 2, k) * dxv[2] + c.S(S_AJ + 3, k) * dxv[5];
+            else if (r == 2) t += c.S(S_AJ + 4, k) * dxv[4] + c.S(S_AJ + 5, k) * dxv[5];
+            else if (r == 3) t += c.S(S_AJ + 6, k) * dxv[3] + c.S(S_AJ + 7, k) * dxv[4] + c.S(S_AJ + 8, k) * dxv[5];
+            else if (r == 4) t += dt * du1;
+            else t += dt * du0;
+            dx = t;
+        }
+    }
+}
+
+// ======== phase: block step recovery + fraction to boundary + directional derivative ========
+// out: [0] alpha_primal (min), [1] alpha_dual (min), [2] grad phi' d (sum), [3] max relative step
+__device__ __noinline__ void phase_recover(const Ctx& c, Shared& sh, double mu, double dw, double tau, int buf, double (&out)[4]) {
+    const int N = c.N;
+    const bool plan = c.plan();
+    double ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
+    for (int k = c.tid; k <= N; k += T) {
+        double x[6], dx[6];
+        load_x(c, k, x);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dx[i] = c.S(S_DX + 6 * buf + i, k);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double xv = x[i], d = dx[i];
+            double g = c.S(S_GX + i, k);
+            rel = fmax(rel, fabs(d) / (1.0 + fabs(xv)));
+            if (c.hlx(i)) {
+                const double sl = xv - c.xl[i], z = c.S(S_ZLX + i, k);
+                g -= mu / sl;
+                ftb_lo(xv, c.xl[i], d, tau, ap);
+                const double dz = mu / sl - z - z / sl * d;
+                if (dz < 0.0) az = fmin(az, -tau * z / dz);
+            }
+            if (c.hux(i)) {
+                const double sl = c.xu[i] - xv, z = c.S(S_ZUX + i, k);
+                g += mu / sl;
+                ftb_hi(xv, c.xu[i], d, tau, ap);
+                const double dz = mu / sl - z + z / sl * d;
+                if (dz < 0.0) az = fmin(az, -tau * z / dz);
+            }
+            Dm += g * d;
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double uv = c.S(S_U + i, k), d = c.S(S_DU + 2 * buf + i, k);
+                double g = c.S(S_GU + i, k);
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(uv)));
+                if (c.hlu(i)) {
+                    const double sl = uv - c.ul[i], z = c.S(S_ZLU + i, k);
+                    g -= mu / sl;
+                    ftb_lo(uv, c.ul[i], d, tau, ap);
+                    const double dz = mu / sl - z - z / sl * d;
+                    if (dz < 0.0) az = fmin(az, -tau * z / dz);
+                }
+                if (c.huu(i)) {
+                    const double sl = c.uu[i] - uv, z = c.S(S_ZUU + i, k);
+                    g += mu / sl;
+                    ftb_hi(uv, c.uu[i], d, tau, ap);
+                    const double dz = mu / sl - z + z / sl * d;
+                    if (dz < 0.0) az = fmin(az, -tau * z / dz);
+                }
+                Dm += g * d;
+            }
+        double C4[10], q4[4];
+        for (int j = 0; j < c.nbk; ++j) {
+            Blk bk;
+            double fw[8], zf[8], t4[4], yp[4], dwv[8];
+            (void)block_setup(c, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4);
+            blk_recover(bk, fw, zf, t4, dx, yp, dwv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const double wv = c.B(B_W + e, j, k), z = c.B(B_ZW + e, j, k), sl = wv + RELAX, d = dwv[e];
+                c.B(B_DW + 8 * buf + e, j, k) = d;
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(wv)));
+                Dm += fw[e] * d;
+                ftb_lo(wv, -RELAX, d, tau, ap);
+                const double dz = mu / sl - z - z / sl * d;
+                if (dz < 0.0) az = fmin(az, -tau * z / dz);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double s = c.B(B_S + r, j, k);
+                const double gs = grad_row(c, r, s, mu);
+                const double ds = (yp[r] - gs) / bk.D[r];
+                c.B(B_YP + 4 * buf + r, j, k) = yp[r];
+                c.B(B_DS + 4 * buf + r, j, k) = ds;
+                rel = fmax(rel, fabs(ds) / (1.0 + fabs(s)));
+                Dm += gs * ds;
+                const double vu = c.B(B_VU + r, j, k), slu = c.rU(r) - s;
+                ftb_hi(s, c.rU(r), ds, tau, ap);
+                const double dvu = mu / slu - vu + vu / slu * ds;
+                if (dvu < 0.0) az = fmin(az, -tau * vu / dvu);
+                if (c.hrl(r)) {
+                    const double vl = c.B(B_VL + r, j, k), sll = s - c.rL(r);
+                    ftb_lo(s, c.rL(r), ds, tau, ap);
+                    const double dvl = mu / sll - vl - vl / sll * ds;
+                    if (dvl < 0.0) az = fmin(az, -tau * vl / dvl);
+                }
+            }
+        }
+        if (k == N && plan)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
+                const double gs = -mu / sl + mu / su;
+                const double yp = sh.Df[i] * (dx[i] + sh.rf[i]);
+                const double ds = (yp - gs) / sh.Df[i];
+                sh.ydpf[buf][i] = yp;
+                sh.dsf[buf][i] = ds;
+                rel = fmax(rel, fabs(ds) / (1.0 + fabs(sh.sf[i])));
+                Dm += gs * ds;
+                ftb_lo(sh.sf[i], c.fL, ds, tau, ap);
+                ftb_hi(sh.sf[i], c.fU, ds, tau, ap);
+                const double dvl = mu / sl - sh.vLf[i] - sh.vLf[i] / sl * ds;
+                const double dvu = mu / su - sh.vUf[i] + sh.vUf[i] / su * ds;
+                if (dvl < 0.0) az = fmin(az, -tau * sh.vLf[i] / dvl);
+                if (dvu < 0.0) az = fmin(az, -tau * sh.vUf[i] / dvu);
+            }
+    }
+    out[0] = ap; out[1] = az; out[2] = Dm; out[3] = rel;
+    const int ops[4] = {R_MIN, R_MIN, R_SUM, R_MAX};
+    wg_reduce(sh, out, ops);
+}
+
+// ======== phase: trial point x + alpha d (step buffer buf) -> theta, phi (barrier objective), bad ========
+// also stores the trial residuals (for second-order corrections)
+__device__ __noinline__ void phase_trial(const Ctx& c, Shared& sh, double mu, double alpha, int buf, double (&out)[3]) {
+    const ObcaArgs& a = *c.a;
+    const int N = c.N;
+    const bool plan = c.plan();
+    double th = 0.0, F = 0.0, logs = 0.0, bad = 0.0;
+    for (int k = c.tid; k <= N; k += T) {
+        double x[6], u[2] = {0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) x[i] = c.S(S_X + i, k) + alpha * c.S(S_DX + 6 * buf + i, k);
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) u[i] = c.S(S_U + i, k) + alpha * c.S(S_DU + 2 * buf + i, k);
+        LogSum ls;
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; ok &= sl > 0.0; ls.add(sl); }
+            if (c.hux(i)) { const double sl = c.xu[i] - x[i]; ok &= sl > 0.0; ls.add(sl); }
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; ok &= sl > 0.0; ls.add(sl); }
+                if (c.huu(i)) { const double sl = c.uu[i] - u[i]; ok &= sl > 0.0; ls.add(sl); }
+            }
+        // dynamics residual c_{k+1} = x_{k+1} - F(x_k, u_k) (thread k), c_0 = x_0 - x_init
+        if (k == 0)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double cv = x[i] - a.x0[6 * (size_t)c.b + i];
+                c.S(S_CT + i, 0) = cv;
+                th += fabs(cv);
+            }
+        if (k < N) {
+            double fo[6];
+            model_f(a, x, u, fo);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double xn = c.S(S_X + i, k + 1) + alpha * c.S(S_DX + 6 * buf + i, k + 1);
+                const double cv = xn - (x[i] + a.dt * fo[i]);
+                c.S(S_CT + i, k + 1) = cv;
+                th += fabs(cv);
+            }
+        }
+        for (int j = 0; j < c.nbk; ++j) {
+            double w[8], d[4];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                w[e] = c.B(B_W + e, j, k) + alpha * c.B(B_DW + 8 * buf + e, j, k);
+                const double sl = w[e] + RELAX;
+                ok &= sl > 0.0;
+                ls.add(sl);
+            }
+            blk_vals(a, x, j, w, d);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double s = c.B(B_S + r, j, k) + alpha * c.B(B_DS + 4 * buf + r, j, k);
+                const double res = d[r] - s;
+                c.B(B_DT + r, j, k) = res;
+                th += fabs(res);
+                const double su = c.rU(r) - s;
+                ok &= su > 0.0;
+                ls.add(su);
+                if (c.hrl(r)) { const double sl = s - c.rL(r); ok &= sl > 0.0; ls.add(sl); }
+            }
+        }
+        if (k == N && plan)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double s = sh.sf[i] + alpha * sh.dsf[buf][i];
+                const double res = (x[i] - c.tgt_x[i]) - s;
+                sh.dft[i] = res;
+                th += fabs(res);
+                const double sl = s - c.fL, su = c.fU - s;
+                ok &= sl > 0.0 && su > 0.0;
+                ls.add(sl);
+                ls.add(su);
+            }
+        F += stage_cost(c, k, x, u);
+        if (!ok) bad = 1.0;
+        else logs += ls.value();
+    }
+    double v[4] = {th, F, logs, bad};
+    const int ops[4] = {R_SUM, R_SUM, R_SUM, R_MAX};
+    wg_reduce(sh, v, ops);
+    out[0] = v[3] > 0.0 ? INFINITY : v[0];
+    out[1] = v[3] > 0.0 ? INFINITY : v[1] - mu * v[2];
+    out[2] = v[3];
+}
+
+// ======== phase: second-order-correction residual r <- a_soc r + r(trial) ========
+__device__ __noinline__ void phase_soc_resid(const Ctx& c, Shared& sh, double a_soc) {
+    for (int k = c.tid; k <= c.N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = a_soc * c.S(S_CR + i, k) + c.S(S_CT + i, k);
+        for (int j = 0; j < c.nbk; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = a_soc * c.B(B_DR + r, j, k) + c.B(B_DT + r, j, k);
+        if (k == c.N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) sh.dfr[i] = a_soc * sh.dfr[i] + sh.dft[i];
+    }
+}
+
+// ======== phase: accept the step ========
+__device__ __noinline__ void phase_update(const Ctx& c, Shared& sh, double mu, double alpha, double az, int buf) {
+    const int N = c.N;
+    for (int k = c.tid; k <= N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double x = c.S(S_X + i, k), d = c.S(S_DX + 6 * buf + i, k);
+            const double xn = x + alpha * d;
+            if (c.hlx(i)) {
+                const double sl = x - c.xl[i], z = c.S(S_ZLX + i, k);
+                double zn = z + az * (mu / sl - z - z / sl * d);
+                clamp_mult(zn, xn - c.xl[i], mu);
+                c.S(S_ZLX + i, k) = zn;
+            }
+            if (c.hux(i)) {
+                const double sl = c.xu[i] - x, z = c.S(S_ZUX + i, k);
+                double zn = z + az * (mu / sl - z + z / sl * d);
+                clamp_mult(zn, c.xu[i] - xn, mu);
+                c.S(S_ZUX + i, k) = zn;
+            }
+            c.S(S_X + i, k) = xn;
+            const double y = c.S(S_YC + i, k);
+            c.S(S_YC + i, k) = y + alpha * (c.S(S_YCP + 6 * buf + i, k) - y);
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double u = c.S(S_U + i, k), d = c.S(S_DU + 2 * buf + i, k);
+                const double un = u + alpha * d;
+                if (c.hlu(i)) {
+                    const double sl = u - c.ul[i], z = c.S(S_ZLU + i, k);
+                    double zn = z + az * (mu / sl - z - z / sl * d);
+                    clamp_mult(zn, un - c.ul[i], mu);
+                    c.S(S_ZLU + i, k) = zn;
+                }
+                if (c.huu(i)) {
+                    const double sl = c.uu[i] - u, z = c.S(S_ZUU + i, k);
+                    double zn = z + az * (mu / sl - z + z / sl * d);
+                    clamp_mult(zn, c.uu[i] - un, mu);
+                    c.S(S_ZUU + i, k) = zn;
+                }
+                c.S(S_U + i, k) = un;
+            }
+        for (int j = 0; j < c.nbk; ++j) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const double w = c.B(B_W + e, j, k), d = c.B(B_DW + 8 * buf + e, j, k), z = c.B(B_ZW + e, j, k);
+                const double sl = w + RELAX, wn = w + alpha * d;
+                double zn = z + az * (mu / sl - z - z / sl * d);
+                clamp_mult(zn, wn + RELAX, mu);
+                c.B(B_W + e, j, k) = wn;
+                c.B(B_ZW + e, j, k) = zn;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double s = c.B(B_S + r, j, k), d = c.B(B_DS + 4 * buf + r, j, k), sn = s + alpha * d;
+                const double vu = c.B(B_VU + r, j, k), slu = c.rU(r) - s;
+                double vun = vu + az * (mu / slu - vu + vu / slu * d);
+                clamp_mult(vun, c.rU(r) - sn, mu);
+                c.B(B_VU + r, j, k) = vun;
+                if (c.hrl(r)) {
+                    const double vl = c.B(B_VL + r, j, k), sll = s - c.rL(r);
+                    double vln = vl + az * (mu / sll - vl - vl / sll * d);
+                    clamp_mult(vln, sn - c.rL(r), mu);
+                    c.B(B_VL + r, j, k) = vln;
+                }
+                c.B(B_S + r, j, k) = sn;
+                const double y = c.B(B_YD + r, j, k);
+                c.B(B_YD + r, j, k) = y + alpha * (c.B(B_YP + 4 * buf + r, j, k) - y);
+            }
+        }
+        if (k == N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double s = sh.sf[i], d = sh.dsf[buf][i], sn = s + alpha * d;
+                const double sl = s - c.fL, su = c.fU - s;
+                double vl = sh.vLf[i] + az * (mu / sl - sh.vLf[i] - sh.vLf[i] / sl * d);
+                double vu = sh.vUf[i] + az * (mu / su - sh.vUf[i] + sh.vUf[i] / su * d);
+                clamp_mult(vl, sn - c.fL, mu);
+                clamp_mult(vu, c.fU - sn, mu);
+                sh.vLf[i] = vl;
+                sh.vUf[i] = vu;
+                sh.sf[i] = sn;
+                sh.ydf[i] += alpha * (sh.ydpf[buf][i] - sh.ydf[i]);
+            }
+    }
+}
+
+__device__ __forceinline__ bool in_filter(const Shared& sh, double th, double ph) {
+    for (int i = 0; i < sh.nf; ++i)
+        if (th >= sh.fth[i] && ph >= sh.fph[i]) return true;
+    return false;
+}
+__device__ __forceinline__ void add_filter(Shared& sh, double th, double ph) {  // thread 0 only
+    int j = 0;
+    for (int i = 0; i < sh.nf; ++i)
+        if (!(sh.fth[i] >= th && sh.fph[i] >= ph)) { sh.fth[j] = sh.fth[i]; sh.fph[j] = sh.fph[i]; ++j; }
+    if (j == kObcaMaxFilter) {
+        for (int i = 0; i + 1 < kObcaMaxFilter; ++i) { sh.fth[i] = sh.fth[i + 1]; sh.fph[i] = sh.fph[i + 1]; }
+        --j;
+    }
+    sh.fth[j] = th;
+    sh.fph[j] = ph;
+    sh.nf = j + 1;
+}
+
+// ======== phase: linearisation at the iterate + optimality-error ingredients ========
+// out: [0] dual inf (max) [1] primal inf (max) [2] complementarity (max) [3] sum |y| + sum z
+//      [4] sum z [5] theta = l1 infeasibility [6] cost [7] sum log slacks
+__device__ __noinline__ void phase_lin(const Ctx& c, Shared& sh, double (&red)[8]) {
+    const ObcaArgs& a = *c.a;
+    const int N = c.N;
+    const bool plan = c.plan();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[i] = 0.0;
+    const double* xinit = a.x0 + 6 * (size_t)c.b;
+    for (int k = c.tid; k <= N; k += T) {
+        double x[6], u[2] = {0.0, 0.0}, gl[6];
+        load_x(c, k, x);
+        if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
+        {
+            const double* tg = plan ? c.tgt_x : c.tgt_x + 6 * k;
+            const double sc = (k == N && plan) ? a.tfac : 1.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double g = 0.0;
+#pragma unroll
+                for (int j2 = 0; j2 < 6; ++j2) g += 0.5 * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]) * (x[j2] - tg[j2]);
+                gl[i] = 2.0 * sc * g;
+                c.S(S_GX + i, k) = gl[i];
+            }
+            if (k < N) {
+                const double r0 = u[0] - (plan ? 0.0 : c.tgt_u[2 * k]), r1 = u[1] - (plan ? 0.0 : c.tgt_u[2 * k + 1]);
+                const double R01 = 0.5 * (a.R[1] + a.R[2]);
+                c.S(S_GU, k) = 2.0 * (a.R[0] * r0 + R01 * r1);
+                c.S(S_GU + 1, k) = 2.0 * (R01 * r0 + a.R[3] * r1);
+            }
+        }
+        double ck[6];
+        if (k == 0) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ck[i] = x[i] - xinit[i];
+        } else {
+            double xp[6], up[2] = {c.S(S_U, k - 1), c.S(S_U + 1, k - 1)}, fo[6];
+            load_x(c, k - 1, xp);
+            model_f(a, xp, up, fo);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ck[i] = x[i] - (xp[i] + a.dt * fo[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            c.S(S_C + i, k) = ck[i];
+            red[1] = fmax(red[1], fabs(ck[i]));
+            red[5] += fabs(ck[i]);
+        }
+        double yk[6], yn[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) yk[i] = c.S(S_YC + i, k);
+        if (k < N) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) yn[i] = c.S(S_YC + i, k + 1);
+            double dj[9], wd[7];
+            model_lin(a, x, yn, dj, wd);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) c.S(S_AJ + i, k) = dj[i];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) c.S(S_WD + i, k) = wd[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) gl[i] += yk[i] - yn[i];
+            gl[2] -= dj[0] * yn[0] + dj[2] * yn[1];
+            gl[3] -= dj[6] * yn[3];
+            gl[4] -= dj[4] * yn[2] + dj[7] * yn[3];
+            gl[5] -= dj[1] * yn[0] + dj[3] * yn[1] + dj[5] * yn[2] + dj[8] * yn[3];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) gl[i] += yk[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
+        LogSum lsum;
+        for (int j = 0; j < c.nbk; ++j) {
+            double w[8], y[4], zw[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
+            Blk bk;
+            blk_lin(a, x, j, w, y, bk);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c.B(B_D + r, j, k) = bk.d[r];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                double s = 0.0;
+#pragma unroll
+                for (int r = 0; r < 3; ++r) s += jx(bk, r, q) * y[r];
+                gl[q] += s;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                double t = -zw[e];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * y[r];
+                red[0] = fmax(red[0], fabs(t));
+                const double sl = w[e] + RELAX;
+                red[2] = fmax(red[2], fabs(zw[e] * sl));
+                red[3] += zw[e];
+                red[4] += zw[e];
+                lsum.add(sl);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+                red[0] = fmax(red[0], fabs(-y[r] - vl + vu));
+                red[1] = fmax(red[1], fabs(bk.d[r] - s));
+                red[5] += fabs(bk.d[r] - s);
+                red[3] += fabs(y[r]) + vu;
+                red[4] += vu;
+                red[2] = fmax(red[2], fabs(vu * (c.rU(r) - s)));
+                lsum.add(c.rU(r) - s);
+                if (c.hrl(r)) {
+                    red[2] = fmax(red[2], fabs(vl * (s - c.rL(r))));
+                    red[3] += vl;
+                    red[4] += vl;
+                    lsum.add(s - c.rL(r));
+                }
+            }
+        }
+        if (k == N && plan)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                gl[i] += sh.ydf[i];
+                const double dfi = x[i] - c.tgt_x[i];
+                sh.df[i] = dfi;
+                red[0] = fmax(red[0], fabs(-sh.ydf[i] - sh.vLf[i] + sh.vUf[i]));
+                red[1] = fmax(red[1], fabs(dfi - sh.sf[i]));
+                red[5] += fabs(dfi - sh.sf[i]);
+                const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
+                red[2] = fmax(red[2], fmax(fabs(sh.vLf[i] * sl), fabs(sh.vUf[i] * su)));
+                red[3] += fabs(sh.ydf[i]) + sh.vLf[i] + sh.vUf[i];
+                red[4] += sh.vLf[i] + sh.vUf[i];
+                lsum.add(sl);
+                lsum.add(su);
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
+            gl[i] += -zl + zu;
+            red[0] = fmax(red[0], fabs(gl[i]));
+            if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
+            if (c.hux(i)) { const double sl = c.xu[i] - x[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double zl = c.S(S_ZLU + i, k), zu = c.S(S_ZUU + i, k);
+                const double t = c.S(S_GU + i, k) - a.dt * yn[i == 0 ? 5 : 4] - zl + zu;
+                red[0] = fmax(red[0], fabs(t));
+                if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
+                if (c.huu(i)) { const double sl = c.uu[i] - u[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
+            }
+        red[6] += stage_cost(c, k, x, u);
+        red[7] += lsum.value();
+        if (!isfinite(red[0]) || !isfinite(red[1])) red[0] = INFINITY;
+    }
+    const int ops[8] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM};
+    wg_reduce(sh, red, ops);
+}
+
+// ======== phase: complementarity vs mu (max |z s - mu|) ========
+__device__ __noinline__ double phase_compl(const Ctx& c, Shared& sh, double mu) {
+    const int N = c.N;
+    double cm[1] = {0.0};
+    for (int k = c.tid; k <= N; k += T) {
+        double m = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double xv = c.S(S_X + i, k);
+            if (c.hlx(i)) m = fmax(m, fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
+            if (c.hux(i)) m = fmax(m, fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double uv = c.S(S_U + i, k);
+                if (c.hlu(i)) m = fmax(m, fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
+                if (c.huu(i)) m = fmax(m, fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
+            }
+        for (int j = 0; j < c.nbk; ++j) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) m = fmax(m, fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double s = c.B(B_S + r, j, k);
+                m = fmax(m, fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
+                if (c.hrl(r)) m = fmax(m, fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
+            }
+        }
+        if (k == N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                m = fmax(m, fmax(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu), fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu)));
+        cm[0] = fmax(cm[0], m);
+    }
+    const int ops[1] = {R_MAX};
+    wg_reduce(sh, cm, ops);
+    return cm[0];
+}
+
+// Newton solve for the current residual arrays (S_CR / B_DR / sh.dfr) with the given dw into buffer buf.
+// Returns false when the Riccati/blocks are not positive definite.
+__device__ bool newton_solve(const Ctx& c, Shared& sh, double mu, double dw, int buf) {
+    if (!phase_factor(c, sh, mu, dw)) return false;
+    if (threadIdx.x < 64) riccati(c, sh);
+    __syncthreads();
+    if (sh.flag) return false;
+    if (threadIdx.x < 64) forward(c, buf);
+    __syncthreads();
+    return true;
+}
 
 // ---------------- the kernel ----------------
-__global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void obca_kernel(ObcaArgs args) {
     __shared__ Shared sh;
     const ObcaArgs& a = args;
     Ctx c;
@@ -634,6 +1418,7 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
     const double* xinit = a.x0 + 6 * (size_t)c.b;
     c.hx = 0;
     c.hu = 0;
+#pragma unroll
     for (int i = 0; i < 6; ++i) {
         const bool l = isfinite(a.xlb[i]) && a.xlb[i] > -1e19, u = isfinite(a.xub[i]) && a.xub[i] < 1e19;
         c.hx |= (l ? 1 : 0) << i;
@@ -641,6 +1426,7 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
         c.xl[i] = l ? a.xlb[i] - RELAX * fmax(1.0, fabs(a.xlb[i])) : -INFINITY;
         c.xu[i] = u ? a.xub[i] + RELAX * fmax(1.0, fabs(a.xub[i])) : INFINITY;
     }
+#pragma unroll
     for (int i = 0; i < 2; ++i) {
         const bool l = isfinite(a.ulb[i]) && a.ulb[i] > -1e19, u = isfinite(a.uub[i]) && a.uub[i] < 1e19;
         c.hu |= (l ? 1 : 0) << i;
@@ -652,51 +1438,56 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
     c.rhi = a.eq_tol + RELAX;
     c.fL = -a.fin_tol - RELAX;
     c.fU = a.fin_tol + RELAX;
-    const int st = 8 + 16 * a.M;  // reference z stride per stage
+    const int st = 8 + 16 * a.M;
     const size_t nz = obca_n(N, a.M);
     const double* zg = a.zg ? a.zg + (size_t)c.b * nz : nullptr;
 
-    // ---------------- initial point ----------------
+    // ---------------- initial point (bound push, slacks = pushed d(x0), multipliers 1 / 0) ----------------
     bool infeasible = false;
+#pragma unroll
     for (int i = 0; i < 6; ++i)
         if (!isfinite(xinit[i]) || (c.hlx(i) && xinit[i] < c.xl[i]) || (c.hux(i) && xinit[i] > c.xu[i])) infeasible = true;
     if (tid == 0) sh.nf = 0;
     for (int k = tid; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0};
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
             if (zg) x[i] = zg[(size_t)k * st + i];
             else if (plan) { const double t = (double)k / N; x[i] = k < N ? (1 - t) * xinit[i] + t * c.tgt_x[i] : c.tgt_x[i]; }
             else x[i] = c.tgt_x[6 * k + i];
         }
-        if (k < N) {
+        if (k < N)
+#pragma unroll
             for (int i = 0; i < 2; ++i) u[i] = zg ? zg[(size_t)k * st + 6 + i] : (plan ? 0.0 : c.tgt_u[2 * k + i]);
-        }
         const int o = k < N ? 8 : 6;
         for (int j = 0; j < NBK; ++j) {
             double w[8];
             const int ob = j >> 1, bd = j & 1;
+#pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (zg) {
                     w[e] = zg[(size_t)k * st + o + ob * 8 + 4 * bd + e];
                     w[4 + e] = zg[(size_t)k * st + o + 8 * a.M + ob * 8 + 4 * bd + e];
                 } else {
                     w[e] = 100.0;
-                    const double pat[4] = {100.0, 105.0, 110.0, 115.0};
-                    w[4 + e] = pat[e];
+                    w[4 + e] = 100.0 + 5.0 * e;  // kron(1_M, [100,105,110,115,...]) (trajectory_optimization.py:222)
                 }
             }
             if (a.dual_init) dual_certificate(a, x, j, w);
+#pragma unroll
             for (int e = 0; e < 8; ++e) {
-                w[e] = push_into(w[e], -RELAX, INFINITY, true, false);
-                c.B(B_W + e, j, k) = w[e];
+                c.B(B_W + e, j, k) = push_into(w[e], -RELAX, INFINITY, true, false);
                 c.B(B_ZW + e, j, k) = 1.0;
             }
         }
         if (!infeasible) {
+#pragma unroll
             for (int i = 0; i < 6; ++i) x[i] = push_into(x[i], c.xl[i], c.xu[i], c.hlx(i), c.hux(i));
             if (k < N)
+#pragma unroll
                 for (int i = 0; i < 2; ++i) u[i] = push_into(u[i], c.ul[i], c.uu[i], c.hlu(i), c.huu(i));
         }
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
             c.S(S_X + i, k) = x[i];
             c.S(S_ZLX + i, k) = c.hlx(i) ? 1.0 : 0.0;
@@ -704,16 +1495,18 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
             c.S(S_YC + i, k) = 0.0;
         }
         if (k < N)
+#pragma unroll
             for (int i = 0; i < 2; ++i) {
                 c.S(S_U + i, k) = u[i];
                 c.S(S_ZLU + i, k) = c.hlu(i) ? 1.0 : 0.0;
                 c.S(S_ZUU + i, k) = c.huu(i) ? 1.0 : 0.0;
             }
-        // slacks = d(x0) pushed into the row bounds; multipliers 1 / 0
         for (int j = 0; j < NBK; ++j) {
             double w[8], d[4];
+#pragma unroll
             for (int e = 0; e < 8; ++e) w[e] = c.B(B_W + e, j, k);
             blk_vals(a, x, j, w, d);
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
                 c.B(B_S + r, j, k) = push_into(d[r], c.rL(r), c.rU(r), c.hrl(r), true);
                 c.B(B_VL + r, j, k) = c.hrl(r) ? 1.0 : 0.0;
@@ -722,6 +1515,7 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
             }
         }
         if (k == N && plan)
+#pragma unroll
             for (int i = 0; i < 6; ++i) {
                 sh.sf[i] = push_into(x[i] - c.tgt_x[i], c.fL, c.fU, true, true);
                 sh.vLf[i] = sh.vUf[i] = 1.0;
@@ -735,161 +1529,26 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
     if (infeasible) {
         status = 3;
     } else {
-        // constants for the optimality-error scaling
         int nxb = 0, nub = 0;
+#pragma unroll
         for (int i = 0; i < 6; ++i) nxb += c.hlx(i) + c.hux(i);
+#pragma unroll
         for (int i = 0; i < 2; ++i) nub += c.hlu(i) + c.huu(i);
         const double n_bounds = (double)(N + 1) * nxb + (double)N * nub + (double)(N + 1) * NBK * 14 + (plan ? 12 : 0);
         const double n_rows = 6.0 * (N + 1) + 4.0 * (N + 1) * NBK + (plan ? 6 : 0);
         double mu = 0.1, tau = fmax(0.99, 1.0 - mu), dw_last = 0.0, th_max = 0.0, th_min = 0.0;
-        int acc_count = 0, buf = 0;
+        int acc_count = 0;
         const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+        const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
         for (iter = 0;; ++iter) {
-            // ======== linearise + optimality error + theta/phi at the iterate ========
-            // (values and Jacobians of the dynamics; OBCA row values; stationarity residuals)
-            double red[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dinf, pinf, c0, sy+sz, sz, theta, phi, bad
-            for (int k = tid; k <= N; k += T) {
-                double x[6], u[2] = {0.0, 0.0}, gl[6];
-                load_x(c, k, x);
-                if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
-                // cost gradient
-                {
-                    const double* tg = plan ? c.tgt_x : c.tgt_x + 6 * k;
-                    const double sc = (k == N && plan) ? a.tfac : 1.0;
-                    for (int i = 0; i < 6; ++i) {
-                        double g = 0.0;
-                        for (int j2 = 0; j2 < 6; ++j2) g += 0.5 * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]) * (x[j2] - tg[j2]);
-                        gl[i] = 2.0 * sc * g;
-                        c.S(S_GX + i, k) = gl[i];
-                    }
-                    if (k < N) {
-                        const double r0 = u[0] - (plan ? 0.0 : c.tgt_u[2 * k]), r1 = u[1] - (plan ? 0.0 : c.tgt_u[2 * k + 1]);
-                        const double R01 = 0.5 * (a.R[1] + a.R[2]);
-                        c.S(S_GU, k) = 2.0 * (a.R[0] * r0 + R01 * r1);
-                        c.S(S_GU + 1, k) = 2.0 * (R01 * r0 + a.R[3] * r1);
-                    }
-                }
-                // dynamics residual c_k (k >= 1 reads the previous stage)
-                double ck[6];
-                if (k == 0) {
-                    for (int i = 0; i < 6; ++i) ck[i] = x[i] - xinit[i];
-                } else {
-                    double xp[6], up[2] = {c.S(S_U, k - 1), c.S(S_U + 1, k - 1)}, fo[6];
-                    load_x(c, k - 1, xp);
-                    model_f(a, xp, up, fo);
-                    for (int i = 0; i < 6; ++i) ck[i] = x[i] - (xp[i] + a.dt * fo[i]);
-                }
-                for (int i = 0; i < 6; ++i) {
-                    c.S(S_C + i, k) = ck[i];
-                    red[1] = fmax(red[1], fabs(ck[i]));
-                    red[5] += fabs(ck[i]);
-                }
-                double yk[6], yn[6] = {0, 0, 0, 0, 0, 0};
-                for (int i = 0; i < 6; ++i) yk[i] = c.S(S_YC + i, k);
-                if (k < N) {
-                    for (int i = 0; i < 6; ++i) yn[i] = c.S(S_YC + i, k + 1);
-                    double dj[9], wd[7];
-                    model_lin(a, x, yn, dj, wd);
-                    for (int i = 0; i < 9; ++i) c.S(S_AJ + i, k) = dj[i];
-                    for (int i = 0; i < 7; ++i) c.S(S_WD + i, k) = wd[i];
-                    // gl += y_k - A'y_{k+1}   (A = I + dJ)
-                    for (int i = 0; i < 6; ++i) gl[i] += yk[i] - yn[i];
-                    gl[2] -= dj[0] * yn[0] + dj[2] * yn[1];
-                    gl[3] -= dj[6] * yn[3];
-                    gl[4] -= dj[4] * yn[2] + dj[7] * yn[3];
-                    gl[5] -= dj[1] * yn[0] + dj[3] * yn[1] + dj[5] * yn[2] + dj[8] * yn[3];
-                } else {
-                    for (int i = 0; i < 6; ++i) gl[i] += yk[i];
-                }
-                for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
-                // blocks
-                LogSum lsum;
-                for (int j = 0; j < NBK; ++j) {
-                    double w[8], y[4], zw[8];
-                    for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); }
-                    for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
-                    Blk bk;
-                    blk_lin(a, x, j, w, y, bk);
-                    for (int r = 0; r < 4; ++r) c.B(B_D + r, j, k) = bk.d[r];
-                    // x stationarity: Jx' y
-                    for (int q = 0; q < 4; ++q) {
-                        double s = 0.0;
-                        for (int r = 0; r < 3; ++r) s += jx(bk, r, q) * y[r];
-                        gl[q] += s;
-                    }
-                    // dual stationarity: Jw' y - zw
-                    for (int e = 0; e < 8; ++e) {
-                        double t = -zw[e];
-                        for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * y[r];
-                        red[0] = fmax(red[0], fabs(t));
-                        const double sl = w[e] + RELAX;
-                        red[2] = fmax(red[2], fabs(zw[e] * sl));
-                        red[3] += zw[e];
-                        red[4] += zw[e];
-                        lsum.add(sl);
-                    }
-                    for (int r = 0; r < 4; ++r) {
-                        const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
-                        red[0] = fmax(red[0], fabs(-y[r] - vl + vu));
-                        red[1] = fmax(red[1], fabs(bk.d[r] - s));
-                        red[5] += fabs(bk.d[r] - s);
-                        red[3] += fabs(y[r]) + vu;
-                        red[4] += vu;
-                        red[2] = fmax(red[2], fabs(vu * (c.rU(r) - s)));
-                        lsum.add(c.rU(r) - s);
-                        if (c.hrl(r)) {
-                            red[2] = fmax(red[2], fabs(vl * (s - c.rL(r))));
-                            red[3] += vl;
-                            red[4] += vl;
-                            lsum.add(s - c.rL(r));
-                        }
-                    }
-                }
-                if (k == N && plan) {
-                    for (int i = 0; i < 6; ++i) {
-                        gl[i] += sh.ydf[i];
-                        const double dfi = x[i] - c.tgt_x[i];
-                        sh.df[i] = dfi;
-                        red[0] = fmax(red[0], fabs(-sh.ydf[i] - sh.vLf[i] + sh.vUf[i]));
-                        red[1] = fmax(red[1], fabs(dfi - sh.sf[i]));
-                        red[5] += fabs(dfi - sh.sf[i]);
-                        const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
-                        red[2] = fmax(red[2], fmax(fabs(sh.vLf[i] * sl), fabs(sh.vUf[i] * su)));
-                        red[3] += fabs(sh.ydf[i]) + sh.vLf[i] + sh.vUf[i];
-                        red[4] += sh.vLf[i] + sh.vUf[i];
-                        lsum.add(sl);
-                        lsum.add(su);
-                    }
-                }
-                for (int i = 0; i < 6; ++i) {
-                    const double zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
-                    gl[i] += -zl + zu;
-                    red[0] = fmax(red[0], fabs(gl[i]));
-                    if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
-                    if (c.hux(i)) { const double sl = c.xu[i] - x[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
-                }
-                if (k < N)
-                    for (int i = 0; i < 2; ++i) {
-                        const double zl = c.S(S_ZLU + i, k), zu = c.S(S_ZUU + i, k);
-                        const double t = c.S(S_GU + i, k) - a.dt * yn[i == 0 ? 5 : 4] - zl + zu;
-                        red[0] = fmax(red[0], fabs(t));
-                        if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
-                        if (c.huu(i)) { const double sl = c.uu[i] - u[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
-                    }
-                red[6] += stage_cost(c, k, x, u);
-                red[7] += lsum.value();  // sum of log slacks (barrier = -mu * this)
-                if (!isfinite(red[0]) || !isfinite(red[1])) red[0] = INFINITY;
-            }
-            {
-                const int ops[8] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM};
-                wg_reduce(sh, red, ops);
-            }
-            const double dinf = red[0], pinf = red[1], c0 = red[2], syz = red[3], szz = red[4];
-            const double th0 = red[5], cost0 = red[6], logs0 = red[7];
+            double red[8];
+            phase_lin(c, sh, red);
+            const double dinf = red[0], pinf = red[1], c0 = red[2];
+            const double th0 = red[5];
             if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; break; }
             const double smax = 100.0;
-            const double sd = fmax(smax, syz / (n_rows + n_bounds)) / smax;
-            const double sc = fmax(smax, szz / n_bounds) / smax;
+            const double sd = fmax(smax, red[3] / (n_rows + n_bounds)) / smax;
+            const double sc = fmax(smax, red[4] / n_bounds) / smax;
             E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
             if (E0 <= a.tol) { status = 0; break; }
             if (E0 <= a.acc_tol) {
@@ -898,160 +1557,156 @@ __global__ __launch_bounds__(T) void obca_kernel(ObcaArgs args) {
                 acc_count = 0;
             }
             if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; break; }
-            // ======== barrier update (monotone) ========
-            for (;;) {
-                if (!(mu > a.tol / 10.0 * 1.0000001)) break;
-                // complementarity vs mu
-                double cm[1] = {0.0};
-                for (int k = tid; k <= N; k += T) {
-                    double m = 0.0;
-                    for (int i = 0; i < 6; ++i) {
-                        const double xv = c.S(S_X + i, k);
-                        if (c.hlx(i)) m = fmax(m, fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
-                        if (c.hux(i)) m = fmax(m, fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
-                    }
-                    if (k < N)
-                        for (int i = 0; i < 2; ++i) {
-                            const double uv = c.S(S_U + i, k);
-                            if (c.hlu(i)) m = fmax(m, fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
-                            if (c.huu(i)) m = fmax(m, fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
-                        }
-                    for (int j = 0; j < NBK; ++j) {
-                        for (int e = 0; e < 8; ++e) m = fmax(m, fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
-                        for (int r = 0; r < 4; ++r) {
-                            const double s = c.B(B_S + r, j, k);
-                            m = fmax(m, fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
-                            if (c.hrl(r)) m = fmax(m, fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
-                        }
-                    }
-                    if (k == N && plan)
-                        for (int i = 0; i < 6; ++i)
-                            m = fmax(m, fmax(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu), fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu)));
-                    cm[0] = fmax(cm[0], m);
-                }
-                const int ops[1] = {R_MAX};
-                wg_reduce(sh, cm, ops);
-                const double Emu = fmax(fmax(dinf / sd, pinf), cm[0] / sc);
-                if (Emu <= kappa_eps * mu) {
-                    mu = fmax(a.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
-                    tau = fmax(0.99, 1.0 - mu);
-                    if (tid == 0) sh.nf = 0;  // IPOPT resets the filter on every barrier update
-                } else {
-                    break;
-                }
+            // ---- barrier update (monotone, Fiacco-McCormick) ----
+            while (mu > a.tol / 10.0 * 1.0000001) {
+                const double Emu = fmax(fmax(dinf / sd, pinf), phase_compl(c, sh, mu) / sc);
+                if (!(Emu <= kappa_eps * mu)) break;
+                mu = fmax(a.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
+                tau = fmax(0.99, 1.0 - mu);
+                __syncthreads();
+                if (tid == 0) sh.nf = 0;  // IPOPT resets the filter on every barrier update
             }
-            // residual arrays of the Newton right-hand side: c, d - s, d_f - s_f
+            const double phi0 = red[6] - mu * red[7];
+            // ---- residual arrays of the Newton right-hand side: c, d - s, d_f - s_f ----
             for (int k = tid; k <= N; k += T) {
+#pragma unroll
                 for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = c.S(S_C + i, k);
                 for (int j = 0; j < NBK; ++j)
+#pragma unroll
                     for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = c.B(B_D + r, j, k) - c.B(B_S + r, j, k);
                 if (k == N && plan)
+#pragma unroll
                     for (int i = 0; i < 6; ++i) sh.dfr[i] = sh.df[i] - sh.sf[i];
             }
-            // ======== Newton step with inertia correction ========
+            __syncthreads();
+            // ---- Newton step with inertia correction (IPOPT delta_w schedule) ----
             double dw = 0.0;
             bool ok = false;
             for (int attempt = 0; attempt < 40; ++attempt) {
-                __syncthreads();
-                // --- stage Hessians + gradients (block eliminations) ---
-                double fail[1] = {0.0};
-                for (int k = tid; k <= N; k += T) {
-                    double x[6];
-                    load_x(c, k, x);
-                    double Qs[21], qv[6];
-                    const double sc = (k == N && plan) ? a.tfac : 1.0;
-                    for (int i = 0; i < 6; ++i)
-                        for (int j2 = i; j2 < 6; ++j2) Qs[sy6(i, j2)] = sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
-                    if (k < N) {
-                        for (int i = 0; i < 6; ++i)
-                            for (int j2 = i; j2 < 6; ++j2) {
-                                const int wi = wd_idx(i, j2);
-                                if (wi >= 0) Qs[sy6(i, j2)] += c.S(S_WD + wi, k);
-                            }
-                    }
-                    for (int i = 0; i < 6; ++i) {
-                        const double xv = x[i], zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
-                        double sg = dw, g = c.S(S_GX + i, k);
-                        if (c.hlx(i)) { sg += zl / (xv - c.xl[i]); g -= mu / (xv - c.xl[i]); }
-                        if (c.hux(i)) { sg += zu / (c.xu[i] - xv); g += mu / (c.xu[i] - xv); }
-                        Qs[sy6(i, i)] += sg;
-                        qv[i] = g;
-                    }
-                    double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
-                    for (int j = 0; j < NBK; ++j) {
-                        double w[8], y[4], sw[8], fw[8], rd[4];
-                        for (int e = 0; e < 8; ++e) {
-                            w[e] = c.B(B_W + e, j, k);
-                            const double sl = w[e] + RELAX;
-                            sw[e] = c.B(B_ZW + e, j, k) / sl;
-                            fw[e] = -mu / sl;
-                        }
-                        for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
-                        Blk bk;
-                        blk_lin(a, x, j, w, y, bk);
-                        for (int r = 0; r < 4; ++r) {
-                            const double s = c.B(B_S + r, j, k), vu = c.B(B_VU + r, j, k);
-                            double sg = vu / (c.rU(r) - s), gs = mu / (c.rU(r) - s);
-                            if (c.hrl(r)) { const double vl = c.B(B_VL + r, j, k); sg += vl / (s - c.rL(r)); gs -= mu / (s - c.rL(r)); }
-                            bk.D[r] = sg + dw;
-                            rd[r] = c.B(B_DR + r, j, k) + gs / bk.D[r];
-                        }
-                        if (!blk_factor(bk, sw, dw, C4)) { fail[0] = 1.0; continue; }
-                        double zf[8], t4[4];
-                        blk_rhs(bk, fw, rd, zf, t4, q4);
-                    }
-                    for (int p = 0; p < 4; ++p) {
-                        for (int q = 0; q <= p; ++q) Qs[sy6(q, p)] += C4[lo4(p, q)];
-                        qv[p] += q4[p];
-                    }
-                    if (k == N && plan)
-                        for (int i = 0; i < 6; ++i) {
-                            const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
-                            const double Df = sh.vLf[i] / sl + sh.vUf[i] / su + dw;
-                            const double gs = -mu / sl + mu / su;
-                            sh.Df[i] = Df;
-                            sh.rf[i] = sh.dfr[i] + gs / Df;
-                            Qs[sy6(i, i)] += Df;
-                            qv[i] += Df * sh.rf[i];
-                        }
-                    for (int i = 0; i < 21; ++i) c.S(S_QT + i, k) = Qs[i];
-                    for (int i = 0; i < 6; ++i) c.S(S_QV + i, k) = qv[i];
-                    if (k < N) {
-                        const double u0 = c.S(S_U, k), u1 = c.S(S_U + 1, k);
-                        double R0 = 2.0 * a.R[0] + dw, R1 = a.R[1] + a.R[2], R3 = 2.0 * a.R[3] + dw;
-                        double g0 = c.S(S_GU, k), g1 = c.S(S_GU + 1, k);
-                        if (c.hlu(0)) { R0 += c.S(S_ZLU, k) / (u0 - c.ul[0]); g0 -= mu / (u0 - c.ul[0]); }
-                        if (c.huu(0)) { R0 += c.S(S_ZUU, k) / (c.uu[0] - u0); g0 += mu / (c.uu[0] - u0); }
-                        if (c.hlu(1)) { R3 += c.S(S_ZLU + 1, k) / (u1 - c.ul[1]); g1 -= mu / (u1 - c.ul[1]); }
-                        if (c.huu(1)) { R3 += c.S(S_ZUU + 1, k) / (c.uu[1] - u1); g1 += mu / (c.uu[1] - u1); }
-                        c.S(S_RT, k) = R0;
-                        c.S(S_RT + 1, k) = R1;
-                        c.S(S_RT + 2, k) = R3;
-                        c.S(S_RV, k) = g0;
-                        c.S(S_RV + 1, k) = g1;
-                    }
-                }
-                {
-                    const int ops[1] = {R_MAX};
-                    wg_reduce(sh, fail, ops);
-                }
-                bool good = fail[0] == 0.0;
-                // --- Riccati backward sweep (wave 0) ---
-                if (good) {
-                    if (tid < 64) riccati(c, sh, true);
-                    __syncthreads();
-                    good = sh.flag == 0;
-                }
-                if (good) { ok = true; break; }
+                if (newton_solve(c, sh, mu, dw, 0)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
                 if (dw > 1e40) break;
             }
             if (!ok) { status = 4; break; }
             if (dw > 0) dw_last = dw;
-            // NOTE: continued in part 2
+            double rec[4];
+            phase_recover(c, sh, mu, dw, tau, 0, rec);
+            const double ap = rec[0], Dm = rec[2], rel = rec[3];
+            double az = rec[1];
+            // ---- filter line search ----
+            if (iter == 0 || !(th_max > 0)) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
+            double amin;
+            if (Dm < 0.0) {
+                amin = fmin(g_th, g_ph * th0 / (-Dm));
+                if (th0 <= th_min) amin = fmin(amin, delta * pow(th0, s_th) / pow(-Dm, s_ph));
+            } else {
+                amin = g_th;
+            }
+            amin *= g_al;
+            const double tolc = 10.0 * EPS;
+            double alpha = ap;
+            int buf = 0;
+            bool accepted = rel < 1e-15;
+            bool ftype = false;
+            for (int ls = 0; !accepted; ++ls) {
+                double tr[3];
+                phase_trial(c, sh, mu, alpha, 0, tr);
+                const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
+                bool okls = false;
+                if (isfinite(tr[1]) && tr[0] <= th_max && !in_filter(sh, tr[0], tr[1])) {
+                    if (th0 <= th_min && sw) { ftype = true; okls = tr[1] - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+                    else { ftype = false; okls = tr[0] <= (1.0 - g_th) * th0 || tr[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+                }
+                if (okls) { accepted = true; break; }
+                if (ls == 0 && isfinite(tr[1]) && tr[0] >= th0) {
+                    // second-order corrections into step buffer 1
+                    for (int k = tid; k <= N; k += T) {
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = c.S(S_C + i, k);
+                        for (int j = 0; j < NBK; ++j)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = c.B(B_D + r, j, k) - c.B(B_S + r, j, k);
+                        if (k == N && plan)
+#pragma unroll
+                            for (int i = 0; i < 6; ++i) sh.dfr[i] = sh.df[i] - sh.sf[i];
+                    }
+                    __syncthreads();
+                    double a_soc = alpha, th_old = th0, th_t = tr[0];
+                    bool soc_ok = false;
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        if (p > 0 && th_t > 0.99 * th_old) break;
+                        th_old = th_t;
+                        phase_soc_resid(c, sh, a_soc);
+                        __syncthreads();
+                        if (!newton_solve(c, sh, mu, dw, 1)) break;
+                        double rs[4];
+                        phase_recover(c, sh, mu, dw, tau, 1, rs);
+                        a_soc = rs[0];
+                        double t2[3];
+                        phase_trial(c, sh, mu, a_soc, 1, t2);
+                        th_t = t2[0];
+                        bool ok2 = false;
+                        if (isfinite(t2[1]) && t2[0] <= th_max && !in_filter(sh, t2[0], t2[1])) {
+                            if (th0 <= th_min && sw) { ftype = true; ok2 = t2[1] - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+                            else { ftype = false; ok2 = t2[0] <= (1.0 - g_th) * th0 || t2[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+                        }
+                        if (ok2) { soc_ok = true; az = rs[1]; break; }
+                        if (!isfinite(t2[1])) break;
+                    }
+                    if (soc_ok) { accepted = true; alpha = a_soc; buf = 1; break; }
+                }
+                if (alpha * 0.5 < amin) break;
+                alpha *= 0.5;
+            }
+            __syncthreads();
+            if (!accepted) {
+                if (tid == 0) sh.nf = 0;  // IPOPT would enter restoration here
+            } else if (!ftype) {
+                if (tid == 0) add_filter(sh, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+            }
+            __syncthreads();
+            phase_update(c, sh, mu, alpha, az, buf);
+            __syncthreads();
         }
+    }
+    // ---------------- outputs ----------------
+    __syncthreads();
+    for (int k = tid; k <= N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) a.xout[((size_t)c.b * (N + 1) + k) * 6 + i] = c.S(S_X + i, k);
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a.uout[((size_t)c.b * N + k) * 2 + i] = c.S(S_U + i, k);
+        if (a.zout) {
+            double* z = a.zout + (size_t)c.b * nz + (size_t)k * st;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) z[i] = c.S(S_X + i, k);
+            int o = 6;
+            if (k < N) { z[6] = c.S(S_U, k); z[7] = c.S(S_U + 1, k); o = 8; }
+            for (int j = 0; j < NBK; ++j) {
+                const int ob = j >> 1, bd = j & 1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    z[o + ob * 8 + 4 * bd + e] = c.B(B_W + e, j, k);
+                    z[o + 8 * a.M + ob * 8 + 4 * bd + e] = c.B(B_W + 4 + e, j, k);
+                }
+            }
+        }
+    }
+    if (tid == 0) {
+        a.status[c.b] = status;
+        if (a.iters) a.iters[c.b] = iter;
+        if (a.kkt) a.kkt[c.b] = E0;
     }
 }
 
 }  // namespace
+
+hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream) {
+    if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(obca_kernel, dim3(a.B), dim3(T), 0, stream, a);
+    return hipGetLastError();
+}
+
 }  // namespace ttmpc

@@ -26,7 +26,7 @@ class TTConfig(C.Structure):
                 ("dt", C.c_double), ("L1", C.c_double), ("L2", C.c_double), ("Mh", C.c_double),
                 ("W1", C.c_double), ("W2", C.c_double), ("variant", C.c_int),
                 ("tol", C.c_double), ("acc_tol", C.c_double), ("max_iter", C.c_int), ("acc_iter", C.c_int),
-                ("warm_shift_compat", C.c_int)]
+                ("warm_shift_compat", C.c_int), ("dual_init", C.c_int)]
 
 
 class TTError(RuntimeError):
@@ -72,6 +72,14 @@ def lib():
     L.tt_solve_batch_device.restype = C.c_int
     L.tt_plan_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _ip, _ip]
     L.tt_plan_batch.restype = C.c_int
+    L.tt_obca_solve_batch.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip, _dp]
+    L.tt_obca_solve_batch.restype = C.c_int
+    L.tt_obca_solve_batch_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 12
+    L.tt_obca_solve_batch_device.restype = C.c_int
+    L.tt_obca_n.argtypes = [C.c_int, C.c_int]
+    L.tt_obca_n.restype = C.c_longlong
+    L.tt_obca_workspace_bytes.argtypes = [C.c_int, C.c_int]
+    L.tt_obca_workspace_bytes.restype = C.c_longlong
     L.tt_destroy.argtypes = [C.c_void_p]
     L.tt_destroy.restype = None
     L.tt_last_error.argtypes = [C.c_void_p]
@@ -86,7 +94,8 @@ def lib():
     return L
 
 
-EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_plan_batch", "tt_destroy",
+EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_plan_batch", "tt_obca_solve_batch",
+                    "tt_obca_solve_batch_device", "tt_obca_n", "tt_obca_workspace_bytes", "tt_destroy",
                     "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version")
 
 
@@ -127,6 +136,7 @@ class BatchSolver:
         cfg.variant = int(variant)
         cfg.tol, cfg.acc_tol, cfg.max_iter, cfg.acc_iter = float(tol), float(acc_tol), int(max_iter), int(acc_iter)
         cfg.warm_shift_compat = 0
+        cfg.dual_init = 0
         self.N = int(N)
         self.variant = int(variant)
         self.Q = _f64(Q, (6, 6))
@@ -184,3 +194,74 @@ class BatchSolver:
                                            u_out, status, iters or None, kkt or None, stream or None)
         if rc != 0:
             self._err(rc, "tt_solve_batch_device")
+
+
+def obca_n(N: int, M: int) -> int:
+    """Length of the reference's OBCA decision vector (trajectory_optimization.py:55-91)."""
+    return N * (8 + 16 * M) + 6 + 16 * M
+
+
+class ObcaSolver:
+    """Handle for the OBCA NLPs: TT_VARIANT_OBCA_PLAN (TrajectoryOptimization) or TT_VARIANT_TRACK_OBCA
+    (MPCTrackingControlObs).  obstacles: (M,4) array of (cx, cy, w, h)."""
+
+    def __init__(self, N, params, Q, R, xlb, xub, ulb, uub, obstacles, variant=TT_VARIANT_OBCA_PLAN, tol=0.0,
+                 acc_tol=0.0, max_iter=0, acc_iter=0, dual_init=True, device=None):
+        ob = _f64(obstacles).reshape(-1, 4)
+        cfg = TTConfig()
+        cfg.nx, cfg.nu, cfg.N, cfg.M = 6, 2, int(N), int(ob.shape[0])
+        cfg.dt, cfg.L1, cfg.L2, cfg.Mh = float(params["dt"]), float(params["L1"]), float(params["L2"]), float(params["M"])
+        cfg.W1, cfg.W2 = float(params["W1"]), float(params["W2"])
+        cfg.variant = int(variant)
+        cfg.tol, cfg.acc_tol, cfg.max_iter, cfg.acc_iter = float(tol), float(acc_tol), int(max_iter), int(acc_iter)
+        cfg.warm_shift_compat = 0
+        cfg.dual_init = int(bool(dual_init))
+        self.N, self.M, self.variant = int(N), int(ob.shape[0]), int(variant)
+        self.n = obca_n(self.N, self.M)
+        self.obstacles = ob
+        self.Q = _f64(Q, (6, 6))
+        self.R = _f64(R, (2, 2))
+        self.bounds = tuple(_bounds(b, n) for b, n in ((xlb, 6), (xub, 6), (ulb, 2), (uub, 2)))
+        self.device = default_device() if device is None else int(device)
+        h = C.c_void_p()
+        L = lib()
+        rc = L.tt_create(C.byref(cfg), _ptr(self.Q), _ptr(self.R), *[_ptr(b) for b in self.bounds], _ptr(ob),
+                         self.device, C.byref(h))
+        if rc != 0:
+            raise TTError(f"tt_create failed ({rc}): {L.tt_last_error(None).decode()}")
+        self._h = h
+        self._L = L
+
+    close = BatchSolver.close
+    __del__ = BatchSolver.__del__
+    _err = BatchSolver._err
+
+    def solve(self, x0, x_goal=None, xref=None, uref=None, z_guess=None):
+        """Host arrays -> (X (B,N+1,6), U (B,N,2), z (B,n), status, iters, kkt)."""
+        N, n = self.N, self.n
+        x0 = _f64(x0)
+        B = x0.shape[0] if x0.ndim == 2 else 1
+        x0 = x0.reshape(B, 6)
+        xg = None if x_goal is None else _f64(x_goal, (B, 6))
+        xr = None if xref is None else _f64(xref, (B, N + 1, 6))
+        ur = None if uref is None else _f64(uref, (B, N, 2))
+        zg = None if z_guess is None else _f64(z_guess, (B, n))
+        X = np.empty((B, N + 1, 6))
+        U = np.empty((B, N, 2))
+        Z = np.empty((B, n))
+        st = np.empty(B, dtype=np.int32)
+        it = np.empty(B, dtype=np.int32)
+        kk = np.empty(B)
+        rc = self._L.tt_obca_solve_batch(self._h, B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg), _ptr(X),
+                                         _ptr(U), _ptr(Z), st.ctypes.data_as(_ip), it.ctypes.data_as(_ip), _ptr(kk))
+        if rc != 0:
+            self._err(rc, "tt_obca_solve_batch")
+        return X, U, Z, st, it, kk
+
+    def solve_device(self, B, x0, x_goal, xref, uref, z_guess, x_out, u_out, z_out, status, iters=0, kkt=0, stream=0):
+        """Device pointers (ints), enqueued on ``stream``."""
+        rc = self._L.tt_obca_solve_batch_device(self._h, int(B), x0, x_goal or None, xref or None, uref or None,
+                                                z_guess or None, x_out, u_out, z_out or None, status, iters or None,
+                                                kkt or None, stream or None)
+        if rc != 0:
+            self._err(rc, "tt_obca_solve_batch_device")

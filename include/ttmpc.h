@@ -46,10 +46,10 @@ enum { TT_CONVERGED = 0, TT_ACCEPTABLE = 1, TT_MAX_ITER = 2, TT_INFEASIBLE = 3, 
 
 enum {
     TT_VARIANT_TRACK = 0,      /* MPCTrackingControl       mpc_control.py       (max_iter 5000, tol 1e-8)  */
-    TT_VARIANT_TRACK_OBCA = 1, /* MPCTrackingControlObs    mpc_control_obs.py   (not in this build)        */
+    TT_VARIANT_TRACK_OBCA = 1, /* MPCTrackingControlObs    mpc_control_obs.py   (max_iter 5000, tol 1e-8)  */
     TT_VARIANT_NMPC = 2,       /* TruckTrailerNMPC         mpc_control_nmpc.py  (tol 1e-3, acc 1e-2 x5)    */
     TT_VARIANT_FUZZY = 3,      /* MPCTrackingControlFuzzy  mpc_control_fuzzy.py (tol 1e-3, per-instance w) */
-    TT_VARIANT_OBCA_PLAN = 4   /* TrajectoryOptimization   trajectory_optimization.py (not in this build) */
+    TT_VARIANT_OBCA_PLAN = 4   /* TrajectoryOptimization   trajectory_optimization.py (max_iter 5000)      */
 };
 
 typedef struct {
@@ -59,6 +59,9 @@ typedef struct {
     double tol, acc_tol;              /* IPOPT tol / acceptable_tol (<=0 -> variant default)          */
     int max_iter, acc_iter;           /* IPOPT max_iter / acceptable_iter (<=0 -> variant default)    */
     int warm_shift_compat;            /* reserved: warm-shift guesses are built host-side (ttmpc.nlp) */
+    int dual_init;                    /* OBCA variants: 1 = start mu/lam from the separating-axis
+                                         certificate of each body/obstacle pair at the guess pose,
+                                         0 = from z_guess's mu/lam as the reference does            */
 } tt_config;
 
 /* Replaces the controller constructors (mpc_control.py:6-15 -> _build_solver 27-56; the CasADi
@@ -79,10 +82,29 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
                           const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out,
                           int* d_status, int* d_iters, double* d_kkt_res, void* stream);
 
-/* Replaces TrajectoryOptimization.plan (trajectory_optimization.py:311-331).  Not in this build:
- * returns -ENOSYS (OBCA is a later milestone). */
+/* Replaces TrajectoryOptimization.plan (trajectory_optimization.py:311-331) for B scenarios of a
+ * TT_VARIANT_OBCA_PLAN handle.  x0, xgoal [B][6] (ca.vertcat(initial_state, goal_state), 316-323);
+ * z_guess [B][n], n = N(8+16M)+6+16M, the reference's interleaved [x_k,u_k,mu_k,lam_k] vector
+ * (55-91), built host-side as _hybrid_a_star_initial_trajectory does (227-274), or NULL for
+ * _generate_initial_trajectory_guess (209-225).  Host pointers; synchronous.  Like plan(), success is
+ * reported (status) but never enforced (326-331). */
 int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess,
                   double* x_out, double* u_out, int* status, int* iters);
+
+/* Both OBCA variants with every output: z_out [B][n] (x, u, mu, lam; _split_decision_variables,
+ * trajectory_optimization.py:277-309) and the scaled KKT error.  Plan variant: xgoal [B][6], xref/uref
+ * NULL.  MPC+OBCA variant (mpc_control_obs.py:290-322): xref [B][N+1][6], uref [B][N][2], xgoal NULL;
+ * z_guess NULL = _get_initial_guess (216-239).  x_out/u_out/z_out/iters/kkt may be NULL. */
+int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
+                        const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
+                        int* status, int* iters, double* kkt_res);
+/* Same with DEVICE pointers, asynchronous on `stream` (NULL = the handle's stream). */
+int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
+                               const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
+                               double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream);
+/* decision-vector length n of the OBCA variants, and device workspace bytes one instance needs */
+long long tt_obca_n(int N, int M);
+long long tt_obca_workspace_bytes(int N, int M);
 
 void tt_destroy(void* handle);
 const char* tt_last_error(void* handle);

@@ -10,7 +10,7 @@ from conftest import PKG, REPO
 
 def _declared():
     hdr = (REPO / "include" / "ttmpc.h").read_text()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(tt_\w+)\s*\(", hdr, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|long long|const char\*)\s+(tt_\w+)\s*\(", hdr, flags=re.M)))
 
 
 def test_header_declares_the_boundary():

@@ -1,0 +1,51 @@
+"""GPU vs CPU-oracle comparison of the OBCA plan solver (development check; prints one summary per case)."""
+import json
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO), str(REPO / "car-trailer-mpc_amd")]
+import numpy as np  # noqa: E402
+
+import ttmpc  # noqa: E402
+from oracle import c_oracle as co  # noqa: E402
+from ttmpc import scenarios as sc  # noqa: E402
+
+obs_all = sc.obstacles_array(sc.load_obstacles(REPO / "tests" / "golden" / "obstacles.json"))
+S = np.load(REPO / "tests" / "golden" / "reference_numpy.npz")["state_traj"]
+
+
+def run(name, N, M, x0, xg, zg, max_iter=1000):
+    obs = obs_all[:M]
+    P = co.make_obca_problem(N, sc.OBCA_PARAMS, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB,
+                             sc.OBCA_UUB, obs, max_iter=max_iter)
+    t = time.time()
+    zc, stc, itc, kkc = co.obca_solve_batch(P, x0, xg, z_guess=zg, nthreads=16)
+    tc = time.time() - t
+    s = ttmpc.ObcaSolver(N, sc.OBCA_PARAMS, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB,
+                         obs, max_iter=max_iter)
+    s.solve(x0[:1], xg[:1], z_guess=zg[:1])  # warm-up (module load)
+    t = time.time()
+    X, U, Z, st, it, kk = s.solve(x0, xg, z_guess=zg)
+    tg = time.time() - t
+    Xc, Uc, _, _ = co.obca_split(zc, N, M)
+    both = (st <= 1) & (stc <= 1)
+    dx = np.abs(X - Xc).max(axis=(1, 2))
+    print(f"[{name}] B={len(x0)} N={N} M={M}  gpu {tg:.3f}s  cpu {tc:.3f}s (16 thr)")
+    print(f"   gpu status {st.tolist()} iters {it.tolist()}")
+    print(f"   cpu status {stc.tolist()} iters {itc.tolist()}")
+    print(f"   max|X_gpu - X_cpu| per instance {np.array2string(dx, precision=2)}; both-converged {both.sum()}")
+    print(f"   gpu kkt {np.array2string(kk, precision=1)}")
+    sys.stdout.flush()
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("small", "all"):
+        cases = json.loads((REPO / "tests" / "golden" / "test_cases.json").read_text())["cases"]
+        x0, xg, zg = sc.obca_case_batch([cases[1], cases[3]], 4, 200, 1, seed=1)
+        run("cases1,3 M=1", 200, 1, x0, xg, zg)
+    if which in ("c4", "all"):
+        x0, xg, zg = sc.obca_replan_batch(S, 16, 200, 6, seed=0)
+        run("replan M=6", 200, 6, x0, xg, zg)
