@@ -247,3 +247,60 @@ def obca_replan_batch(base_states, B: int, N: int, M: int, seed: int = 0, n_wayp
         xg[b] = [pos[-1, 0], pos[-1, 1], hd[-1], hi[-1], 0.0, 0.0]
         zg[b] = obca_guess(pos, hd, hi, N, M)
     return x0, xg, zg
+
+
+def interpolate_plan(state_traj, input_traj, dt_1, dt_2):
+    """do_interpolation (simulation.py:201-218): OBCA plan at dt_1 -> MPC reference at dt_2
+    (linear states, zero-order-hold inputs)."""
+    N = input_traj.shape[1]
+    n = int(math.floor(dt_1 / dt_2))
+    S = np.zeros((state_traj.shape[0], n * N + 1))
+    U = np.zeros((input_traj.shape[0], n * N))
+    for k in range(N):
+        for m in range(n):
+            t = m / n
+            S[:, k * n + m] = (1 - t) * state_traj[:, k] + t * state_traj[:, k + 1]
+            U[:, k * n + m] = input_traj[:, k]
+    S[:, -1] = state_traj[:, -1]
+    return S, U
+
+
+def reference_window(ref_states, ref_inputs, k, horizon):
+    """Reference windowing with end padding (simulation.py:485-499): (6, H+1), (2, H)."""
+    N = ref_inputs.shape[1]
+    Xr = np.zeros((NX, horizon + 1))
+    Ur = np.zeros((NU, horizon))
+    if k + horizon <= N:
+        Xr[:, :] = ref_states[:, k:k + horizon + 1]
+        Ur[:, :] = ref_inputs[:, k:k + horizon]
+    elif k < N:
+        Xr[:, :N + 1 - k] = ref_states[:, k:]
+        Xr[:, N + 1 - k:] = ref_states[:, -1:]
+        Ur[:, :N - k] = ref_inputs[:, k:]
+        Ur[:, N - k:] = ref_inputs[:, -1:]
+    else:
+        Xr[:, :] = ref_states[:, -1:]
+        Ur[:, :] = 0.0
+    return Xr, Ur
+
+
+def mpc_obs_batch(state_traj, input_traj, B: int, horizon: int, seed: int = 0, dt_plan=0.1, dt=0.05,
+                  pos_sigma=0.2, ang_sigma=0.02):
+    """MPC+OBCA batch (mpc_control_obs.py, driven as simulation.py:417-424, 484-522): the OBCA plan is
+    interpolated to the MPC step (do_interpolation), instance b tracks the window starting at an evenly
+    spread step index, x0 = window start + Gaussian perturbation.  Returns x0 (B,6), xref (B,H+1,6),
+    uref (B,H,2) in the stage-major parameter layout (mpc_control_obs.py:290-301)."""
+    rng = np.random.default_rng(seed)
+    S, U = interpolate_plan(np.asarray(state_traj, float), np.asarray(input_traj, float), dt_plan, dt)
+    ks = np.linspace(0, U.shape[1] - 1, B).round().astype(int)
+    x0 = np.empty((B, NX))
+    xref = np.empty((B, horizon + 1, NX))
+    uref = np.empty((B, horizon, NU))
+    for b, k in enumerate(ks):
+        Xr, Ur = reference_window(S, U, int(k), horizon)
+        xref[b] = Xr.T
+        uref[b] = Ur.T
+        pert = np.concatenate([rng.normal(0, pos_sigma, 2), rng.normal(0, ang_sigma, 2), [0.0, 0.0]])
+        x0[b] = np.clip(Xr[:, 0] + pert, np.where(np.isfinite(XLB), XLB + 1e-6, -np.inf),
+                        np.where(np.isfinite(XUB), XUB - 1e-6, np.inf))
+    return x0, xref, uref

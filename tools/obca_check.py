@@ -40,6 +40,29 @@ def run(name, N, M, x0, xg, zg, max_iter=1000):
     sys.stdout.flush()
 
 
+def run_track(name, N, M, x0, xr, ur, max_iter=1000):
+    obs = obs_all[:M]
+    p = dict(sc.OBCA_PARAMS, dt=0.05)
+    P = co.make_obca_problem(N, p, sc.OBCA_Q, sc.OBCA_R, sc.XLB, sc.XUB, sc.ULB, sc.UUB, obs, mode=co.OBCA_TRACK,
+                             max_iter=max_iter)
+    t = time.time()
+    zc, stc, itc, kkc = co.obca_solve_batch(P, x0, xref=xr, uref=ur, nthreads=16)
+    tc = time.time() - t
+    s = ttmpc.ObcaSolver(N, p, sc.OBCA_Q, sc.OBCA_R, sc.XLB, sc.XUB, sc.ULB, sc.UUB, obs,
+                         variant=ttmpc.TT_VARIANT_TRACK_OBCA, max_iter=max_iter)
+    s.solve(x0[:1], xref=xr[:1], uref=ur[:1])
+    t = time.time()
+    X, U, Z, st, it, kk = s.solve(x0, xref=xr, uref=ur)
+    tg = time.time() - t
+    Xc, Uc, _, _ = co.obca_split(zc, N, M)
+    dx = np.abs(X - Xc).max(axis=(1, 2))
+    print(f"[{name}] B={len(x0)} N={N} M={M}  gpu {tg:.3f}s  cpu {tc:.3f}s (16 thr)")
+    print(f"   gpu status {st.tolist()} iters {it.tolist()}")
+    print(f"   cpu status {stc.tolist()} iters {itc.tolist()}")
+    print(f"   max|X_gpu - X_cpu| per instance {np.array2string(dx, precision=2)}")
+    sys.stdout.flush()
+
+
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("small", "all"):
@@ -49,3 +72,7 @@ if __name__ == "__main__":
     if which in ("c4", "all"):
         x0, xg, zg = sc.obca_replan_batch(S, 16, 200, 6, seed=0)
         run("replan M=6", 200, 6, x0, xg, zg)
+    if which in ("track", "all"):
+        I = np.load(REPO / "tests" / "golden" / "reference_numpy.npz")["input_traj"]
+        x0, xr, ur = sc.mpc_obs_batch(S, I, 16, 50, seed=0)
+        run_track("mpc+obca M=11", 50, 11, x0, xr, ur)
