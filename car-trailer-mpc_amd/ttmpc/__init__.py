@@ -9,7 +9,9 @@ from ._lib import (STATUS_NAMES, TT_ACCEPTABLE, TT_CONVERGED, TT_INFEASIBLE, TT_
 from .mpc_control import MPCTrackingControl  # noqa: F401
 from .mpc_control_fuzzy import MPCTrackingControlFuzzy, fuzzy_weights  # noqa: F401
 from .mpc_control_nmpc import TruckTrailerNMPC  # noqa: F401
+from .mpc_control_obs import MPCTrackingControlObs  # noqa: F401
+from .trajectory_optimization import TrajectoryOptimization  # noqa: F401
 from .truck_trailer_model import TruckTrailerModel  # noqa: F401
 
-__all__ = ["MPCTrackingControl", "TruckTrailerNMPC", "MPCTrackingControlFuzzy", "TruckTrailerModel", "BatchSolver", "ObcaSolver",
+__all__ = ["MPCTrackingControl", "MPCTrackingControlObs", "TrajectoryOptimization", "TruckTrailerNMPC", "MPCTrackingControlFuzzy", "TruckTrailerModel", "BatchSolver", "ObcaSolver",
            "fuzzy_weights", "TTError", "lib"]

@@ -172,26 +172,53 @@ def interpolate_waypoints(waypoints, num_output_nodes):
     return sp(np.linspace(0.0, 1.0, num_output_nodes))
 
 
-def obca_guess(positions, headings, hitch, N, M):
+def complete_speed_steering(X, dt, L1, vlim=(-5.0, 10.0), philim=np.pi / 4):
+    """Fill the speed / steering columns the reference leaves at 0 ("has to be implemented later",
+    trajectory_optimization.py:251-252): v_k from the position increment along the heading, phi_k from
+    the heading increment (theta_dot = v tan(phi) / L1, truck_trailer_model.py:19), both clipped to 90%
+    of their bounds; v_N = phi_N = 0.  X (N+1, 6) -> copy."""
+    X = np.array(X, dtype=np.float64)
+    d = X[1:, :2] - X[:-1, :2]
+    v = (d[:, 0] * np.cos(X[:-1, 2]) + d[:, 1] * np.sin(X[:-1, 2])) / dt
+    v = np.clip(v, 0.9 * vlim[0], 0.9 * vlim[1])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        phi = np.where(np.abs(v) > 1e-3, np.arctan(L1 * (X[1:, 2] - X[:-1, 2]) / (dt * v)), 0.0)
+    X[:-1, 5] = v
+    X[:-1, 4] = np.clip(phi, -0.9 * philim, 0.9 * philim)
+    X[-1, 4:6] = 0.0
+    return X
+
+
+def obca_guess(positions, headings, hitch, N, M, complete=False, dt=0.1, L1=7.05):
     """_hybrid_a_star_initial_trajectory (trajectory_optimization.py:227-274): waypoint splines to N
     nodes, x_k = (p_k, theta_k, psi_k, 0, 0) for k < N, x_N = last node, u = 0, mu = 100,
     lam = kron(1_M, [100,105,110,115,100,105,110,115]).  ``headings`` already carry the +pi/2 shift
-    (trajectory_optimization.py:238).  Returns the reference's interleaved z (n = N(8+16M)+6+16M)."""
+    (trajectory_optimization.py:238).  complete=True fills the speed/steering placeholders
+    (complete_speed_steering).  Returns the reference's interleaved z (n = N(8+16M)+6+16M)."""
     P = interpolate_waypoints(positions, N)
     H = interpolate_waypoints(headings, N)
     S = interpolate_waypoints(hitch, N)
+    X = np.zeros((N + 1, NX))
+    X[:N, 0:2] = P
+    X[:N, 2] = H
+    X[:N, 3] = S
+    X[N, 0:2] = P[-1]
+    X[N, 2] = H[-1]
+    X[N, 3] = S[-1]
+    if complete:
+        X = complete_speed_steering(X, dt, L1)
     st = 8 + 16 * M
     z = np.zeros(N * st + 6 + 16 * M)
     duals = np.concatenate([np.full(8 * M, 100.0), np.tile(LAM_PATTERN, M)])
     for k in range(N):
-        z[k * st:k * st + 6] = [P[k, 0], P[k, 1], H[k], S[k], 0.0, 0.0]
+        z[k * st:k * st + 6] = X[k]
         z[k * st + 8:(k + 1) * st] = duals
-    z[N * st:N * st + 6] = [P[-1, 0], P[-1, 1], H[-1], S[-1], 0.0, 0.0]
+    z[N * st:N * st + 6] = X[N]
     z[N * st + 6:] = duals
     return z
 
 
-def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5, ang_sigma=0.05):
+def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5, ang_sigma=0.05, complete=False):
     """C4 generator: test_cases.json cases x Monte-Carlo start perturbations.  Each instance is the
     2-waypoint initialize.json of its case (apply_case.py:16-34) with a perturbed start; the guess is
     built from those waypoints (obca_guess) and (x_init, x_goal) as get_initial_goal_states.py:5-26 +
@@ -213,20 +240,21 @@ def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5,
             hi[0] = float(np.clip(hi[0] + rng.normal(0.0, ang_sigma), -0.5, 0.5))
         x0[b] = [pos[0, 0], pos[0, 1], hd[0], hi[0], 0.0, 0.0]
         xg[b] = [pos[1, 0], pos[1, 1], hd[1], hi[1], 0.0, 0.0]
-        zg[b] = obca_guess(pos, hd, hi, N, M)
+        zg[b] = obca_guess(pos, hd, hi, N, M, complete=complete)
     return x0, xg, zg
 
 
 def obca_replan_batch(base_states, B: int, N: int, M: int, seed: int = 0, n_waypoints: int = 8,
-                      pos_sigma=0.5, ang_sigma=0.05):
+                      pos_sigma=0.5, ang_sigma=0.05, complete=True):
     """C4 generator: Monte-Carlo re-plans around a collision-free OBCA plan.
 
     ``base_states`` (6, N+1) is a plan such as the reference's committed IPOPT solution
     (python-files/data/state_traj.txt).  Each instance subsamples it to ``n_waypoints`` waypoints
     (the shape of a Hybrid-A* initialize.json, trajectory_optimization.py:227-274), perturbs the
     start pose (instance 0 unperturbed) and builds the reference's guess from those waypoints
-    (obca_guess).  x_init = first waypoint, x_goal = last waypoint with zero steering and speed
-    (get_initial_goal_states.py + trajectory_animation.py:83-92).
+    (obca_guess; complete=True fills its speed/steering placeholders).  x_init = first waypoint,
+    x_goal = last waypoint with zero steering and speed (get_initial_goal_states.py +
+    trajectory_animation.py:83-92).
     Returns x0 (B,6), x_goal (B,6), z_guess (B,n)."""
     S = np.asarray(base_states, dtype=np.float64)
     rng = np.random.default_rng(seed)
@@ -245,7 +273,7 @@ def obca_replan_batch(base_states, B: int, N: int, M: int, seed: int = 0, n_wayp
             hi[0] += rng.normal(0.0, ang_sigma)
         x0[b] = [pos[0, 0], pos[0, 1], hd[0], hi[0], 0.0, 0.0]
         xg[b] = [pos[-1, 0], pos[-1, 1], hd[-1], hi[-1], 0.0, 0.0]
-        zg[b] = obca_guess(pos, hd, hi, N, M)
+        zg[b] = obca_guess(pos, hd, hi, N, M, complete=complete)
     return x0, xg, zg
 
 

@@ -37,9 +37,12 @@ class TrajectoryPlanning:
         self._Q = np.asarray(Q, dtype=np.float64).reshape(6, 6)
         self._R = np.asarray(R, dtype=np.float64).reshape(2, 2)
         self._device = device
-        self._solver = BatchSolver(self._horizon, self._params, self._Q, self._R, self._state_bound["lb"],
-                                   self._state_bound["ub"], self._input_bound["lb"], self._input_bound["ub"],
-                                   variant=self._variant, device=device, **self._ipopt)
+        self._solver = self._make_solver()
+
+    def _make_solver(self):
+        return BatchSolver(self._horizon, self._params, self._Q, self._R, self._state_bound["lb"],
+                           self._state_bound["ub"], self._input_bound["lb"], self._input_bound["ub"],
+                           variant=self._variant, device=self._device, **self._ipopt)
 
     # trajectory_planning.py:62-84
     def _split_decision_variables(self, vars):

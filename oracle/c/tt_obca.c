@@ -1264,6 +1264,17 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         if (chk) fprintf(stderr, "   newton residual %.3e (dw %.2e)\n", check_newton(W, mu, dw), dw);
         mult_steps(W, mu);
         double ap = ftb_primal(W, W->dx, W->du, W->dw, W->ds, W->dsf, tau);
+        if (getenv("TTO_FTBDBG")) {
+            double aw = 1, as_[4] = {1, 1, 1, 1}, ax = 1, au = 1, af = 1; int kw = -1, kx = -1, ix = -1;
+            for (int bi = 0; bi < W->nb; ++bi) {
+                for (int e = 0; e < 8; ++e) { double t = aw; FTB_P(W->w[8 * bi + e], -RELAX, W->dw[8 * bi + e], tau, aw); if (aw < t) kw = bi / W->nbk; }
+                for (int r = 0; r < 4; ++r) { const int v = 4 * bi + r; if (W->hrL[r]) FTB_P(W->s[v], W->rL[r], W->ds[v], tau, as_[r]); if (W->hrU[r]) FTB_PU(W->s[v], W->rU[r], W->ds[v], tau, as_[r]); }
+            }
+            for (int k = 0; k <= N; ++k) for (int i = 0; i < 6; ++i) { double t = ax; if (W->hxl[i]) FTB_P(W->x[6 * k + i], W->xl[i], W->dx[6 * k + i], tau, ax); if (W->hxu[i]) FTB_PU(W->x[6 * k + i], W->xu[i], W->dx[6 * k + i], tau, ax); if (ax < t) { kx = k; ix = i; } }
+            for (int k = 0; k < N; ++k) for (int i = 0; i < 2; ++i) { if (W->hul[i]) FTB_P(W->u[2 * k + i], W->ul[i], W->du[2 * k + i], tau, au); if (W->huu[i]) FTB_PU(W->u[2 * k + i], W->uu[i], W->du[2 * k + i], tau, au); }
+            if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) { FTB_P(W->sf[i], W->fL, W->dsf[i], tau, af); FTB_PU(W->sf[i], W->fU, W->dsf[i], tau, af); }
+            fprintf(stderr, "     ftb w %.1e(k%d) s %.1e %.1e %.1e %.1e x %.1e(k%d,i%d) u %.1e f %.1e\n", aw, kw, as_[0], as_[1], as_[2], as_[3], ax, kx, ix, au, af);
+        }
         double az = ftb_dual(W, tau);
         /* filter line search (Waechter & Biegler 2006, IPOPT defaults) */
         double ymax = 0.0;
