@@ -61,29 +61,36 @@ class ObcaNLP:
     def g(self, z, x_init, x_goal=None):
         X, U, mu, lam = self.split(z)
         dyn = [X[0] - x_init, (X[1:] - (X[:-1] + self.p["dt"] * self.f(X[:-1], U))).reshape(-1)]
-        rows, lo, hi = [], [], []
         L1, L2, W1, W2, Mh = self.p["L1"], self.p["L2"], self.p["W1"], self.p["W2"], self.p["M"]
-        A = np.array([[1.0, 0.0], [0.0, 1.0], [-1.0, 0.0], [0.0, -1.0]])
-        for k in range(self.N + 1):
-            x, y, th, psi = X[k, 0], X[k, 1], X[k, 2], X[k, 3]
-            pv = np.array([x + np.cos(th) * L1 / 2, y + np.sin(th) * L1 / 2])               # truck_trailer_model.py:58-61
-            hx, hy = x - np.cos(th) * Mh, y - np.sin(th) * Mh                               # 63-72
-            pt = np.array([hx - np.cos(th + psi) * L2 / 2, hy - np.sin(th + psi) * L2 / 2])
-            Rv = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
-            Rt = np.array([[np.cos(th + psi), -np.sin(th + psi)], [np.sin(th + psi), np.cos(th + psi)]])
-            gv = np.array([L1 / 2, W1 / 2, L1 / 2, W1 / 2])
-            gt = np.array([L2 / 2, W2 / 2, L2 / 2, W2 / 2])
-            for i, (cx, cy, w, h) in enumerate(self.ob):
-                b = np.array([w / 2, h / 2, w / 2, h / 2]) + A @ np.array([cx, cy])     # trajectory_optimization.py:32-53
-                mv, mt = mu[k, 8 * i:8 * i + 4], mu[k, 8 * i + 4:8 * i + 8]
-                lv, lt = lam[k, 8 * i:8 * i + 4], lam[k, 8 * i + 4:8 * i + 8]
-                r = [gv @ mv - (A @ pv - b) @ lv + self.dmin, gt @ mt - (A @ pt - b) @ lt + self.dmin]
-                r += list(A.T @ mv + Rv.T @ A.T @ lv) + list(A.T @ mt + Rt.T @ A.T @ lt)
-                r += [np.linalg.norm(A.T @ lv) - 1.0, np.linalg.norm(A.T @ lt) - 1.0]
-                rows += r
-                lo += [-np.inf, -np.inf] + [-self.eq_tol] * 4 + [-np.inf, -np.inf]
-                hi += [0.0, 0.0] + [self.eq_tol] * 4 + [0.0, 0.0]
-        out = [np.concatenate(dyn), np.array(rows)]
+        x, y, th, psi = X[:, 0], X[:, 1], X[:, 2], X[:, 3]
+        pv = np.stack([x + np.cos(th) * L1 / 2, y + np.sin(th) * L1 / 2], axis=1)          # truck_trailer_model.py:58-61
+        hx, hy = x - np.cos(th) * Mh, y - np.sin(th) * Mh                                    # 63-72
+        pt = np.stack([hx - np.cos(th + psi) * L2 / 2, hy - np.sin(th + psi) * L2 / 2], axis=1)
+        gv = np.array([L1 / 2, W1 / 2, L1 / 2, W1 / 2])
+        gt = np.array([L2 / 2, W2 / 2, L2 / 2, W2 / 2])
+        K = self.N + 1
+        R = np.zeros((K, self.M, 8))
+        for i, (cx, cy, w, h) in enumerate(self.ob):
+            b = np.array([w / 2 + cx, h / 2 + cy, w / 2 - cx, h / 2 - cy])               # trajectory_optimization.py:32-53
+            mv, mt = mu[:, 8 * i:8 * i + 4], mu[:, 8 * i + 4:8 * i + 8]
+            lv, lt = lam[:, 8 * i:8 * i + 4], lam[:, 8 * i + 4:8 * i + 8]
+            Apv = np.stack([pv[:, 0], pv[:, 1], -pv[:, 0], -pv[:, 1]], axis=1)             # A p, A = [I; -I]
+            Apt = np.stack([pt[:, 0], pt[:, 1], -pt[:, 0], -pt[:, 1]], axis=1)
+            R[:, i, 0] = mv @ gv - ((Apv - b) * lv).sum(1) + self.dmin
+            R[:, i, 1] = mt @ gt - ((Apt - b) * lt).sum(1) + self.dmin
+            av, cv = lv[:, 0] - lv[:, 2], lv[:, 1] - lv[:, 3]                                 # A' lam
+            at, ct = lt[:, 0] - lt[:, 2], lt[:, 1] - lt[:, 3]
+            c1, s1, c2, s2 = np.cos(th), np.sin(th), np.cos(th + psi), np.sin(th + psi)
+            R[:, i, 2] = mv[:, 0] - mv[:, 2] + c1 * av + s1 * cv                              # G'mu + R'A'lam
+            R[:, i, 3] = mv[:, 1] - mv[:, 3] - s1 * av + c1 * cv
+            R[:, i, 4] = mt[:, 0] - mt[:, 2] + c2 * at + s2 * ct
+            R[:, i, 5] = mt[:, 1] - mt[:, 3] - s2 * at + c2 * ct
+            R[:, i, 6] = np.hypot(av, cv) - 1.0
+            R[:, i, 7] = np.hypot(at, ct) - 1.0
+        rows = R.reshape(-1)
+        lo = np.tile([-np.inf, -np.inf] + [-self.eq_tol] * 4 + [-np.inf, -np.inf], K * self.M)
+        hi = np.tile([0.0, 0.0] + [self.eq_tol] * 4 + [0.0, 0.0], K * self.M)
+        out = [np.concatenate(dyn), rows]
         lbg = [np.zeros(6 * (self.N + 1)), np.array(lo)]
         ubg = [np.zeros(6 * (self.N + 1)), np.array(hi)]
         if self.mode == "plan":

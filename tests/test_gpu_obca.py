@@ -1,0 +1,166 @@
+"""GPU parity for the OBCA path (TrajectoryOptimization / MPCTrackingControlObs) through the C ABI.
+
+The GPU (car-trailer-mpc_amd/csrc/tt_obca.hip) and the CPU oracle (oracle/c/tt_obca.c) run the same
+restated algorithm.  On well-conditioned instances both take the same iterates, so status, iteration
+count and solution agree to rounding (<= 1e-9).  On the hard C4 re-plans the filter line search can
+branch differently on rounding-level differences, so there the test compares solutions only where both
+converged (same local optimum to <= 1e-6) and checks properties: feasibility, collision-free plans,
+bitwise-deterministic reruns.  Independent optimality: the finite-difference KKT certificate of
+oracle/obca_nlp.py (numpy restatement of the reference NLP) on the GPU's output.
+"""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+from test_obca_oracle import P6, toy_plan
+
+pytestmark = pytest.mark.gpu
+
+
+def _solver(N, obs, variant=None, params=P6, bounds=None, **kw):
+    import ttmpc
+    from ttmpc import scenarios as sc
+    b = bounds or (sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB)
+    v = ttmpc.TT_VARIANT_OBCA_PLAN if variant is None else variant
+    return ttmpc.ObcaSolver(N, params, sc.OBCA_Q, sc.OBCA_R, *b, obs, variant=v, **kw)
+
+
+def _oracle(N, obs, mode=0, params=P6, bounds=None, **kw):
+    from oracle import c_oracle as co
+    from ttmpc import scenarios as sc
+    b = bounds or (sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB)
+    return co.make_obca_problem(N, params, sc.OBCA_Q, sc.OBCA_R, *b, obs, mode=mode, **kw)
+
+
+def test_toy_plan_matches_oracle_and_is_kkt():
+    from oracle import c_oracle as co
+    from oracle.obca_nlp import ObcaNLP
+    from ttmpc import collision
+    from ttmpc import scenarios as sc
+    N, M, obs, x0, xg, zg = toy_plan()
+    X, U, Z, st, it, kk = _solver(N, obs).solve(x0, xg, z_guess=zg)
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(N, obs), x0, xg, z_guess=zg)
+    assert np.array_equal(st, stc) and np.all(st == 0)
+    assert np.array_equal(it, itc)
+    assert np.max(np.abs(Z - zc)) <= 1e-9
+    nlp = ObcaNLP(N, M, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
+    r = nlp.kkt_check(Z[1], x0[1], xg[1])
+    assert r["stat_rel"] < 1e-6 and r["prim"] < 1e-7 and r["bviol"] < 1e-7, r
+    assert collision.sat_gap(X[1], P6, obs).min() > 0.0
+    # outputs are the split of z (trajectory_optimization.py:277-309)
+    Xs, Us, _, _ = nlp.split(Z[0])
+    assert np.array_equal(X[0], Xs) and np.array_equal(U[0], Us)
+
+
+def test_mpc_obca_windows_match_oracle():
+    """MPC+OBCA (mpc_control_obs.py, simulation.py:417-424 setup: N=50, dt=0.05, all 11 obstacles) on
+    windows of the reference's interpolated plan."""
+    from oracle import c_oracle as co
+    from ttmpc import scenarios as sc
+    import ttmpc
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    obs = g["obstacles"]
+    x0, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 16, 50, seed=0)
+    sel = np.arange(10)  # the open-road windows; the last ones squeeze into the bay
+    p = dict(P6, dt=0.05)
+    bnd = (sc.XLB, sc.XUB, sc.ULB, sc.UUB)
+    X, U, Z, st, it, kk = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0[sel], xref=xr[sel], uref=ur[sel])
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0[sel], xref=xr[sel], uref=ur[sel])
+    assert np.all(st == 0) and np.array_equal(st, stc)
+    assert np.max(np.abs(Z - zc)) <= 1e-8
+
+
+def test_c4_replan_subset_vs_oracle():
+    from oracle import c_oracle as co
+    from oracle.obca_nlp import ObcaNLP
+    from ttmpc import collision
+    from ttmpc import scenarios as sc
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
+    x0, xg, zg = sc.obca_replan_batch(g["state_traj"], 16, 200, 6, seed=0)
+    X, U, Z, st, it, kk = _solver(200, obs, max_iter=1000).solve(x0, xg, z_guess=zg)
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs, max_iter=1000), x0, xg, z_guess=zg, nthreads=16)
+    ok = st <= 1
+    assert ok.sum() >= 11, (st, it)
+    both = ok & (stc <= 1)
+    Xc = co.obca_split(zc, 200, 6)[0]
+    assert np.max(np.abs(X[both] - Xc[both])) <= 1e-6      # same local optimum
+    nlp = ObcaNLP(200, 6, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
+    for b in np.flatnonzero(ok):
+        gv, lbg, ubg = nlp.g(Z[b], x0[b], xg[b])
+        assert np.all(gv >= lbg - 1e-6) and np.all(gv <= ubg + 1e-6)
+        assert collision.sat_gap(X[b], P6, obs).min() > 0.0
+
+
+def test_c4_full_batch_properties_and_determinism():
+    """BASELINE config C4 at full size: B=256 scenarios, N=200, M=6."""
+    from ttmpc import collision
+    from ttmpc import scenarios as sc
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
+    x0, xg, zg = sc.obca_replan_batch(g["state_traj"], 256, 200, 6, seed=1)
+    s = _solver(200, obs, max_iter=1000)
+    X, U, Z, st, it, kk = s.solve(x0, xg, z_guess=zg)
+    X2, U2, Z2, st2, it2, kk2 = s.solve(x0, xg, z_guess=zg)
+    assert np.array_equal(Z, Z2) and np.array_equal(st, st2)   # bitwise-deterministic
+    ok = st <= 1
+    assert ok.mean() >= 0.75, np.bincount(st)
+    dyn = X[:, 1:] - (X[:, :-1] + 0.1 * _f(X[:, :-1], U))
+    assert np.abs(dyn[ok]).max() <= 1e-8
+    assert np.abs(X[ok, 0] - x0[ok]).max() <= 1e-8
+    assert np.abs(X[ok, -1] - xg[ok]).max() <= 1e-2 + 1e-7               # final box
+    assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
+
+
+def _f(X, U):
+    L1, L2, M = P6["L1"], P6["L2"], P6["M"]
+    th, psi, phi, v = X[..., 2], X[..., 3], X[..., 4], X[..., 5]
+    return np.stack([v * np.cos(th), v * np.sin(th), v * np.tan(phi) / L1,
+                     -v * np.tan(phi) / L1 * (1 + M / L2 * np.cos(psi)) - v * np.sin(psi) / L2,
+                     U[..., 1], U[..., 0]], axis=-1)
+
+
+def test_reference_call_surface_obca(capsys):
+    """TrajectoryOptimization.plan / MPCTrackingControlObs.solve mirror the reference signatures."""
+    import ttmpc
+    from ttmpc import scenarios as sc
+    model = ttmpc.TruckTrailerModel(dict(P6, horizon=60))
+    obstacle_list = [{"center": (10.5, 2.6), "width": 3.0, "height": 2.0}]
+    planner = ttmpc.TrajectoryOptimization(model, dict(P6, horizon=60), sc.OBCA_Q, sc.OBCA_R,
+                                           {"lb": sc.OBCA_XLB, "ub": sc.OBCA_XUB}, {"lb": sc.OBCA_ULB, "ub": sc.OBCA_UUB},
+                                           obstacle_list)
+    states, inputs = planner.plan(np.array([0.0, 0.0, 0.02, 0.0, 0.0, 0.0]), np.array([26.0, -0.2, 0, 0, 0, 0]))
+    assert states.shape == (6, 61) and inputs.shape == (2, 60)
+    assert planner.last_status is not None
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    p = dict(P6, dt=0.05, horizon=50)
+    ctrl = ttmpc.MPCTrackingControlObs(model, p, sc.OBCA_Q, sc.OBCA_R, {"lb": sc.XLB, "ub": sc.XUB},
+                                       {"lb": sc.ULB, "ub": sc.UUB},
+                                       obstacle_list=[{"center": (o[0], o[1]), "width": o[2], "height": o[3]}
+                                                      for o in g["obstacles"]])
+    x0, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 1, 50, seed=0)
+    st_, in_ = ctrl.solve(x0[0], xr[0].T, ur[0].T)
+    assert st_.shape == (6, 51) and in_.shape == (2, 50)
+    assert "Cannot find a solution!" not in capsys.readouterr().out
+    with pytest.raises(ValueError):
+        ttmpc.TrajectoryOptimization(model, dict(P6, horizon=60), sc.OBCA_Q, sc.OBCA_R,
+                                     {"lb": sc.OBCA_XLB, "ub": sc.OBCA_XUB}, {"lb": sc.OBCA_ULB, "ub": sc.OBCA_UUB}, [])
+
+
+def test_obca_abi_errors():
+    import ctypes as C
+    import ttmpc
+    from ttmpc import _lib
+    L = ttmpc.lib()
+    cfg = _lib.TTConfig()
+    cfg.nx, cfg.nu, cfg.N, cfg.M = 6, 2, 20, 0
+    cfg.dt, cfg.L1, cfg.L2, cfg.Mh, cfg.W1, cfg.W2 = 0.1, 7.05, 12.45, 0.15, 3.05, 2.95
+    cfg.variant = ttmpc.TT_VARIANT_OBCA_PLAN
+    z6, z2 = np.zeros(36), np.zeros(4)
+    lb, ub = np.full(6, -1e20), np.full(6, 1e20)
+    h = C.c_void_p()
+    p = _lib._ptr
+    assert L.tt_create(C.byref(cfg), p(z6), p(z2), p(lb), p(ub), p(lb[:2].copy()), p(ub[:2].copy()), None, 0,
+                       C.byref(h)) == -22  # M = 0 obstacles
+    assert L.tt_obca_n(200, 6) == 200 * (8 + 96) + 6 + 96
