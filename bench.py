@@ -119,7 +119,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "c4", "cobs"],
+                    help="c2/c3/c5: tracking NMPC; c4: OBCA plans (trajectory_optimization.py); "
+                         "cobs: MPC+OBCA (mpc_control_obs.py)")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default by config)")
     ap.add_argument("--horizon", type=int, default=0)
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (0 = skip)")
@@ -127,7 +129,10 @@ def main():
     ap.add_argument("--traffic-csv", default="",
                     help="comma-separated rocprofv3 --pmc CSVs (FETCH_SIZE, WRITE_SIZE) of this config; "
                          "default: the committed profiles/ pair when the config is the default C2")
+    ap.add_argument("--max-iter", type=int, default=1000, help="OBCA configs: IPOPT max_iter (reference: 5000)")
     args = ap.parse_args()
+    if args.config in ("c4", "cobs"):
+        return main_obca(args)
 
     defaults = {"c2": (1024, 20), "c3": (8192, 40), "c5": (8192, 20)}
     B = args.batch or defaults[args.config][0]
@@ -243,6 +248,156 @@ def main():
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def obca_flops(N, M, iters):
+    """SURVEY §8(d) C4 formula per KKT solve: F_ric,obca = (N+1) [M (16^3/3 + 2*16^2*6 + 16*6^2) + F_ric],
+    plus the linearisation and forward sweep of the tracking formula; one KKT solve per iteration."""
+    F_ric_stage = 1539
+    per_kkt = (N + 1) * (M * (16 ** 3 / 3 + 2 * 16 ** 2 * 6 + 16 * 6 ** 2) + F_ric_stage) + N * (152 + 120)
+    F_lin = (N + 1) * (160 + 2 * M * 60)
+    return (iters + 1) * F_lin + iters * per_kkt
+
+
+def main_obca(args):
+    """OBCA configs: one step = one launch solving B independent OBCA NLPs to IPOPT tol 1e-8.
+    c4  : BASELINE configs[3] -- TrajectoryOptimization, 6 obstacle rectangles (obstacles.json[0:6]),
+          N=200, dt=0.1, B=256 Monte-Carlo re-plans around the reference's committed IPOPT plan
+          (data/state_traj.txt subsampled to 8 Hybrid-A*-style waypoints, start perturbed).
+    cobs: MPCTrackingControlObs as simulation.py drives it (N=50, dt=0.05, all 11 obstacles), windows of
+          the interpolated plan with perturbed initial states."""
+    import numpy as np
+
+    import ttmpc
+    from ttmpc import scenarios as sc
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    g = np.load(REPO / "tests" / "golden" / "reference_numpy.npz")
+    if args.config == "c4":
+        B, N, M = args.batch or 256, args.horizon or 200, 6
+        obs = sc.obstacles_array(sc.load_obstacles(REPO / "tests" / "golden" / "obstacles.json"))[:M]
+        x0, xg, zg = sc.obca_replan_batch(g["state_traj"], B, N, M, seed=rank_seed(rank))
+        params, bnd = sc.OBCA_PARAMS, (sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB)
+        variant, xr = ttmpc.TT_VARIANT_OBCA_PLAN, None
+    else:
+        B, N = args.batch or 256, args.horizon or 50
+        obs = g["obstacles"]
+        M = obs.shape[0]
+        x0, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], B, N, seed=rank_seed(rank))
+        params, bnd = dict(sc.OBCA_PARAMS, dt=0.05), (sc.XLB, sc.XUB, sc.ULB, sc.UUB)
+        variant, xg, zg = ttmpc.TT_VARIANT_TRACK_OBCA, None, None
+    solver = ttmpc.ObcaSolver(N, params, sc.OBCA_Q, sc.OBCA_R, *bnd, obs, variant=variant, max_iter=args.max_iter,
+                              device=local)
+    n = ttmpc.obca_n(N, M)
+    T = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_x0, d_xg, d_zg = T(x0), T(xg), T(zg)
+    d_xr, d_ur = (T(xr), T(ur)) if variant == ttmpc.TT_VARIANT_TRACK_OBCA else (None, None)
+    X = torch.empty((B, N + 1, 6), dtype=torch.float64, device=dev)
+    U = torch.empty((B, N, 2), dtype=torch.float64, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    kk = torch.empty(B, dtype=torch.float64, device=dev)
+    stream = torch.cuda.Stream(dev)
+    ptr = lambda a: 0 if a is None else a.data_ptr()  # noqa: E731
+
+    def step():
+        solver.solve_device(B, ptr(d_x0), ptr(d_xg), ptr(d_xr), ptr(d_ur), ptr(d_zg), X.data_ptr(), U.data_ptr(), 0,
+                            st.data_ptr(), it.data_ptr(), kk.data_ptr(), stream=stream.cuda_stream)
+
+    torch.cuda.synchronize(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    status, iters = st.cpu().numpy(), it.cpu().numpy()
+    ok = int(np.sum(status <= 1))
+    wall_max, ok_total, B_total = reduce_over_ranks(dist, wall, ok, B)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    F = float(np.sum(obca_flops(N, M, iters.astype(np.float64))))
+    achieved = F / (kernel_ms * 1e-3) / 1e12
+    name = "c4: TrajectoryOptimization OBCA plans" if args.config == "c4" else "cobs: MPC+OBCA (MPCTrackingControlObs)"
+    out = {
+        "metric": f"OBCA {'plan' if args.config == 'c4' else 'MPC+OBCA'} solves/sec (N={N}, M={M} obstacles, "
+                  f"n={n} variables)",
+        "value": round(ok_total * args.steps / wall_max, 2),
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic scenarios derived from the reference's committed OBCA plan (data/state_traj.txt)",
+        "config": {"workload": f"{name}, B={B}/GPU, N={N}, M={M}, IPOPT tol 1e-8, max_iter {args.max_iter}",
+                   "batch_per_gpu": B, "horizon": N, "obstacles": M,
+                   "parallelism": f"dp{world} (independent instance shards)"},
+        "solver": {"converged_or_acceptable": ok_total, "instances": B_total,
+                   "status_counts": {str(k): int(v) for k, v in zip(*np.unique(status, return_counts=True))},
+                   "iters_mean": float(iters.mean()), "iters_p50": float(np.median(iters)),
+                   "iters_max": int(iters.max()), "kernel_ms_per_launch": round(kernel_ms, 3)},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP64_PEAK_TFLOPS, 7), "traffic": None,
+                     "note": "latency-bound (serial Riccati over N stages per instance, one workgroup per instance); "
+                             "flops: SURVEY §8(d) C4 block-arrow formula x per-instance iterations"},
+    }
+    if args.cpu_budget > 0 and world == 1:
+        out["cpu_baseline"] = obca_cpu_baseline(args.config, N, M, params, bnd, obs, x0, xg, xr if xr is not None else None,
+                                                ur if args.config == "cobs" else None, zg, args.max_iter, args.cpu_budget)
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter, budget_s):
+    import numpy as np
+
+    from oracle import c_oracle as co
+    from ttmpc import scenarios as sc
+    ncores = len(os.sched_getaffinity(0))
+    threads = max(1, min(16, ncores))
+    P = co.make_obca_problem(N, params, sc.OBCA_Q, sc.OBCA_R, *bnd, obs, mode=0 if cfg == "c4" else 1,
+                             max_iter=max_iter)
+    done, solved, t0 = 0, 0, time.perf_counter()
+    B = x0.shape[0]
+    while True:
+        lo = done % B
+        hi = min(B, lo + threads)
+        sl = slice(lo, hi)
+        _, st, _, _ = co.obca_solve_batch(P, x0[sl], None if xg is None else xg[sl], None if xr is None else xr[sl],
+                                          None if ur is None else ur[sl], None if zg is None else zg[sl],
+                                          nthreads=threads)
+        done += hi - lo
+        solved += int(np.sum(st <= 1))
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": solved / el, "unit": "solves/s", "cores": threads, "kind": "port",
+            "sample": f"{done} instances ({solved} solved) of the same {cfg} workload in {el:.1f}s, OpenMP {threads} "
+                      f"threads on {ncores} visible host cores; oracle/c/tt_obca.c (same restated IPM)"}
 
 
 def read_traffic(paths):

@@ -311,6 +311,8 @@ int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_x
 }
 #endif
 
+static unsigned long long* g_obca_stamps = nullptr;  // diagnostics: set by ttx_obca_set_stamps
+
 int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
                                const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
                                double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream) {
@@ -368,6 +370,7 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
     a.iters = d_iters;
     a.kkt = d_kkt_res;
     a.ws = h->d_ows;
+    a.stamps = g_obca_stamps;
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
     e = ttmpc::launch_obca(a, s);
     if (e != hipSuccess) return hip_fail(h, e, "OBCA kernel launch");
@@ -419,6 +422,13 @@ int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgo
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(h, e, "OBCA solve");
     return 0;
+}
+
+/* diagnostics only (not part of include/ttmpc.h): per-instance phase cycle sums of the next OBCA launches
+ * into d_stamps[B][kObcaPhases] (device pointer; NULL switches it off) */
+int ttx_obca_set_stamps(unsigned long long* d_stamps) {
+    g_obca_stamps = d_stamps;
+    return ttmpc::kObcaPhases;
 }
 
 int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess, double* x_out,

@@ -98,7 +98,18 @@ struct Shared {
     double fth[kObcaMaxFilter], fph[kObcaMaxFilter];
     int nf;
     int flag;
+    unsigned long long stamp[kObcaPhases];
+    unsigned long long t0;
 };
+
+// diagnostic phase clock (thread 0, shader cycles); a no-op unless the caller passed a stamps buffer
+__device__ __forceinline__ void stamp(Shared& sh, bool on, int ph) {
+    if (on && threadIdx.x == 0) {
+        const unsigned long long t = clock64();
+        sh.stamp[ph] += t - sh.t0;
+        sh.t0 = t;
+    }
+}
 
 // workgroup reduction of NV values with per-value op; result uniform in every thread, fixed order
 template <int NV>
@@ -149,6 +160,7 @@ struct LogSum {
 struct Ctx {
     const ObcaArgs* a;
     double* ws;
+    double* lds;  // dynamic LDS for the staged sweeps, or nullptr (sweeps read the HBM workspace)
     int N, NP, nbk, tid, b;
     double dt;
     double xl[6], xu[6], ul[2], uu[2];
@@ -713,27 +725,90 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, Shared& sh, double mu, d
     return fail[0] == 0.0;
 }
 
+// Stage data of the serial sweeps, either straight from the HBM workspace (GSrc) or from LDS copies
+// staged by all four waves before the sweep (LSrc: region A = sweep inputs, region B = its outputs).
+struct GSrc {
+    const Ctx& c;
+    __device__ double QT(int i, int k) const { return c.S(S_QT + i, k); }
+    __device__ double QV(int i, int k) const { return c.S(S_QV + i, k); }
+    __device__ double RT(int i, int k) const { return c.S(S_RT + i, k); }
+    __device__ double RV(int i, int k) const { return c.S(S_RV + i, k); }
+    __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
+    __device__ double CR(int i, int k) const { return c.S(S_CR + i, k); }
+    __device__ double P(int i, int k) const { return c.S(S_P + i, k); }
+    __device__ double PV(int i, int k) const { return c.S(S_PV + i, k); }
+    __device__ double K(int i, int k) const { return c.S(S_K + i, k); }
+    __device__ double KF(int i, int k) const { return c.S(S_KF + i, k); }
+    __device__ void setP(int i, int k, double v) const { c.S(S_P + i, k) = v; }
+    __device__ void setPV(int i, int k, double v) const { c.S(S_PV + i, k) = v; }
+    __device__ void setK(int i, int k, double v) const { c.S(S_K + i, k) = v; }
+    __device__ void setKF(int i, int k, double v) const { c.S(S_KF + i, k) = v; }
+};
+// region A per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CR 6  (47);  region B: P 21 | PV 6 | K 12 | KF 2 (41)
+constexpr int LA = 47, LB = 41;
+struct LSrc {
+    const double* A;
+    double* B;
+    __device__ double QT(int i, int k) const { return A[k * LA + i]; }
+    __device__ double QV(int i, int k) const { return A[k * LA + 21 + i]; }
+    __device__ double RT(int i, int k) const { return A[k * LA + 27 + i]; }
+    __device__ double RV(int i, int k) const { return A[k * LA + 30 + i]; }
+    __device__ double AJ(int i, int k) const { return A[k * LA + 32 + i]; }
+    __device__ double CR(int i, int k) const { return A[k * LA + 41 + i]; }
+    __device__ double P(int i, int k) const { return B[k * LB + i]; }
+    __device__ double PV(int i, int k) const { return B[k * LB + 21 + i]; }
+    __device__ double K(int i, int k) const { return B[k * LB + 27 + i]; }
+    __device__ double KF(int i, int k) const { return B[k * LB + 39 + i]; }
+    __device__ void setP(int i, int k, double v) const { B[k * LB + i] = v; }
+    __device__ void setPV(int i, int k, double v) const { B[k * LB + 21 + i] = v; }
+    __device__ void setK(int i, int k, double v) const { B[k * LB + 27 + i] = v; }
+    __device__ void setKF(int i, int k, double v) const { B[k * LB + 39 + i] = v; }
+};
+__host__ __device__ inline size_t obca_lds_bytes(int N) { return (size_t)(LA + LB) * (N + 1) * 8; }
+constexpr size_t kObcaLdsMax = 150 * 1024;  // dynamic LDS budget for the staged sweeps (+ static Shared)
+
+// all threads: copy the sweep inputs of every stage into region A (field-major reads: coalesced in k)
+__device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
+    const int NP = c.NP;
+    for (int idx = threadIdx.x; idx < LA * NP; idx += T) {
+        const int f = idx / NP, k = idx - f * NP;
+        int g;
+        if (f < 21) g = S_QT + f;
+        else if (f < 27) g = S_QV + f - 21;
+        else if (f < 30) g = S_RT + f - 27;
+        else if (f < 32) g = S_RV + f - 30;
+        else if (f < 41) g = S_AJ + f - 32;
+        else g = S_CR + f - 41;
+        A[k * LA + f] = (k < c.N || (f < 27 || f >= 41)) ? c.S(g, k) : 0.0;
+    }
+}
+
 // ======== phase: Riccati backward sweep (wave 0).  Sets sh.flag = 1 if an input block is not PD ========
 // P_N = Q~_N; G = R~ + B'PB, H = B'PA, K = -G^-1 H, P_k = Q~_k + A'PA + H'K   (B = dt [e5 e4])
 // vector: p' = p_{k+1} - P_{k+1} c_{k+1}, kff = -G^-1 (r~ + B'p'), p_k = q~_k + A'p' + H'kff
-__device__ __noinline__ void riccati(const Ctx& c, Shared& sh) {
+template <class Src>
+__device__ __noinline__ void riccati(const Ctx& c, Shared& sh, const Src& src) {
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
     const int i = lane / 6, j = lane % 6;
     const bool act = lane < 36;
-    if (act) sh.P[lane] = c.S(S_QT + sy6(i, j), N);
-    if (act && i <= j) c.S(S_P + sy6(i, j), N) = sh.P[lane];
-    double pv = lane < 6 ? c.S(S_QV + lane, N) : 0.0;
-    if (lane < 6) c.S(S_PV + lane, N) = pv;
+    if (act) sh.P[lane] = src.QT(sy6(i, j), N);
+    if (act && i <= j) src.setP(sy6(i, j), N, sh.P[lane]);
+    double pv = lane < 6 ? src.QV(lane, N) : 0.0;
+    if (lane < 6) src.setPV(lane, N, pv);
     int fail = 0;
     wave_sync();
     for (int k = N - 1; k >= 0; --k) {
         double dj[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) dj[q] = c.S(S_AJ + q, k);
+        for (int q = 0; q < 9; ++q) dj[q] = src.AJ(q, k);
         double e[6];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = c.S(S_CR + q, k + 1);
+        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k + 1);
+        const double R0 = src.RT(0, k), R1 = src.RT(1, k), R3 = src.RT(2, k);
+        const double rv0 = src.RV(0, k), rv1 = src.RV(1, k);
+        const double qt = act && i <= j ? src.QT(sy6(i, j), k) : 0.0;
+        const double qv = lane < 6 ? src.QV(lane, k) : 0.0;
         // PA = P + P dJ   (column j of dJ: 2:{0,1} 3:{3} 4:{2,3} 5:{0,1,2,3})
         double pa = 0.0, pp = 0.0;
         if (act) {
@@ -751,32 +826,27 @@ __device__ __noinline__ void riccati(const Ctx& c, Shared& sh) {
             for (int q = 0; q < 6; ++q) pp -= sh.P[6 * lane + q] * e[q];
         }
         wave_sync();
-        const double R0 = c.S(S_RT, k), R1 = c.S(S_RT + 1, k), R3 = c.S(S_RT + 2, k);
         const double G00 = R0 + dt * dt * sh.P[35], G01 = R1 + dt * dt * sh.P[34], G11 = R3 + dt * dt * sh.P[28];
-        const double g00 = G00, det = G00 * G11 - G01 * G01;
-        if (!(g00 > 0.0) || !(det > 0.0)) fail = 1;
+        const double det = G00 * G11 - G01 * G01;
+        if (!(G00 > 0.0) || !(det > 0.0)) fail = 1;
         const double idet = 1.0 / det;
         const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
-        // H rows: H0[j] = dt PA[5][j], H1[j] = dt PA[4][j]
         double Pk = 0.0;
         if (act && i <= j) {
             const double* PAc = sh.PA;
             double at = PAc[6 * i + j];
-            // A'PA = PA + dJ' PA: column i of dJ
             if (i == 2) at += dj[0] * PAc[0 * 6 + j] + dj[2] * PAc[1 * 6 + j];
             else if (i == 3) at += dj[6] * PAc[3 * 6 + j];
             else if (i == 4) at += dj[4] * PAc[2 * 6 + j] + dj[7] * PAc[3 * 6 + j];
             else if (i == 5) at += dj[1] * PAc[0 * 6 + j] + dj[3] * PAc[1 * 6 + j] + dj[5] * PAc[2 * 6 + j] + dj[8] * PAc[3 * 6 + j];
             const double H0i = dt * PAc[30 + i], H1i = dt * PAc[24 + i], H0j = dt * PAc[30 + j], H1j = dt * PAc[24 + j];
             const double K0j = -(Gi00 * H0j + Gi01 * H1j), K1j = -(Gi01 * H0j + Gi11 * H1j);
-            Pk = c.S(S_QT + sy6(i, j), k) + at + H0i * K0j + H1i * K1j;
+            Pk = qt + at + H0i * K0j + H1i * K1j;
         }
-        // vector part
-        const double pp5 = readlane_d(pp, 5), pp4 = readlane_d(pp, 4);
         double ppl[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, q);
-        const double g0 = c.S(S_RV, k) + dt * pp5, g1 = c.S(S_RV + 1, k) + dt * pp4;
+        const double g0 = rv0 + dt * ppl[5], g1 = rv1 + dt * ppl[4];
         const double kf0 = -(Gi00 * g0 + Gi01 * g1), kf1 = -(Gi01 * g0 + Gi11 * g1);
         double pnew = 0.0;
         if (lane < 6) {
@@ -786,58 +856,51 @@ __device__ __noinline__ void riccati(const Ctx& c, Shared& sh) {
             else if (r == 3) at += dj[6] * ppl[3];
             else if (r == 4) at += dj[4] * ppl[2] + dj[7] * ppl[3];
             else if (r == 5) at += dj[1] * ppl[0] + dj[3] * ppl[1] + dj[5] * ppl[2] + dj[8] * ppl[3];
-            pnew = c.S(S_QV + r, k) + at + dt * sh.PA[30 + r] * kf0 + dt * sh.PA[24 + r] * kf1;
-        }
-        // K, H stored for the forward sweep
-        if (lane < 6) {
+            pnew = qv + at + dt * sh.PA[30 + r] * kf0 + dt * sh.PA[24 + r] * kf1;
             const double H0 = dt * sh.PA[30 + lane], H1 = dt * sh.PA[24 + lane];
-            c.S(S_H + lane, k) = H0;
-            c.S(S_H + 6 + lane, k) = H1;
-            c.S(S_K + lane, k) = -(Gi00 * H0 + Gi01 * H1);
-            c.S(S_K + 6 + lane, k) = -(Gi01 * H0 + Gi11 * H1);
+            src.setK(lane, k, -(Gi00 * H0 + Gi01 * H1));
+            src.setK(6 + lane, k, -(Gi01 * H0 + Gi11 * H1));
         }
         if (lane == 0) {
-            c.S(S_KF, k) = kf0;
-            c.S(S_KF + 1, k) = kf1;
-            c.S(S_GI, k) = Gi00;
-            c.S(S_GI + 1, k) = Gi01;
-            c.S(S_GI + 2, k) = Gi11;
+            src.setKF(0, k, kf0);
+            src.setKF(1, k, kf1);
         }
         wave_sync();
         if (act && i <= j) {
             sh.P[6 * i + j] = Pk;
             sh.P[6 * j + i] = Pk;
-            c.S(S_P + sy6(i, j), k) = Pk;
+            src.setP(sy6(i, j), k, Pk);
         }
         pv = pnew;
-        if (lane < 6) c.S(S_PV + lane, k) = pv;
+        if (lane < 6) src.setPV(lane, k, pv);
         wave_sync();
     }
     if (lane == 0) sh.flag = fail;
 }
 
 // ======== phase: forward sweep (wave 0) into step buffer buf ========
-__device__ __noinline__ void forward(const Ctx& c, int buf) {
+template <class Src>
+__device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
-    double dx = lane < 6 ? -c.S(S_CR + lane, 0) : 0.0;
+    double dx = lane < 6 ? -src.CR(lane, 0) : 0.0;
     for (int k = 0;; ++k) {
         double dxv[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) dxv[q] = readlane_d(dx, q);
         if (lane < 6) {
-            double t = c.S(S_PV + lane, k);
+            double t = src.PV(lane, k);
 #pragma unroll
-            for (int q = 0; q < 6; ++q) t += c.S(S_P + sy6(lane, q), k) * dxv[q];
+            for (int q = 0; q < 6; ++q) t += src.P(sy6(lane, q), k) * dxv[q];
             c.S(S_YCP + 6 * buf + lane, k) = -t;
             c.S(S_DX + 6 * buf + lane, k) = dx;
         }
         if (k == N) break;
-        double du0 = c.S(S_KF, k), du1 = c.S(S_KF + 1, k);
+        double du0 = src.KF(0, k), du1 = src.KF(1, k);
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
-            du0 += c.S(S_K + q, k) * dxv[q];
-            du1 += c.S(S_K + 6 + q, k) * dxv[q];
+            du0 += src.K(q, k) * dxv[q];
+            du1 += src.K(6 + q, k) * dxv[q];
         }
         if (lane == 0) {
             c.S(S_DU + 2 * buf, k) = du0;
@@ -845,11 +908,11 @@ __device__ __noinline__ void forward(const Ctx& c, int buf) {
         }
         if (lane < 6) {
             const int r = lane;
-            double t = dx - c.S(S_CR + r, k + 1);
-            if (r == 0) t += c.S(S_AJ + 0, k) * dxv[2] + c.S(S_AJ + 1, k) * dxv[5];
-            else if (r == 1) t += c.S(S_AJ + 2, k) * dxv[2] + c.S(S_AJ + 3, k) * dxv[5];
-            else if (r == 2) t += c.S(S_AJ + 4, k) * dxv[4] + c.S(S_AJ + 5, k) * dxv[5];
-            else if (r == 3) t += c.S(S_AJ + 6, k) * dxv[3] + c.S(S_AJ + 7, k) * dxv[4] + c.S(S_AJ + 8, k) * dxv[5];
+            double t = dx - src.CR(r, k + 1);
+            if (r == 0) t += src.AJ(0, k) * dxv[2] + src.AJ(1, k) * dxv[5];
+            else if (r == 1) t += src.AJ(2, k) * dxv[2] + src.AJ(3, k) * dxv[5];
+            else if (r == 2) t += src.AJ(4, k) * dxv[4] + src.AJ(5, k) * dxv[5];
+            else if (r == 3) t += src.AJ(6, k) * dxv[3] + src.AJ(7, k) * dxv[4] + src.AJ(8, k) * dxv[5];
             else if (r == 4) t += dt * du1;
             else t += dt * du0;
             dx = t;
@@ -1388,22 +1451,43 @@ __device__ __noinline__ double phase_compl(const Ctx& c, Shared& sh, double mu) 
 
 // Newton solve for the current residual arrays (S_CR / B_DR / sh.dfr) with the given dw into buffer buf.
 // Returns false when the Riccati/blocks are not positive definite.
-__device__ bool newton_solve(const Ctx& c, Shared& sh, double mu, double dw, int buf) {
-    if (!phase_factor(c, sh, mu, dw)) return false;
-    if (threadIdx.x < 64) riccati(c, sh);
+__device__ __noinline__ bool newton_solve(const Ctx& c, Shared& sh, double mu, double dw, int buf) {
+    const bool on = c.a->stamps != nullptr;
+    stamp(sh, on, OPH_UPD);
+    const bool f = phase_factor(c, sh, mu, dw);
+    stamp(sh, on, OPH_FACTOR);
+    if (!f) return false;
+    if (c.lds) {
+        stage_inputs(c, c.lds);
+        __syncthreads();
+        stamp(sh, on, OPH_COMPL);  // (diagnostic: staging cost booked under 'compl')
+        const LSrc src{c.lds, c.lds + (size_t)LA * c.NP};
+        if (threadIdx.x < 64) riccati(c, sh, src);
+        __syncthreads();
+        stamp(sh, on, OPH_RIC);
+        if (sh.flag) return false;
+        if (threadIdx.x < 64) forward(c, src, buf);
+    } else {
+        const GSrc src{c};
+        if (threadIdx.x < 64) riccati(c, sh, src);
+        __syncthreads();
+        stamp(sh, on, OPH_RIC);
+        if (sh.flag) return false;
+        if (threadIdx.x < 64) forward(c, src, buf);
+    }
     __syncthreads();
-    if (sh.flag) return false;
-    if (threadIdx.x < 64) forward(c, buf);
-    __syncthreads();
+    stamp(sh, on, OPH_FWD);
     return true;
 }
 
 // ---------------- the kernel ----------------
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void obca_kernel(ObcaArgs args) {
     __shared__ Shared sh;
+    extern __shared__ double dyn_lds[];
     const ObcaArgs& a = args;
     Ctx c;
     c.a = &args;
+    c.lds = obca_lds_bytes(a.N) <= kObcaLdsMax ? dyn_lds : nullptr;
     c.b = blockIdx.x;
     c.N = a.N;
     c.NP = a.N + 1;
@@ -1442,6 +1526,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     const size_t nz = obca_n(N, a.M);
     const double* zg = a.zg ? a.zg + (size_t)c.b * nz : nullptr;
 
+    const bool ston = a.stamps != nullptr;
+    if (tid == 0) {
+        for (int i = 0; i < kObcaPhases; ++i) sh.stamp[i] = 0;
+        sh.t0 = clock64();
+    }
+    const unsigned long long tstart = clock64();
     // ---------------- initial point (bound push, slacks = pushed d(x0), multipliers 1 / 0) ----------------
     bool infeasible = false;
 #pragma unroll
@@ -1542,7 +1632,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
         for (iter = 0;; ++iter) {
             double red[8];
+            stamp(sh, ston, OPH_UPD);
             phase_lin(c, sh, red);
+            stamp(sh, ston, OPH_LIN);
             const double dinf = red[0], pinf = red[1], c0 = red[2];
             const double th0 = red[5];
             if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; break; }
@@ -1560,6 +1652,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             // ---- barrier update (monotone, Fiacco-McCormick) ----
             while (mu > a.tol / 10.0 * 1.0000001) {
                 const double Emu = fmax(fmax(dinf / sd, pinf), phase_compl(c, sh, mu) / sc);
+                stamp(sh, ston, OPH_COMPL);
                 if (!(Emu <= kappa_eps * mu)) break;
                 mu = fmax(a.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
                 tau = fmax(0.99, 1.0 - mu);
@@ -1591,6 +1684,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             if (dw > 0) dw_last = dw;
             double rec[4];
             phase_recover(c, sh, mu, dw, tau, 0, rec);
+            stamp(sh, ston, OPH_REC);
             const double ap = rec[0], Dm = rec[2], rel = rec[3];
             double az = rec[1];
             // ---- filter line search ----
@@ -1611,6 +1705,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             for (int ls = 0; !accepted; ++ls) {
                 double tr[3];
                 phase_trial(c, sh, mu, alpha, 0, tr);
+                stamp(sh, ston, OPH_TRIAL);
                 const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
                 bool okls = false;
                 if (isfinite(tr[1]) && tr[0] <= th_max && !in_filter(sh, tr[0], tr[1])) {
@@ -1642,9 +1737,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                         if (!newton_solve(c, sh, mu, dw, 1)) break;
                         double rs[4];
                         phase_recover(c, sh, mu, dw, tau, 1, rs);
+                        stamp(sh, ston, OPH_REC);
                         a_soc = rs[0];
                         double t2[3];
                         phase_trial(c, sh, mu, a_soc, 1, t2);
+                        stamp(sh, ston, OPH_TRIAL);
                         th_t = t2[0];
                         bool ok2 = false;
                         if (isfinite(t2[1]) && t2[0] <= th_max && !in_filter(sh, t2[0], t2[1])) {
@@ -1668,6 +1765,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             __syncthreads();
             phase_update(c, sh, mu, alpha, az, buf);
             __syncthreads();
+            stamp(sh, ston, OPH_UPD);
         }
     }
     // ---------------- outputs ----------------
@@ -1698,6 +1796,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         a.status[c.b] = status;
         if (a.iters) a.iters[c.b] = iter;
         if (a.kkt) a.kkt[c.b] = E0;
+        if (ston) {
+            sh.stamp[OPH_TOTAL] = clock64() - tstart;
+            for (int i = 0; i < kObcaPhases; ++i) a.stamps[(size_t)c.b * kObcaPhases + i] = sh.stamp[i];
+        }
     }
 }
 
@@ -1705,7 +1807,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
 
 hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream) {
     if (a.B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(obca_kernel, dim3(a.B), dim3(T), 0, stream, a);
+    const size_t need = obca_lds_bytes(a.N);
+    const size_t bytes = need <= kObcaLdsMax ? need : 0;
+    static size_t configured = 0;
+    if (bytes > 64 * 1024 && configured < bytes) {
+        hipError_t e = hipFuncSetAttribute((const void*)obca_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+        if (e != hipSuccess) return e;
+        configured = bytes;
+    }
+    hipLaunchKernelGGL(obca_kernel, dim3(a.B), dim3(T), bytes, stream, a);
     return hipGetLastError();
 }
 
