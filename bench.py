@@ -1,6 +1,8 @@
 """Benchmark: batched truck-trailer NMPC solves on MI355X (BASELINE.json metric).
 
-    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5] [--batch B] [--horizon H]
+    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5|c4|cobs] [--batch B] [--horizon H]
+
+c5 is the sharded path: one global batch on rank 0, RCCL scatter -> solve -> gather (ttmpc/sharded.py).
 
 A "step" = one launch of the HIP solver over one batch of B independent NLP instances (B solves),
 inputs already resident in HBM.  Default workload = BASELINE configs[1] (C2): B = 1024 instances
@@ -133,8 +135,10 @@ def main():
     args = ap.parse_args()
     if args.config in ("c4", "cobs"):
         return main_obca(args)
+    if args.config == "c5":
+        return main_c5(args)
 
-    defaults = {"c2": (1024, 20), "c3": (8192, 40), "c5": (8192, 20)}
+    defaults = {"c2": (1024, 20), "c3": (8192, 40)}
     B = args.batch or defaults[args.config][0]
     N = args.horizon or defaults[args.config][1]
 
@@ -245,6 +249,103 @@ def main():
         out["p99_latency_ms"] = round(p99, 4)
     if args.cpu_budget > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.config, B, N, rank_seed(rank), args.cpu_budget)
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def main_c5(args):
+    """BASELINE configs[4] (C5): ONE global batch of B_total = 65536 mixed test_cases.json scenarios
+    (N = 20) resident on rank 0's GPU, sharded over the ranks with RCCL (torch.distributed "nccl"):
+    a step = scatter -> per-rank solve -> gather to rank 0 -> stats all-reduce (ttmpc.sharded).
+    Total work is fixed as N grows: strong scaling."""
+    import numpy as np
+
+    import ttmpc
+    from oracle import ttmpc_oracle as to  # constants only
+    from ttmpc.sharded import ShardedBatch, gpu_shard_solver
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    B_total, N = args.batch or 65536, args.horizon or 20
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl", device_id=dev)
+    solver = ttmpc.BatchSolver(N, to.DEFAULT_PARAMS, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB,
+                               to.MPC_UUB, device=local)
+    stream = torch.cuda.Stream(dev)
+    sb = ShardedBatch(B_total, N, gpu_shard_solver(solver, stream), device=dev)
+    if rank == 0:
+        x0, xr, ur = workload("c5", B_total, N, seed=rank_seed(0))
+        sb.pack_inputs(x0, xr, ur)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            sb.step()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.steps):
+            ssum, smax = sb.step()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+    step_ms_local = e0.elapsed_time(e1) / args.steps
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    stats = ShardedBatch.stats(ssum, smax)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # kernel-only time of this rank's shard: one more solve on the same stream, HIP events around it
+    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        k0.record(stream)
+        sb.solve_shard(sb.x0, sb.xr, sb.ur, sb.X, sb.U, sb.st, sb.it, sb.kkt)
+        k1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = k0.elapsed_time(k1)
+    X, U, st, it, kk = sb.results()
+    F_shard = float(np.sum(flops_per_solve(N, sb.it[: sb.valid].cpu().numpy().astype(np.float64))))
+    achieved = F_shard / (kernel_ms * 1e-3) / 1e12
+    out = {
+        "metric": "MPC solves/sec (N=20, nx=6, nu=2; BASELINE label says nx=5, the reference model has 6 states)"
+        if N == 20 else f"MPC solves/sec (N={N}, nx=6, nu=2)",
+        "value": round(B_total * args.steps / wall_max, 1),
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (test_cases.json start/goal poses x Monte-Carlo start perturbations, straight-line "
+                "references; the global batch is generated on rank 0 and scattered)",
+        "config": {"workload": f"c5: ONE global batch B={B_total}, N={N}, tracking NMPC (mpc_control.py NLP), IPOPT "
+                               f"tol 1e-8; scatter/solve/gather over RCCL ({world} ranks x {sb.per} instances)",
+                   "global_batch": B_total, "horizon": N,
+                   "parallelism": f"dp{world} (contiguous shards; RCCL scatter + gather + stats all-reduce per step)"},
+        "solver": {"converged_or_acceptable": stats["converged"], "instances": stats["instances"],
+                   "iters_mean": float(it.mean()), "iters_max": stats["iters_max"], "kkt_max": stats["kkt_max"],
+                   "step_ms_rank0_hip_events": round(step_ms_local, 4),
+                   "kernel_ms_per_launch": round(kernel_ms, 4)},
+        "roofline": {"bound": "mfma", "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP64_PEAK_TFLOPS, 6), "traffic": None,
+                     "note": "rank-0 shard kernel (track_kernel) only; SURVEY §8(d) flop formula x per-instance "
+                             "iterations"},
+    }
+    if args.cpu_budget > 0 and world == 1:
+        out["cpu_baseline"] = cpu_baseline("c5", min(B_total, 8192), N, rank_seed(0), args.cpu_budget)
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -1678,9 +1678,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             for (int attempt = 0; attempt < 40; ++attempt) {
                 if (newton_solve(c, sh, mu, dw, 0)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-                if (dw > 1e40) break;
+                if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
             }
-            if (!ok) { status = 4; break; }
+            if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
             if (dw > 0) dw_last = dw;
             double rec[4];
             phase_recover(c, sh, mu, dw, tau, 0, rec);

@@ -945,9 +945,9 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
                 if (phase_riccati(c, dw)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0))
                                  : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-                if (dw > 1e40) break;
+                if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
             }
-            if (!ok) { status = 4; break; }
+            if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
             if (dw > 0.0) dw_last = dw;
             STAMP(PH_RIC);
             phase_forward(c, rCC, rBH, rDX);

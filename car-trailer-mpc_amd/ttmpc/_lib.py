@@ -16,9 +16,9 @@ LIB_PATH = Path(__file__).resolve().parent / "libttmpc.so"
 if os.environ.get("TTMPC_LIB"):
     LIB_PATH = Path(os.environ["TTMPC_LIB"]).resolve()
 
-TT_CONVERGED, TT_ACCEPTABLE, TT_MAX_ITER, TT_INFEASIBLE, TT_NONFINITE = range(5)
+TT_CONVERGED, TT_ACCEPTABLE, TT_MAX_ITER, TT_INFEASIBLE, TT_NONFINITE, TT_STEP_FAILED = range(6)
 TT_VARIANT_TRACK, TT_VARIANT_TRACK_OBCA, TT_VARIANT_NMPC, TT_VARIANT_FUZZY, TT_VARIANT_OBCA_PLAN = range(5)
-STATUS_NAMES = {0: "converged", 1: "acceptable", 2: "max_iter", 3: "infeasible", 4: "non-finite"}
+STATUS_NAMES = {0: "converged", 1: "acceptable", 2: "max_iter", 3: "infeasible", 4: "non-finite", 5: "step_failed"}
 
 
 class TTConfig(C.Structure):

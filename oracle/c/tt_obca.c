@@ -1252,9 +1252,9 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         for (int attempt = 0; attempt < 40; ++attempt) {
             if (factor(W, dw) == 0) { ok = 1; break; }
             dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-            if (dw > 1e40) break;
+            if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
         }
-        if (!ok) { status = 4; break; }
+        if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
         if (dw > 0) dw_last = dw;
         for (int i = 0; i < 4 * W->nb; ++i) W->dr[i] = W->d[i] - W->s[i];
         double fr[6] = {0};

@@ -470,9 +470,9 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
                 dc = 1e-8 * pow(mu, 0.25);
             }
             dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-            if (dw > 1e40) break;
+            if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
         }
-        if (!ok) { status = 4; break; }
+        if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
         if (dw > 0) dw_last = dw;
         /* ---- bound-multiplier steps ---- */
         for (int v = 0; v < n; ++v) {
