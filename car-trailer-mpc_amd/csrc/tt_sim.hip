@@ -1,0 +1,328 @@
+// Closed-loop simulation step on gfx950: the per-timestep glue of python-files/simulation.py around
+// the NLP solve, batched over B independent Monte-Carlo instances and kept resident in HBM between
+// steps.  All kernels here are tiny and HBM/launch bound (a few hundred bytes
+// per instance per step); they exist so that a closed loop never leaves the device.
+//
+//   sim_window_kernel   reference window with end padding       simulation.py:486-501
+//                       + noisy state measurement               simulation.py:509-513, 151-165
+//   collision_kernel    SAT OBB-vs-AABB over a trajectory       simulation.py:224-385
+//   plant_kernel        disturbed plant update                  simulation.py:167-199 (+50-149)
+//                       (zero control after an NMPC failure     simulation_nmpc.py:204-218)
+//   warm_kernel         shifted warm start for NMPC / fuzzy     mpc_control_nmpc.py:69-100
+//   record_kernel       keep the last successful optimum        mpc_control_nmpc.py:107-111
+//   interp_kernel       OBCA plan -> MPC rate (dt 0.1 -> 0.05)  simulation.py:201-218
+#include <errno.h>
+#include <math.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include "ttmpc.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__host__ __device__ inline int grid_for(long long n) { return (int)((n + kThreads - 1) / kThreads); }
+
+// ---- reference window + measured state, one thread per (instance, stage) --------------------------
+// xr[j] = plan_x[min(k+j, Np)] in all three branches of simulation.py:486-501; ur[j] = plan_u[min(k+j,
+// Np-1)] while k < Np, else 0 (the k >= N branch zeroes the inputs).
+__global__ void __launch_bounds__(kThreads) sim_window_kernel(int B, int N, int k, int Np, const double* __restrict__ px,
+                                                              const double* __restrict__ pu, int per_instance,
+                                                              const double* __restrict__ state,
+                                                              const double* __restrict__ noise,
+                                                              double* __restrict__ xmeas, double* __restrict__ xr,
+                                                              double* __restrict__ ur) {
+    const long long t = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const long long total = (long long)B * (N + 1);
+    if (t >= total) return;
+    const int b = (int)(t / (N + 1)), j = (int)(t % (N + 1));
+    const size_t pb = per_instance ? (size_t)b : 0;
+    const int sx = min(k + j, Np);
+    const double* src = px + (pb * (Np + 1) + sx) * 6;
+    double* dst = xr + ((size_t)b * (N + 1) + j) * 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dst[i] = src[i];
+    if (j < N) {
+        double* du = ur + ((size_t)b * N + j) * 2;
+        if (k < Np) {
+            const double* su = pu + (pb * Np + min(k + j, Np - 1)) * 2;
+            du[0] = su[0];
+            du[1] = su[1];
+        } else {
+            du[0] = 0.0;
+            du[1] = 0.0;
+        }
+    } else if (xmeas) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double s = state[(size_t)b * 6 + i];
+            xmeas[(size_t)b * 6 + i] = noise ? s + noise[(size_t)b * 6 + i] : s;
+        }
+    }
+}
+
+// ---- SAT collision: check_obb_aabb_collision for truck and trailer, every pose, every obstacle ------
+// Evaluated literally as the reference does (corners = R local + c, projections min/max of corners . axis,
+// strict '<' gap test, touching = collision), without FMA contraction so the arithmetic is numpy's.
+struct Poly {
+    double x[4], y[4];
+};
+
+__device__ __forceinline__ void rect_corners(double cx, double cy, double hl, double hw, double ang, Poly& p) {
+#pragma clang fp contract(off)
+    const double c = cos(ang), s = sin(ang);
+    const double lx[4] = {hl, hl, -hl, -hl}, ly[4] = {hw, -hw, -hw, hw};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        p.x[i] = (c * lx[i] + (-s) * ly[i]) + cx;
+        p.y[i] = (s * lx[i] + c * ly[i]) + cy;
+    }
+}
+
+__device__ __forceinline__ void proj(const Poly& p, double ax, double ay, double& lo, double& hi) {
+#pragma clang fp contract(off)
+    lo = hi = p.x[0] * ax + p.y[0] * ay;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        const double v = p.x[i] * ax + p.y[i] * ay;
+        lo = fmin(lo, v);
+        hi = fmax(hi, v);
+    }
+}
+
+__device__ bool obb_aabb(const Poly& o, double cx, double cy, double hw, double hh) {
+#pragma clang fp contract(off)
+    Poly a;
+    a.x[0] = cx + hw; a.y[0] = cy + hh;
+    a.x[1] = cx + hw; a.y[1] = cy - hh;
+    a.x[2] = cx - hw; a.y[2] = cy - hh;
+    a.x[3] = cx - hw; a.y[3] = cy + hh;
+    double ax[4] = {1.0, 0.0, 0.0, 0.0}, ay[4] = {0.0, 1.0, 0.0, 0.0};
+    int na = 2;
+    const double e1x = o.x[1] - o.x[0], e1y = o.y[1] - o.y[0];
+    const double e2x = o.x[3] - o.x[0], e2y = o.y[3] - o.y[0];
+    const double n1 = sqrt(e1x * e1x + e1y * e1y), n2 = sqrt(e2x * e2x + e2y * e2y);
+    if (n1 > 1e-9) { ax[na] = -e1y / n1; ay[na] = e1x / n1; ++na; }
+    if (n2 > 1e-9) { ax[na] = -e2y / n2; ay[na] = e2x / n2; ++na; }
+    for (int i = 0; i < na; ++i) {
+        double omin, omax, amin, amax;
+        proj(o, ax[i], ay[i], omin, omax);
+        proj(a, ax[i], ay[i], amin, amax);
+        if (omax < amin || amax < omin) return false;
+    }
+    return true;
+}
+
+__device__ bool pose_collides(const double* q, const double* obs, int M, double L1, double L2, double Mh, double W1,
+                              double W2) {
+#pragma clang fp contract(off)
+    const double x = q[0], y = q[1], th = q[2], ps = q[3];
+    Poly v, t;
+    rect_corners(x + cos(th) * L1 / 2, y + sin(th) * L1 / 2, L1 / 2, W1 / 2, th, v);          // 318-326
+    const double hx = x - cos(th) * Mh, hy = y - sin(th) * Mh;                                    // 328-335
+    rect_corners(hx - cos(th + ps) * L2 / 2, hy - sin(th + ps) * L2 / 2, L2 / 2, W2 / 2, th + ps, t);
+    for (int m = 0; m < M; ++m) {
+        const double* o = obs + 4 * m;
+        if (obb_aabb(v, o[0], o[1], o[2] / 2, o[3] / 2)) return true;
+        if (obb_aabb(t, o[0], o[1], o[2] / 2, o[3] / 2)) return true;
+    }
+    return false;
+}
+
+// one wave per instance, lanes over the K poses; flag = any pose collides (check_trajectory_collision)
+__global__ void __launch_bounds__(64) collision_kernel(int B, int K, long long stride_b, int stride_k,
+                                                      const double* __restrict__ poses, const double* __restrict__ obs,
+                                                      int M, double L1, double L2, double Mh, double W1, double W2,
+                                                      int* __restrict__ flag) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= B) return;
+    bool hit = false;
+    for (int j = lane; j < K; j += 64)
+        hit = hit || pose_collides(poses + b * stride_b + (long long)j * stride_k, obs, M, L1, L2, Mh, W1, W2);
+    const unsigned long long any = __ballot(hit);
+    if (lane == 0) flag[b] = any != 0ull ? 1 : 0;
+}
+
+// ---- disturbed plant: update(q, u, params, DISTURBANCE_PARAMS), simulation.py:167-199 ------------------
+__global__ void __launch_bounds__(kThreads) plant_kernel(int B, tt_plant p, double* __restrict__ state,
+                                                         const double* __restrict__ u, long long u_stride,
+                                                         const int* __restrict__ status, int zero_on_fail,
+                                                         double* __restrict__ u_applied) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= B) return;
+    double q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = state[(size_t)b * 6 + i];
+    double a = u[b * u_stride], om = u[b * u_stride + 1];
+    if (zero_on_fail && status && status[b] > TT_ACCEPTABLE) { a = 0.0; om = 0.0; }   // simulation_nmpc.py:208-214
+    if (u_applied) { u_applied[(size_t)b * 2] = a; u_applied[(size_t)b * 2 + 1] = om; }
+    if (p.enable) { a *= p.friction_coeff; om *= p.slippage_coeff; }                     // apply_disturbances 66-80
+    const double th = q[2], ps = q[3], ph = q[4], v = q[5];
+    double qd[6];                                                                        // f_dyn 34-48
+    qd[0] = v * cos(th);
+    qd[1] = v * sin(th);
+    qd[2] = v * tan(ph) / p.L1;
+    qd[3] = -v * tan(ph) / p.L1 * (1 + p.Mh / p.L2 * cos(ps)) - v * sin(ps) / p.L2;
+    qd[4] = om;
+    qd[5] = a;
+    if (p.enable) {                                                                      // slippage 89-115
+        const double slip = 1.0 - fmin(fabs(ph) * fabs(v) * p.slip_angle_max, 0.3);
+        qd[2] *= slip;
+        qd[3] *= slip;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = q[i] + qd[i] * p.dt;
+    if (p.enable) {                                                                      // lateral slip 117-149
+        const double mag = p.lateral_slip_gain * fabs(v) * fabs(ph);
+        q[0] += mag * cos(th + M_PI / 2) * p.dt;
+        q[1] += mag * sin(th + M_PI / 2) * p.dt;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) state[(size_t)b * 6 + i] = q[i];
+}
+
+// ---- NMPC warm start: z_guess = have ? shift(last) : [xr_0, ur_0, ..., xr_N] ----------------------------
+// shift (mpc_control_nmpc.py:69-88): stages 1..N-1 move to 0..N-2; the last stage is built from
+// last[-8:-2] / last[-2:] (bug_compatible: [u_{N-1}, x_N[0:4]] and x_N[4:6]) or the intended x_N / u_{N-1}.
+__global__ void __launch_bounds__(kThreads) warm_kernel(int B, int N, const double* __restrict__ last,
+                                                        const int* __restrict__ have, const double* __restrict__ xr,
+                                                        const double* __restrict__ ur, int bug_compatible,
+                                                        double* __restrict__ zg) {
+    const int n = 8 * N + 6;
+    const long long t = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= (long long)B * n) return;
+    const int b = (int)(t / n), e = (int)(t % n);
+    const double* L = last + (size_t)b * n;
+    double v;
+    if (!have[b]) {
+        const int k = e / 8, r = e % 8;   // reference-copy guess (mpc_control_nmpc.py:60-67)
+        v = k == N ? xr[((size_t)b * (N + 1) + N) * 6 + r]
+                   : (r < 6 ? xr[((size_t)b * (N + 1) + k) * 6 + r] : ur[((size_t)b * N + k) * 2 + (r - 6)]);
+    } else if (e < 8 * (N - 1)) {
+        v = L[e + 8];
+    } else {
+        const int r = e - 8 * (N - 1);    // 0..13: last_state(6), last_input(2), last_state(6)
+        const int rs = r < 6 ? r : (r < 8 ? 6 + (r - 6) : r - 8);
+        if (bug_compatible) {
+            v = rs < 6 ? L[n - 8 + rs] : L[n - 2 + (rs - 6)];
+        } else {
+            v = rs < 6 ? L[8 * N + rs] : L[8 * (N - 1) + 6 + (rs - 6)];
+        }
+    }
+    zg[t] = v;
+}
+
+// last <- pack(X, U) where the solve succeeded (status <= acceptable); have[b] |= success
+__global__ void __launch_bounds__(kThreads) record_kernel(int B, int N, const double* __restrict__ X,
+                                                          const double* __restrict__ U, const int* __restrict__ status,
+                                                          double* __restrict__ last, int* __restrict__ have) {
+    const int n = 8 * N + 6;
+    const long long t = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= (long long)B * n) return;
+    const int b = (int)(t / n), e = (int)(t % n);
+    if (status[b] > TT_ACCEPTABLE) return;
+    const int k = e / 8, r = e % 8;
+    last[t] = k == N ? X[((size_t)b * (N + 1) + N) * 6 + r]
+                     : (r < 6 ? X[((size_t)b * (N + 1) + k) * 6 + r] : U[((size_t)b * N + k) * 2 + (r - 6)]);
+    if (e == 0) have[b] = 1;
+}
+
+// ---- do_interpolation (simulation.py:201-218): linear states, zero-order-hold inputs, factor n --------
+__global__ void __launch_bounds__(kThreads) interp_kernel(int B, int Np, int n, const double* __restrict__ sx,
+                                                          const double* __restrict__ su, double* __restrict__ dx,
+                                                          double* __restrict__ du) {
+#pragma clang fp contract(off)
+    const int Nn = n * Np;
+    const long long t = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= (long long)B * (Nn + 1)) return;
+    const int b = (int)(t / (Nn + 1)), c = (int)(t % (Nn + 1));
+    const double* S = sx + (size_t)b * (Np + 1) * 6;
+    double* D = dx + ((size_t)b * (Nn + 1) + c) * 6;
+    if (c == Nn) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) D[i] = S[(size_t)Np * 6 + i];
+        return;
+    }
+    const int k = c / n, m = c % n;
+    const double tt = (double)m / (double)n;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) D[i] = (1 - tt) * S[(size_t)k * 6 + i] + tt * S[(size_t)(k + 1) * 6 + i];
+    const double* Su = su + ((size_t)b * Np + k) * 2;
+    double* Du = du + ((size_t)b * Nn + c) * 2;
+    Du[0] = Su[0];
+    Du[1] = Su[1];
+}
+
+int launched(const char* where) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        fprintf(stderr, "ttmpc: %s launch failed: %s\n", where, hipGetErrorString(e));
+        return -EIO;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tt_sim_window_device(int B, int N, int k, int Np, const double* plan_x, const double* plan_u, int per_instance,
+                         const double* state, const double* meas_noise, double* x_meas, double* xref, double* uref,
+                         void* stream) {
+    if (B < 0 || N < 1 || Np < 1 || k < 0 || !plan_x || !plan_u || !xref || !uref || (x_meas && !state))
+        return -EINVAL;
+    if (B == 0) return 0;
+    const long long tot = (long long)B * (N + 1);
+    hipLaunchKernelGGL(sim_window_kernel, dim3(grid_for(tot)), dim3(kThreads), 0, (hipStream_t)stream, B, N, k, Np,
+                       plan_x, plan_u, per_instance, state, meas_noise, x_meas, xref, uref);
+    return launched("sim_window_kernel");
+}
+
+int tt_collision_device(int B, int K, const double* poses, long long stride_b, int stride_k, const double* obstacles,
+                        int M, const tt_plant* p, int* flag, void* stream) {
+    if (B < 0 || K < 1 || !poses || !p || !flag || M < 0 || (M > 0 && !obstacles) || stride_k < 4) return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(collision_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, B, K, stride_b, stride_k, poses,
+                       obstacles, M, p->L1, p->L2, p->Mh, p->W1, p->W2, flag);
+    return launched("collision_kernel");
+}
+
+int tt_plant_update_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
+                           const int* status, int zero_on_fail, double* u_applied, void* stream) {
+    if (B < 0 || !p || !state || !u || u_stride < 2) return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(plant_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, *p, state, u,
+                       u_stride, status, zero_on_fail, u_applied);
+    return launched("plant_kernel");
+}
+
+int tt_warm_start_device(int B, int N, const double* last, const int* have, const double* xref, const double* uref,
+                         int bug_compatible, double* z_guess, void* stream) {
+    if (B < 0 || N < 1 || !last || !have || !xref || !uref || !z_guess) return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(warm_kernel, dim3(grid_for((long long)B * (8 * N + 6))), dim3(kThreads), 0,
+                       (hipStream_t)stream, B, N, last, have, xref, uref, bug_compatible, z_guess);
+    return launched("warm_kernel");
+}
+
+int tt_record_solution_device(int B, int N, const double* x_out, const double* u_out, const int* status, double* last,
+                              int* have, void* stream) {
+    if (B < 0 || N < 1 || !x_out || !u_out || !status || !last || !have) return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(record_kernel, dim3(grid_for((long long)B * (8 * N + 6))), dim3(kThreads), 0,
+                       (hipStream_t)stream, B, N, x_out, u_out, status, last, have);
+    return launched("record_kernel");
+}
+
+int tt_interpolate_device(int B, int Np, int factor, const double* state_traj, const double* input_traj,
+                          double* state_out, double* input_out, void* stream) {
+    if (B < 0 || Np < 1 || factor < 1 || !state_traj || !input_traj || !state_out || !input_out) return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(interp_kernel, dim3(grid_for((long long)B * (factor * Np + 1))), dim3(kThreads), 0,
+                       (hipStream_t)stream, B, Np, factor, state_traj, input_traj, state_out, input_out);
+    return launched("interp_kernel");
+}
+
+}  // extern "C"

@@ -167,6 +167,9 @@ __device__ __forceinline__ bool armijo(double trial, double ref, double alpha, d
     return trial - (ref + 1e-4 * alpha * D) <= 10.0 * 2.220446049250313e-16 * fabs(ref);
 }
 
+// IPOPT filter constants (gamma_theta, gamma_phi, s_phi, s_theta; delta = 1, eta_phi = 1e-4)
+constexpr double kGTh = 1e-5, kGPh = 1e-8, kSPh = 2.3, kSTh = 1.1;
+
 // fraction-to-boundary: largest a with s + a*d >= (1-tau) s  (divide only when the bound is active)
 __device__ __forceinline__ void ftb(double s, double d, double tau, double& a) {
     if (d < 0.0 && tau * s < -a * d) a = -tau * s / d;
@@ -178,7 +181,7 @@ struct Ctx {
     double* sm;
     int N, lane;
     double dt, iL1, iL2, Mh;
-    double mu, tau, nu;
+    double mu, tau;
     __device__ __forceinline__ double& r(int row, int k) const { return sm[HEAD + k * SR + row]; }
     __device__ __forceinline__ double& h(int i) const { return sm[i]; }
     __device__ __forceinline__ bool hl(int v) const {
@@ -391,6 +394,7 @@ __device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
 // transposed into the PA tile, so both are contiguous b128 reads).  The 16x16 f64 MFMA was measured
 // at ~185 cycles per srcC-chained link on gfx950 and runs no faster than the VALU for f64, so the
 // whole recursion stays on the VALU with ~300 cycles of dependent latency per stage.
+constexpr int hFTH = 256, hFPH = 256 + kTrackFilter;  // filter entries (theta, phi)
 constexpr int hPF = 128, hPT = 192;  // P tile [8i + j] and transposed PA tile [8j + i] (64 doubles each)
 
 // branch-free predicated LDS store: invalid lanes write their own dump slot
@@ -679,11 +683,15 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
     return r;
 }
 
-// ============ merit value at z + alpha*dz (rows dzr): F - mu*sum(log s) + nu*||c||_1 ============
+// ============ filter trial at z + alpha*dz (rows dzr): phi_mu = F - mu*sum(log s) and theta = ||c||_1 ============
+struct Trial {
+    double phi, th;
+};
+
 template <int BM>
-__device__ __forceinline__ double phase_merit(const Ctx<BM>& c, double alpha, int dzr, bool storeC) {
+__device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int dzr, bool storeC) {
     const int N = c.N;
-    double val = 0.0;
+    double val = 0.0, thl = 0.0;
     bool bad = false;
     for (int k = c.lane; k <= N; k += W) {
         double x[6], u[2] = {0.0, 0.0};
@@ -734,11 +742,32 @@ __device__ __forceinline__ double phase_merit(const Ctx<BM>& c, double alpha, in
                 if (storeC) c.r(rCT + i, k + 1) = cc;
             }
         }
-        val += cost - c.mu * ls.value() + c.nu * th;
+        val += cost - c.mu * ls.value();
+        thl += th;
     }
-    const double v = wsum(bad ? INFINITY : val);  // one reduction; any bad lane -> +inf
+    Trial t;
+    t.phi = wsum(bad ? INFINITY : val);  // any lane outside the relaxed box -> +inf
+    t.th = wsum(thl);
     __syncthreads();
-    return v;
+    return t;
+}
+
+// filter acceptance of a trial (theta, phi): not dominated by the filter (entries in LDS) and either
+// f-type Armijo (theta0 <= theta_min and the switching condition) or sufficient theta / phi decrease,
+// each compared with IPOPT's round-off allowance.  Wave-uniform.
+template <int BM>
+__device__ __forceinline__ bool filter_ok(const Ctx<BM>& c, int nf, const Trial& t, double th0, double phi0, double D,
+                                          double alpha, double th_max, double th_min, bool& ftype) {
+    if (!isfinite(t.phi) || t.th > th_max) return false;
+    for (int f = 0; f < nf; ++f)
+        if (t.th >= c.sm[hFTH + f] && t.phi >= c.sm[hFPH + f]) return false;
+    const bool sw = D < 0.0 && alpha * pow(-D, kSPh) > pow(th0, kSTh);
+    if (th0 <= th_min && sw) {
+        ftype = true;
+        return armijo(t.phi, phi0, alpha, D);
+    }
+    ftype = false;
+    return t.th <= (1.0 - kGTh) * th0 || t.phi - (phi0 - kGPh * th0) <= 10.0 * 2.220446049250313e-16 * fabs(phi0);
 }
 
 // ============ accept the step (stage-parallel) ============
@@ -886,7 +915,6 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
     c.Mh = a.Mh;
     c.mu = 0.1;
     c.tau = fmax(0.99, 1.0 - c.mu);
-    c.nu = 1.0;
 #ifdef TT_STAMPS
     Stamps stamps;
     stamps.begin();
@@ -911,8 +939,8 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
     if (!infeas) {
         phase_init(c);
         STAMP(PH_LOAD);
-        double dw_last = 0.0;
-        int acc_count = 0;
+        double dw_last = 0.0, th_max = 0.0, th_min = 0.0;
+        int acc_count = 0, nf = 0;
         for (iter = 0;; ++iter) {
             const Lin e = phase_linearize(c);
             STAMP(PH_LIN);
@@ -934,6 +962,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
                 if (!(Emu <= 10.0 * c.mu && c.mu > a.tol / 10.0 * 1.0000001)) break;
                 c.mu = fmax(a.tol / 10.0, fmin(0.2 * c.mu, c.mu * sqrt(c.mu)));
                 c.tau = fmax(0.99, 1.0 - c.mu);
+                nf = 0;  // IPOPT resets the filter on every barrier update
                 cmu = phase_compl_mu(c);
             }
             STAMP(PH_MU_BAR);
@@ -954,26 +983,32 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             STAMP(PH_FWD);
             const StepInfo si = phase_step(c, rDX, true);
             STAMP(PH_STEP);
-            if (c.nu < si.ymax + 1.0) c.nu = fmax(1.1 * si.ymax + 1.0, c.nu);
-            // l1-merit backtracking line search with one second-order correction; the merit value of
-            // the current point comes from the linearisation pass
-            const double phi0 = e.cost - c.mu * e.logs + c.nu * e.th;
-            const double D = si.Dg - c.nu * e.th;
+            // IPOPT filter line search (Waechter & Biegler 2006, IPOPT defaults) with one second-order
+            // correction; theta / phi_mu of the current point come from the linearisation pass
+            const double th0 = e.th, phi0 = e.cost - c.mu * e.logs, D = si.Dg;
+            if (iter == 0) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
+            double amin = kGTh;
+            if (D < 0.0) {
+                amin = fmin(kGTh, kGPh * th0 / (-D));
+                if (th0 <= th_min) amin = fmin(amin, pow(th0, kSTh) / pow(-D, kSPh));
+            }
+            amin *= 0.05;
             double alpha = si.ap, az = si.az;
             int accepted = si.rel < 1e-15 ? 1 : 0;
-            bool soc = false;
-            for (int ls = 0; ls < 40 && !accepted; ++ls) {
-                const double phit = phase_merit(c, alpha, rDX, ls == 0);
+            const bool tiny = accepted;
+            bool soc = false, ftype = false;
+            for (int ls = 0; !accepted; ++ls) {
+                const Trial t = phase_trial(c, alpha, rDX, ls == 0);
                 STAMP(PH_MERIT);
-                if (armijo(phit, phi0, alpha, D)) { accepted = 1; break; }
-                if (ls == 0 && isfinite(phit)) {
+                if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, ftype)) { accepted = 1; break; }
+                if (ls == 0 && isfinite(t.phi) && t.th >= th0) {
                     phase_soc_rhs(c, alpha);
                     phase_soc_backward(c);
                     phase_forward(c, rCT, rWC, rDXS);
                     const double as = phase_soc_alpha(c);
-                    const double phis = phase_merit(c, as, rDXS, false);
+                    const Trial ts = phase_trial(c, as, rDXS, false);
                     STAMP(PH_SOC);
-                    if (armijo(phis, phi0, alpha, D)) {
+                    if (filter_ok(c, nf, ts, th0, phi0, D, alpha, th_max, th_min, ftype)) {
                         accepted = 2;
                         soc = true;
                         alpha = as;
@@ -981,9 +1016,19 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
                         break;
                     }
                 }
+                if (alpha * 0.5 < amin) break;
                 alpha *= 0.5;
             }
-            if (!accepted) alpha *= 2.0;
+            if (!accepted) {
+                nf = 0;  // IPOPT would enter its restoration phase: take the last trial step, reset the filter
+            } else if (!tiny && !ftype && nf < kTrackFilter) {
+                if (c.lane == 0) {
+                    c.sm[hFTH + nf] = (1.0 - kGTh) * th0;
+                    c.sm[hFPH + nf] = phi0 - kGPh * th0;
+                }
+                ++nf;
+                __syncthreads();
+            }
             phase_update(c, soc ? rDXS : rDX, alpha, az);
             STAMP(PH_UPDATE);
         }

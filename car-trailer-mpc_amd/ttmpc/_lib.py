@@ -29,6 +29,14 @@ class TTConfig(C.Structure):
                 ("warm_shift_compat", C.c_int), ("dual_init", C.c_int)]
 
 
+class TTPlant(C.Structure):
+    """tt_plant (include/ttmpc.h): params + DISTURBANCE_PARAMS of simulation.py:26-32, 391-397."""
+    _fields_ = [("dt", C.c_double), ("L1", C.c_double), ("L2", C.c_double), ("Mh", C.c_double),
+                ("W1", C.c_double), ("W2", C.c_double), ("enable", C.c_int), ("friction_coeff", C.c_double),
+                ("slippage_coeff", C.c_double), ("process_noise_std", C.c_double),
+                ("lateral_slip_gain", C.c_double), ("slip_angle_max", C.c_double)]
+
+
 class TTError(RuntimeError):
     pass
 
@@ -90,13 +98,26 @@ def lib():
     L.tt_max_horizon.restype = C.c_int
     L.tt_version.argtypes = []
     L.tt_version.restype = C.c_char_p
+    vp, i, ll = C.c_void_p, C.c_int, C.c_longlong
+    sim = {"tt_sim_window_device": [i, i, i, i, vp, vp, i, vp, vp, vp, vp, vp, vp],
+           "tt_collision_device": [i, i, vp, ll, i, vp, i, C.POINTER(TTPlant), vp, vp],
+           "tt_plant_update_device": [i, C.POINTER(TTPlant), vp, vp, ll, vp, i, vp, vp],
+           "tt_warm_start_device": [i, i, vp, vp, vp, vp, i, vp, vp],
+           "tt_record_solution_device": [i, i, vp, vp, vp, vp, vp, vp],
+           "tt_interpolate_device": [i, i, i, vp, vp, vp, vp, vp]}
+    for name, args in sim.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
     _lib = L
     return L
 
 
 EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_plan_batch", "tt_obca_solve_batch",
                     "tt_obca_solve_batch_device", "tt_obca_n", "tt_obca_workspace_bytes", "tt_destroy",
-                    "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version")
+                    "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version", "tt_sim_window_device",
+                    "tt_collision_device", "tt_plant_update_device", "tt_warm_start_device",
+                    "tt_record_solution_device", "tt_interpolate_device")
 
 
 def _ptr(a):

@@ -107,6 +107,54 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
 long long tt_obca_n(int N, int M);
 long long tt_obca_workspace_bytes(int N, int M);
 
+/* ---------------------------------------------------------------------------------------------
+ * Closed-loop simulation step, device pointers, asynchronous on `stream`.
+ * The per-timestep glue of python-files/simulation.py:484-531 around the solve, batched over B
+ * Monte-Carlo instances so that the whole loop stays in HBM:
+ *   window -> [collision check] -> [warm start] -> tt_solve_batch_device -> [record] -> plant update.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    double dt, L1, L2, Mh, W1, W2;     /* params dict (simulation.py:391-397)                         */
+    int enable;                        /* ENABLE_DISTURBANCES (simulation.py:21): 0 = update(q, u, p) */
+    double friction_coeff;             /* DISTURBANCE_PARAMS (simulation.py:26-32)                    */
+    double slippage_coeff;
+    double process_noise_std;          /* std of the measurement noise the caller draws (509-513)     */
+    double lateral_slip_gain;
+    double slip_angle_max;
+} tt_plant;
+
+/* Reference window at step k with end padding (simulation.py:486-501) from a plan of Np inputs
+ * (plan_x [P][Np+1][6], plan_u [P][Np][2]; P = 1 shared plan or B per-instance plans), and the
+ * measured state x_meas = state + meas_noise (simulation.py:509-513; meas_noise NULL = exact state;
+ * x_meas NULL = skip).  Outputs xref [B][N+1][6], uref [B][N][2]. */
+int tt_sim_window_device(int B, int N, int k, int Np, const double* plan_x, const double* plan_u, int per_instance,
+                         const double* state, const double* meas_noise, double* x_meas, double* xref, double* uref,
+                         void* stream);
+/* check_trajectory_collision (simulation.py:363-385) of K poses per instance, pose (b, j) at
+ * poses + b*stride_b + j*stride_k (doubles; x, y, theta, psi first), against M axis-aligned obstacles
+ * (device [M][4]: cx, cy, w, h).  flag[b] = 1 if any pose's truck or trailer touches an obstacle. */
+int tt_collision_device(int B, int K, const double* poses, long long stride_b, int stride_k, const double* obstacles,
+                        int M, const tt_plant* p, int* flag, void* stream);
+/* update(q, u, params[, DISTURBANCE_PARAMS]) (simulation.py:167-199) in place on state [B][6] with
+ * u = u[b*u_stride + 0..1] (u_out of a solve: u_stride = 2N applies inputs[:, 0]).  zero_on_fail:
+ * instances with status > TT_ACCEPTABLE apply zero control (simulation_nmpc.py:204-214).
+ * u_applied [B][2] (may be NULL) receives the control before friction/slippage scaling. */
+int tt_plant_update_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
+                           const int* status, int zero_on_fail, double* u_applied, void* stream);
+/* NMPC / fuzzy warm start (mpc_control_nmpc.py:90-100): z_guess [B][8N+6] = shift(last) where have[b],
+ * else the reference-copy guess from xref / uref.  bug_compatible = the reference's last-stage slicing
+ * (mpc_control_nmpc.py:83-84). */
+int tt_warm_start_device(int B, int N, const double* last, const int* have, const double* xref, const double* uref,
+                         int bug_compatible, double* z_guess, void* stream);
+/* After a solve: last[b] = pack(x_out[b], u_out[b]) and have[b] = 1 where status <= TT_ACCEPTABLE
+ * (the reference keeps _last_solution only on success, mpc_control_nmpc.py:107-111). */
+int tt_record_solution_device(int B, int N, const double* x_out, const double* u_out, const int* status, double* last,
+                              int* have, void* stream);
+/* do_interpolation (simulation.py:201-218) of B plans: state_traj [B][Np+1][6], input_traj [B][Np][2]
+ * -> [B][factor*Np+1][6], [B][factor*Np][2]; factor = floor(dt_1 / dt_2) (OBCA dt 0.1 -> MPC 0.05: 2). */
+int tt_interpolate_device(int B, int Np, int factor, const double* state_traj, const double* input_traj,
+                          double* state_out, double* input_out, void* stream);
+
 void tt_destroy(void* handle);
 const char* tt_last_error(void* handle);
 

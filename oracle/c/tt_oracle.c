@@ -23,6 +23,8 @@
 #include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
+
+#define TTO_MAX_FILTER 16 /* = kTrackFilter of the GPU kernel */
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -303,15 +305,16 @@ static void ws_free(ws_t* w) {
 }
 
 /* merit = F - mu*sum(log s) + nu*||c||_1 ; returns +inf if outside the bounds */
-static double merit_at(const tto_problem* P, ws_t* w, const double* z, const double* xinit, const double* xref,
-                       const double* uref, double mu, double nu, double* th_out) {
+/* filter trial point: returns the barrier objective phi_mu(z) (+inf outside the relaxed box) and
+ * theta(z) = ||c(z)||_1 in *th_out; c(z) is left in w->ct for the second-order correction */
+static double trial_at(const tto_problem* P, ws_t* w, const double* z, const double* xinit, const double* xref,
+                       const double* uref, double mu, double* th_out) {
     int bad = 0;
     double b = barrier(w, z, mu, &bad);
-    if (bad) return INFINITY;
     eval_cons(P, w, z, xinit, w->ct);
-    double th = norm1(w->ct, w->m);
-    if (th_out) *th_out = th;
-    return eval_cost(w, z, xref, uref) + b + nu * th;
+    *th_out = norm1(w->ct, w->m);
+    if (bad) return INFINITY;
+    return eval_cost(w, z, xref, uref) + b;
 }
 
 static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const double* xref, const double* uref,
@@ -379,7 +382,9 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
         w->zU[v] = w->hasU[v] ? 1.0 : 0.0;
     }
     memset(w->y, 0, (size_t)m * 8);
-    double mu = 0.1, tau = fmax(0.99, 1.0 - mu), nu = 1.0, dw_last = 0.0;
+    double mu = 0.1, tau = fmax(0.99, 1.0 - mu), nu = 1.0, dw_last = 0.0, th_max = 0.0, th_min = 0.0;
+    double fth[TTO_MAX_FILTER], fph[TTO_MAX_FILTER];
+    int nf = 0;
     int acc_count = 0, nb = 0;
     for (int v = 0; v < n; ++v) nb += w->hasL[v] + w->hasU[v];
 
@@ -432,6 +437,7 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
             if (Emu <= kappa_eps * mu && mu > tol / 10.0 * 1.0000001) {
                 mu = fmax(tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
                 tau = fmax(0.99, 1.0 - mu);
+                nf = 0; /* IPOPT resets the filter on every barrier update */
                 cmu = 0.0;
                 for (int v = 0; v < n; ++v) {
                     if (w->hasL[v]) cmu = fmax(cmu, fabs(w->zL[v] * (w->z[v] - w->lb[v]) - mu));
@@ -493,31 +499,54 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
                 if (w->dzU[v] < 0) az = fmin(az, -tau * w->zU[v] / w->dzU[v]);
             }
         }
-        /* ---- l1-merit backtracking line search (+1 second-order correction) ---- */
+        /* ---- filter line search (Waechter & Biegler 2006; IPOPT defaults) + one second-order correction ---- */
         double ymax = 0.0;
         for (int j = 0; j < m; ++j) ymax = fmax(ymax, fabs(w->yp[j]));
-        if (nu < ymax + 1.0) nu = fmax(1.1 * ymax + 1.0, nu);
+        if (nu < ymax + 1.0) nu = fmax(1.1 * ymax + 1.0, nu); /* diagnostics only (printed) */
         int bad = 0;
-        double th0 = norm1(w->c, m);
-        double phi0 = eval_cost(w, w->z, xref, uref) + barrier(w, w->z, mu, &bad) + nu * th0;
-        double D = -nu * th0;
+        const double th0 = norm1(w->c, m);
+        const double phi0 = eval_cost(w, w->z, xref, uref) + barrier(w, w->z, mu, &bad);
+        double D = 0.0;
         for (int v = 0; v < n; ++v) {
             double g = w->gF[v];
             if (w->hasL[v]) g -= mu / (w->z[v] - w->lb[v]);
             if (w->hasU[v]) g += mu / (w->ub[v] - w->z[v]);
             D += g * w->dz[v];
         }
+        if (iter == 0) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
+        const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, g_al = 0.05;
+        double amin = g_th;
+        if (D < 0.0) {
+            amin = fmin(g_th, g_ph * th0 / (-D));
+            if (th0 <= th_min) amin = fmin(amin, delta * pow(th0, s_th) / pow(-D, s_ph));
+        }
+        amin *= g_al;
+        const double tolc = 10.0 * DBL_EPSILON;
         double alpha = ap;
-        int accepted = 0;
+        int accepted = 0, ftype = 0;
         /* tiny step -> accept */
         double rel = 0.0;
         for (int v = 0; v < n; ++v) rel = fmax(rel, fabs(w->dz[v]) / (1.0 + fabs(w->z[v])));
         if (rel < 1e-15) accepted = 1;
-        for (int ls = 0; ls < 40 && !accepted; ++ls) {
+#define FILTER_OK(tht_, pht_, a_, ok_) do { \
+            ok_ = 0; \
+            if (isfinite(pht_) && (tht_) <= th_max) { \
+                int blocked = 0; \
+                for (int f_ = 0; f_ < nf; ++f_) if ((tht_) >= fth[f_] && (pht_) >= fph[f_]) { blocked = 1; break; } \
+                if (!blocked) { \
+                    const int sw_ = D < 0.0 && (a_) * pow(-D, s_ph) > delta * pow(th0, s_th); \
+                    if (th0 <= th_min && sw_) { ftype = 1; ok_ = (pht_) - (phi0 + eta * (a_) * D) <= tolc * fabs(phi0); } \
+                    else { ftype = 0; ok_ = (tht_) <= (1.0 - g_th) * th0 || (pht_) - (phi0 - g_ph * th0) <= tolc * fabs(phi0); } \
+                } \
+            } } while (0)
+        for (int ls = 0; !accepted; ++ls) {
             for (int v = 0; v < n; ++v) w->zt[v] = w->z[v] + alpha * w->dz[v];
-            double phit = merit_at(P, w, w->zt, xinit, xref, uref, mu, nu, NULL);
-            if (phit - (phi0 + eta * alpha * D) <= 10.0 * DBL_EPSILON * fabs(phi0)) { accepted = 1; break; } /* IPOPT Compare_le */
-            if (ls == 0 && isfinite(phit)) {
+            double tht = 0.0;
+            const double pht = trial_at(P, w, w->zt, xinit, xref, uref, mu, &tht);
+            int ok;
+            FILTER_OK(tht, pht, alpha, ok);
+            if (ok) { accepted = 1; break; }
+            if (ls == 0 && isfinite(pht) && tht >= th0) {
                 /* second-order correction: c_soc = alpha c(z) + c(z + alpha dz) */
                 for (int k = 0; k <= N; ++k) {
                     for (int i = 0; i < (k < N ? 8 : 6); ++i) {
@@ -538,8 +567,11 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
                     if (w->hasU[v] && w->dzs[v] > 0) as = fmin(as, tau * (w->ub[v] - w->z[v]) / w->dzs[v]);
                 }
                 for (int v = 0; v < n; ++v) w->zt[v] = w->z[v] + as * w->dzs[v];
-                double phis = merit_at(P, w, w->zt, xinit, xref, uref, mu, nu, NULL);
-                if (phis - (phi0 + eta * alpha * D) <= 10.0 * DBL_EPSILON * fabs(phi0)) {
+                double ths = 0.0;
+                const double phs = trial_at(P, w, w->zt, xinit, xref, uref, mu, &ths);
+                int ok2;
+                FILTER_OK(ths, phs, alpha, ok2);
+                if (ok2) {
                     accepted = 2;
                     alpha = as;
                     for (int j = 0; j < m; ++j) w->yp[j] = w->rhs2[ky(j / 6) + j % 6];
@@ -556,9 +588,19 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
                     break;
                 }
             }
+            if (alpha * 0.5 < amin) break;
             alpha *= 0.5;
         }
-        if (!accepted) alpha *= 2.0; /* last tried */
+#undef FILTER_OK
+        if (!accepted) {
+            nf = 0; /* IPOPT would enter its restoration phase; take the last trial step and reset the filter */
+        } else if (accepted == 1 && rel < 1e-15) {
+            /* negligible step: nothing to add */
+        } else if (!ftype && nf < TTO_MAX_FILTER) {
+            fth[nf] = (1.0 - g_th) * th0;
+            fph[nf] = phi0 - g_ph * th0;
+            ++nf;
+        }
         if (getenv("TTO_DEBUG")) fprintf(stderr, "   ap %.3e az %.3e alpha %.3e acc %d D %.3e\n", ap, az, alpha, accepted, D);
         /* ---- update ---- */
         for (int v = 0; v < n; ++v) w->z[v] += alpha * w->dz[v];

@@ -388,3 +388,67 @@ def reference_window(ref_states, ref_inputs, k, horizon):
         Xr[:, :] = ref_states[:, -1:]
         Ur[:, :] = 0.0
     return Xr, Ur
+
+
+# ----------------------------------------------------------------------------------------------
+# closed-loop simulation pieces
+# ----------------------------------------------------------------------------------------------
+# simulation.py:26-32
+DISTURBANCE_PARAMS = {"friction_coeff": 0.9, "slippage_coeff": 0.9, "process_noise_std": 0.02,
+                      "lateral_slip_gain": 0.01, "slip_angle_max": 0.0}
+
+
+def plant_update(q, u, p, dist=None):
+    """update(q, u, params, disturbance_params) of simulation.py:167-199, vectorised over leading axes:
+    apply_disturbances (50-87: u scaled by friction / slippage; its noise draw is discarded),
+    f_dyn (34-48), apply_slippage_to_dynamics (89-115), Euler step, apply_lateral_slip (117-149)."""
+    q = np.asarray(q, dtype=np.float64)
+    u = np.array(u, dtype=np.float64)
+    if dist is not None:
+        u[..., 0] = u[..., 0] * dist.get("friction_coeff", 1.0)
+        u[..., 1] = u[..., 1] * dist.get("slippage_coeff", 1.0)
+    qd = f(q, u, p)
+    if dist is not None and "slip_angle_max" in dist:
+        slip = 1.0 - np.minimum(np.abs(q[..., 4]) * np.abs(q[..., 5]) * dist["slip_angle_max"], 0.3)
+        qd[..., 2] = qd[..., 2] * slip
+        qd[..., 3] = qd[..., 3] * slip
+    nq = q + qd * p["dt"]
+    if dist is not None and "lateral_slip_gain" in dist:
+        mag = dist["lateral_slip_gain"] * np.abs(q[..., 5]) * np.abs(q[..., 4])
+        nq[..., 0] = nq[..., 0] + mag * np.cos(q[..., 2] + np.pi / 2) * p["dt"]
+        nq[..., 1] = nq[..., 1] + mag * np.sin(q[..., 2] + np.pi / 2) * p["dt"]
+    return nq
+
+
+def step_indices(T_sim, dt):
+    """simulation.py:484-531 loop counter: t = 0; while t <= T_sim: k = floor(t/dt); ...; t += dt."""
+    ks, t = [], 0.0
+    while t <= T_sim:
+        ks.append(math.floor(t / dt))
+        t += dt
+    return ks
+
+
+def closed_loop(solve, x_init, plan_x, plan_u, horizon, T_sim, p, dist=None, noise=None, zero_on_fail=False):
+    """The reference loop for B instances sharing one plan (plan_x (6,Np+1), plan_u (2,Np)).
+    solve(x_meas (B,6), Xr (B,N+1,6), Ur (B,N,2)) -> (X (B,N+1,6), U (B,N,2), status (B,)).
+    noise: (steps, B, 6) measurement noise (simulation.py:509-513) or None.
+    Returns states (steps+1,B,6), applied controls (steps,B,2), status (steps,B)."""
+    x = np.array(x_init, dtype=np.float64).reshape(-1, 6)
+    B = x.shape[0]
+    ks = step_indices(T_sim, p["dt"])
+    S, Ua, St = [x.copy()], [], []
+    for j, k in enumerate(ks):
+        Xr, Ur = reference_window(plan_x, plan_u, k, horizon)
+        Xr = np.broadcast_to(Xr.T, (B, horizon + 1, NX)).copy()
+        Ur = np.broadcast_to(Ur.T, (B, horizon, NU)).copy()
+        xm = x + noise[j] if noise is not None else x
+        _, U, st = solve(xm, Xr, Ur)
+        u0 = U[:, 0].copy()
+        if zero_on_fail:
+            u0[st > 1] = 0.0
+        x = plant_update(x, u0, p, dist)
+        S.append(x.copy())
+        Ua.append(u0)
+        St.append(np.asarray(st).copy())
+    return np.array(S), np.array(Ua), np.array(St)
