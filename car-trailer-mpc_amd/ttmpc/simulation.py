@@ -94,7 +94,10 @@ def collision_flags(poses, obstacles, params, flag=None, stream=None):
     flag = torch.empty(B, dtype=torch.int32, device=dev) if flag is None else flag
     p = plant(params)
     M = 0 if obstacles is None else int(obstacles.shape[0])
-    _check(lib().tt_collision_device(B, K, poses.data_ptr(), poses.stride(0), poses.stride(1),
+    if poses.stride(-1) != 1:
+        raise ValueError("pose rows must be contiguous")
+    sk = poses.stride(1) if K > 1 else w          # a size-1 dim may carry any stride (numpy gives 0)
+    _check(lib().tt_collision_device(B, K, poses.data_ptr(), poses.stride(0), sk,
                                      None if M == 0 else obstacles.data_ptr(), M, C.byref(p), flag.data_ptr(),
                                      _stream(stream, dev)), "tt_collision_device")
     return flag
