@@ -121,7 +121,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "c4", "cobs"],
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "c4", "cobs", "sim"],
                     help="c2/c3/c5: tracking NMPC; c4: OBCA plans (trajectory_optimization.py); "
                          "cobs: MPC+OBCA (mpc_control_obs.py)")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default by config)")
@@ -137,6 +137,8 @@ def main():
         return main_obca(args)
     if args.config == "c5":
         return main_c5(args)
+    if args.config == "sim":
+        return main_sim(args)
 
     defaults = {"c2": (1024, 20), "c3": (8192, 40)}
     B = args.batch or defaults[args.config][0]
@@ -349,6 +351,135 @@ def main_c5(args):
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def main_sim(args):
+    """Closed-loop Monte-Carlo: simulation.py's loop (N=50, dt=0.05, disturbances on,
+    noisy measurements, collision check vs obstacles.json) for B instances started around the plan's start,
+    tracking the reference's committed OBCA plan interpolated to 0.05 s.  A step = one closed-loop step of
+    every instance: window -> collision check -> solve -> plant update, all on the device."""
+    import numpy as np
+
+    import ttmpc
+    from oracle import ttmpc_oracle as to  # constants only
+    from ttmpc import simulation as sim
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="gloo")
+    B, N = args.batch or 1024, args.horizon or 50
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    g = np.load(REPO / "tests" / "golden" / "reference_numpy.npz")
+    S, U = g["interp_states"], g["interp_inputs"]
+    params = dict(to.DEFAULT_PARAMS, horizon=N)
+    rng = np.random.default_rng(rank_seed(rank))
+    x0 = S[:, 0][None] + rng.normal(scale=[0.3, 0.3, 0.02, 0.02, 0.0, 0.0], size=(B, 6))
+    solver = ttmpc.BatchSolver(N, params, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB, to.MPC_UUB,
+                               device=local)
+    cl = sim.ClosedLoop(solver, S, U, params, sim.DISTURBANCE_PARAMS, obstacles=g["obstacles"], seed=rank_seed(rank))
+    cl.reset(x0)
+    dt = 0.05   # the reference's clock: t accumulated with +=, k = floor(t / dt) (simulation.py:484-531)
+    t_sim, k_list = 0.0, []
+    while len(k_list) < args.warmup + args.steps:
+        k_list.append(int(np.floor(t_sim / dt)))
+        t_sim += dt
+    for k in k_list[: args.warmup]:
+        cl.step(k)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(cl.stream)
+    for k in k_list[args.warmup:]:
+        cl.step(k)
+    e1.record(cl.stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    st = cl.st.cpu().numpy()
+    ok = int(np.sum(st <= 1))
+    wall_max, ok_total, B_total = reduce_over_ranks(dist, wall, ok, B)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    # one more solve alone: the track_kernel share of a closed-loop step
+    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    k0.record(cl.stream)
+    solver.solve_device(B, cl.x_meas.data_ptr(), cl.xref.data_ptr(), cl.uref.data_ptr(), cl.X.data_ptr(),
+                        cl.U.data_ptr(), cl.st.data_ptr(), cl.it.data_ptr(), cl.kkt.data_ptr(),
+                        stream=cl.stream.cuda_stream)
+    k1.record(cl.stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = k0.elapsed_time(k1)
+    iters = cl.it.cpu().numpy()
+    F = float(np.sum(flops_per_solve(N, iters.astype(np.float64))))
+    out = {
+        "metric": f"closed-loop MPC steps/sec (simulation.py loop, N={N}, disturbed plant)",
+        "value": round(B_total * args.steps / wall_max, 1),
+        "unit": "instance-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "the reference's committed OBCA plan (data/state_traj.txt, do_interpolation 0.1 -> 0.05) with "
+                "B perturbed starts, DISTURBANCE_PARAMS of simulation.py, device-drawn measurement noise",
+        "config": {"workload": f"sim: B={B} closed loops/GPU, N={N}, steps {args.warmup}+{args.steps} of the "
+                               "simulation.py loop (window, SAT collision check, solve, disturbed plant update)",
+                   "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world} (independent instances)"},
+        "solver": {"converged_or_acceptable_last_step": ok_total, "instances": B_total,
+                   "status_counts_last_step": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+                   "iters_mean_last_step": float(iters.mean()), "step_ms_hip_events": round(
+                       e0.elapsed_time(e1) / args.steps, 4), "kernel_ms_per_solve": round(kernel_ms, 4)},
+        "roofline": {"bound": "mfma", "achieved": round(F / (kernel_ms * 1e-3) / 1e12, 4), "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(F / (kernel_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 6),
+                     "traffic": None, "note": "track_kernel of one closed-loop step; SURVEY §8(d) flop formula"},
+    }
+    if args.cpu_budget > 0 and world == 1:
+        out["cpu_baseline"] = sim_cpu_baseline(S, U, g["obstacles"], x0, N, params, args.cpu_budget)
+    print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def sim_cpu_baseline(S, U, obstacles, x0, N, params, budget_s):
+    """The oracle's restatement of the simulation.py loop (C IPM per step, numpy plant), OpenMP over
+    instances, on a bounded sample."""
+    import numpy as np
+
+    from oracle import c_oracle as co
+    from oracle import ttmpc_oracle as to
+    from ttmpc import layout
+    ncores = len(os.sched_getaffinity(0))
+    threads = max(1, min(16, ncores))
+    nlp = to.TrackingNLP(N)
+    P = co.make_problem(N, params, nlp.Q, nlp.R, nlp.xlb, nlp.xub, nlp.ulb, nlp.uub)
+
+    def solve(x, Xr, Ur):
+        z, st, _, _ = co.solve_batch(P, x, Xr, Ur, nthreads=threads)
+        X, Uo = layout.unpack(z, N)
+        return X, Uo, st
+    Bs = min(len(x0), 16 * threads)
+    rng = np.random.default_rng(0)
+    done, t0, T = 0, time.perf_counter(), 0.5
+    while True:
+        K = len(to.step_indices(T, 0.05))
+        noise = rng.normal(scale=0.02, size=(K, Bs, 6))
+        to.closed_loop(solve, x0[:Bs], S, U, N, T, params, to.DISTURBANCE_PARAMS, noise)
+        done += K * Bs
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "instance-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} instance-steps ({Bs} instances x {T}s loops) in {el:.1f}s; oracle closed loop "
+                      f"(oracle/ttmpc_oracle.closed_loop + oracle/c/tt_oracle.c), OpenMP {threads} threads"}
 
 
 def obca_flops(N, M, iters):
