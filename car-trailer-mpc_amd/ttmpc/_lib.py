@@ -104,7 +104,8 @@ def lib():
            "tt_plant_update_device": [i, C.POINTER(TTPlant), vp, vp, ll, vp, i, vp, vp],
            "tt_warm_start_device": [i, i, vp, vp, vp, vp, i, vp, vp],
            "tt_record_solution_device": [i, i, vp, vp, vp, vp, vp, vp],
-           "tt_interpolate_device": [i, i, i, vp, vp, vp, vp, vp]}
+           "tt_interpolate_device": [i, i, i, vp, vp, vp, vp, vp],
+           "tt_lqr_score_device": [i, C.POINTER(TTPlant), _dp, _dp, vp, vp, vp, vp, vp, vp, vp]}
     for name, args in sim.items():
         fn = getattr(L, name)
         fn.argtypes = args
@@ -117,7 +118,7 @@ EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_
                     "tt_obca_solve_batch_device", "tt_obca_n", "tt_obca_workspace_bytes", "tt_destroy",
                     "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version", "tt_sim_window_device",
                     "tt_collision_device", "tt_plant_update_device", "tt_warm_start_device",
-                    "tt_record_solution_device", "tt_interpolate_device")
+                    "tt_record_solution_device", "tt_interpolate_device", "tt_lqr_score_device")
 
 
 def _ptr(a):

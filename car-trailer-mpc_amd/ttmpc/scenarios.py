@@ -95,7 +95,11 @@ def load_obstacles(path):
     """obstacles.json corner format -> [{'center': (cx, cy), 'width': w, 'height': h}] rounded to 4 dp
     (get_obstacles.py:5-32)."""
     with open(path) as fh:
-        data = json.load(fh)
+        return obstacles_from_corners(json.load(fh))
+
+
+def obstacles_from_corners(data):
+    """Corner-format list (obstacles.json) -> centre / width / height dicts (get_obstacles.py:5-32)."""
     out = []
     for ob in data:
         FL, FR, BL, BR = ob["FL"], ob["FR"], ob["BL"], ob["BR"]
@@ -332,3 +336,56 @@ def mpc_obs_batch(state_traj, input_traj, B: int, horizon: int, seed: int = 0, d
         x0[b] = np.clip(Xr[:, 0] + pert, np.where(np.isfinite(XLB), XLB + 1e-6, -np.inf),
                         np.where(np.isfinite(XUB), XUB - 1e-6, np.inf))
     return x0, xref, uref
+
+
+# ----------------------------------------------------------------------------------------------
+# scenario generators / writers of the reference
+# ----------------------------------------------------------------------------------------------
+STALL_WIDTH, STRIPE_WIDTH, WALL_WIDTH, N_STALLS = 5.0, 1.0, 30.0, 10
+
+
+def _rect(x0, x1, y0, y1):
+    """corner format of obstacles.json: FL/FR at the far edge y1, BL/BR at y0."""
+    return {"FL": {"X": x0, "Y": y1}, "FR": {"X": x1, "Y": y1}, "BL": {"X": x0, "Y": y0}, "BR": {"X": x1, "Y": y0}}
+
+
+def build_parking_obstacles(open_spot: int, depth: float = 20.0):
+    """One-sided parking row (make_parking_obstacles.py:6-51): two 30 m walls bounding 10 stalls of
+    5 m separated by 1 m stripes, every stall blocked except ``open_spot`` (1-based).  Returns the
+    obstacles.json corner-format list (walls first, then stalls in x order)."""
+    if not 1 <= open_spot <= N_STALLS:
+        raise ValueError("open_spot must be between 1 and 10 (inclusive)")
+    pitch = STALL_WIDTH + STRIPE_WIDTH
+    span_end = STRIPE_WIDTH + N_STALLS * pitch - STRIPE_WIDTH
+    out = [_rect(-WALL_WIDTH, 0.0, 0.0, depth), _rect(span_end, span_end + WALL_WIDTH, 0.0, depth)]
+    for i in range(N_STALLS):
+        if i + 1 != open_spot:
+            x0 = STRIPE_WIDTH + i * pitch
+            out.append(_rect(x0, x0 + STALL_WIDTH, 0.0, depth))
+    return out
+
+
+def parking_goal(open_spot: int):
+    """Goal the reference writes for the open stall (make_parking_obstacles.py:83-87): stall centre x,
+    y = 12.45 (parked flush at the trailer length)."""
+    return STRIPE_WIDTH + (open_spot - 1) * (STALL_WIDTH + STRIPE_WIDTH) + STALL_WIDTH / 2.0, 12.45
+
+
+def initialize_doc(case: dict) -> dict:
+    """The 2-waypoint initialize.json of a test_cases.json case (apply_case.py:16-34)."""
+    s, g = case["start"], case["goal"]
+    return {"Positions": [[s["x"], s["y"]], [g["x"], g["y"]]],
+            "Headings": [s["heading_rad"], g["heading_rad"]],
+            "HitchAngles": [s["hitch_angle_rad"], g["hitch_angle_rad"]]}
+
+
+def write_initialize(case: dict, output_path) -> None:
+    """apply_case.write_initialize: json.dump(indent=2) of initialize_doc(case)."""
+    with open(output_path, "w") as fh:
+        json.dump(initialize_doc(case), fh, indent=2)
+
+
+def load_test_cases(path) -> dict:
+    """test_cases.json -> {name: case} (apply_case.py:10-13)."""
+    with open(path) as fh:
+        return {c["name"]: c for c in json.load(fh)["cases"]}

@@ -155,6 +155,14 @@ int tt_record_solution_device(int B, int N, const double* x_out, const double* u
 int tt_interpolate_device(int B, int Np, int factor, const double* state_traj, const double* input_traj,
                           double* state_out, double* input_out, void* stream);
 
+/* lqr_distance (LQR_cost.py:7-41) for B instances: A, B of the forward-Euler map at (x_goal, u_goal),
+ * P = DARE(A, B, Q, R) symmetrised, score[b] = (x_cur - x_goal)' P (x_cur - x_goal).  Q (6x6), R (2x2) are
+ * HOST row-major arrays; x_cur, x_goal [B][6], u_goal [B][2] (may be NULL: the map is linear in u) are device
+ * pointers.  P_out [B][36] and iters [B] (doublings used, -1 = not converged in 64) may be NULL. */
+int tt_lqr_score_device(int B, const tt_plant* p, const double* Q, const double* R, const double* x_cur,
+                        const double* x_goal, const double* u_goal, double* P_out, double* score, int* iters,
+                        void* stream);
+
 void tt_destroy(void* handle);
 const char* tt_last_error(void* handle);
 

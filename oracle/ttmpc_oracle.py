@@ -452,3 +452,20 @@ def closed_loop(solve, x_init, plan_x, plan_u, horizon, T_sim, p, dist=None, noi
         Ua.append(u0)
         St.append(np.asarray(st).copy())
     return np.array(S), np.array(Ua), np.array(St)
+
+
+def lqr_riccati(p, Q, R, x_goal):
+    """LQR_cost.py:7-34 with the reference's own DARE solver (scipy.linalg.solve_discrete_are); the
+    CasADi Jacobian of the Euler map is the analytic jac_f (sympy-verified)."""
+    from scipy.linalg import solve_discrete_are
+    A = np.eye(NX) + p["dt"] * jac_f(np.asarray(x_goal, dtype=np.float64), p)
+    B = p["dt"] * B_F
+    P = solve_discrete_are(A, B, np.asarray(Q, dtype=np.float64), np.asarray(R, dtype=np.float64))
+    return 0.5 * (P + P.T)
+
+
+def lqr_distance(x_current, x_goal, p, Q, R):
+    """LQR_cost.py:37-41."""
+    P = lqr_riccati(p, Q, R, x_goal)
+    dx = np.asarray(x_current, dtype=np.float64) - np.asarray(x_goal, dtype=np.float64)
+    return float(dx @ P @ dx)

@@ -229,3 +229,19 @@ def test_switch_mode_routes_colliding_instances_to_obca(plan, golden_ref):
     Xr, _ = to.reference_window(S, U, 0, N)
     assert bool(out["collide"][0, 0]) == collision.check_trajectory_collision(Xr, P, obs)
     assert np.isfinite(out["states"]).all()
+
+
+def test_obca_plans_feed_tracking_batch_on_device(golden_ref):
+    """§8(f) row 2: B device-resident OBCA-style plans -> do_interpolation on the GPU -> per-instance
+    ClosedLoop references, equal to the reference's host resampling of each plan."""
+    from oracle import ttmpc_oracle as to
+    from ttmpc import handoff
+    S, U = golden_ref["state_traj"], golden_ref["input_traj"]
+    B = 4
+    X = np.stack([S.T + 0.5 * b for b in range(B)])
+    Uu = np.stack([U.T * (1 + 0.1 * b) for b in range(B)])
+    Xr, Ur = handoff.plan_batch_to_references(_t(X), _t(Uu))
+    torch.cuda.synchronize()
+    for b in range(B):
+        S2, U2 = to.do_interpolation(X[b].T, Uu[b].T, 0.1, 0.05)
+        assert np.array_equal(Xr.cpu().numpy()[b], S2.T) and np.array_equal(Ur.cpu().numpy()[b], U2.T)
