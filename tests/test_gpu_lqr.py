@@ -1,7 +1,9 @@
 """GPU suite: batched LQR terminal score (csrc/tt_lqr.hip, doubling algorithm) against the reference's
 algorithm (LQR_cost.py: scipy.linalg.solve_discrete_are on the Euler linearisation at the goal).
-Tolerance: |P - P_scipy| <= 1e-8 |P_scipy|_max, score relative 1e-8 (FP64; both solvers are backward
-stable, the DARE condition at slow goals reaches ~1e7)."""
+Tolerance: the GPU P satisfies the DARE to a relative residual <= 1e-12, and agrees with scipy's P (and
+score) to max(1e-9, 1e6 x scipy's own relative residual): at near-stationary goals (|v| ~ 0.01, P ~ 1e7)
+the DARE is ill-conditioned and scipy's Schur solution carries residuals ~1e-11 while the doubling
+iteration reaches ~1e-14, so the two differ at the 1e-7 level there."""
 import numpy as np
 import pytest
 
@@ -24,11 +26,20 @@ def test_lqr_scores_match_scipy_dare(golden_ref):
     s, P, it = lqr.lqr_scores(xc, xg, P6, Q, R)
     s, P, it = s.cpu().numpy(), P.cpu().numpy(), it.cpu().numpy()
     assert np.all(it > 0)
+    def resid(Pm, x):
+        A = np.eye(6) + P6["dt"] * to.jac_f(x, P6)
+        Bm = P6["dt"] * to.B_F
+        K = np.linalg.solve(R + Bm.T @ Pm @ Bm, Bm.T @ Pm @ A)
+        return np.abs(A.T @ Pm @ A - Pm - A.T @ Pm @ Bm @ K + Q).max() / np.abs(Pm).max()
     for b in range(B):
         Pr = to.lqr_riccati(P6, Q, R, xg[b])
-        assert np.max(np.abs(P[b] - Pr)) <= 1e-8 * np.max(np.abs(Pr)), b
+        assert resid(P[b], xg[b]) <= 1e-12, b
+        rs = resid(Pr, xg[b])
+        assert resid(P[b], xg[b]) <= max(1e-13, rs), b          # at least as accurate as scipy
+        tol = max(1e-9, 1e6 * rs)                                 # forward error <= cond x residual
+        assert np.max(np.abs(P[b] - Pr)) <= tol * np.max(np.abs(Pr)), b
         sr = float((xc[b] - xg[b]) @ Pr @ (xc[b] - xg[b]))
-        assert abs(s[b] - sr) <= 1e-8 * abs(sr), b
+        assert abs(s[b] - sr) <= tol * abs(sr), b
 
 
 def test_lqr_reference_signatures():
