@@ -49,7 +49,10 @@ constexpr int SR = kRowsPerStage;
 constexpr int HEAD = kHead;
 
 // head
-constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54, hDUMP = 64;  // dump: one slot per lane
+constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54;
+// dump: sink of branch-free predicated stores, one slot per lane pair (l, l+32: different LDS halves)
+constexpr int hDUMP = 64, hFTH = 96, hFPH = 112;  // filter entries (theta, phi), kTrackFilter each
+static_assert(hFTH + kTrackFilter == hFPH && hFPH + kTrackFilter <= 128, "filter fits the head");
 // (128..255: the P and transposed-PA tiles of the Riccati sweep, see phase_riccati)
 // rows
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
@@ -394,13 +397,12 @@ __device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
 // transposed into the PA tile, so both are contiguous b128 reads).  The 16x16 f64 MFMA was measured
 // at ~185 cycles per srcC-chained link on gfx950 and runs no faster than the VALU for f64, so the
 // whole recursion stays on the VALU with ~300 cycles of dependent latency per stage.
-constexpr int hFTH = 256, hFPH = 256 + kTrackFilter;  // filter entries (theta, phi)
 constexpr int hPF = 128, hPT = 192;  // P tile [8i + j] and transposed PA tile [8j + i] (64 doubles each)
 
 // branch-free predicated LDS store: invalid lanes write their own dump slot
 template <int BM>
 __device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
-    c.sm[valid ? HEAD + k * SR + row : hDUMP + c.lane] = v;
+    c.sm[valid ? HEAD + k * SR + row : hDUMP + (c.lane & 31)] = v;
 }
 
 // stage-parallel: fold the barrier, curvature and constraint terms into the Riccati operand rows
@@ -752,17 +754,19 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
     return t;
 }
 
-// filter acceptance of a trial (theta, phi): not dominated by the filter (entries in LDS) and either
-// f-type Armijo (theta0 <= theta_min and the switching condition) or sufficient theta / phi decrease,
-// each compared with IPOPT's round-off allowance.  Wave-uniform.
+// filter acceptance of a trial (theta, phi): not dominated by the filter (entries in the LDS head; lane
+// f tests entry f, one ballot) and either f-type Armijo (theta0 <= theta_min and the switching
+// condition) or sufficient theta / phi decrease, each compared with IPOPT's round-off allowance.
+// Wave-uniform result.
 template <int BM>
 __device__ __forceinline__ bool filter_ok(const Ctx<BM>& c, int nf, const Trial& t, double th0, double phi0, double D,
-                                          double alpha, double th_max, double th_min, bool& ftype) {
+                                          double alpha, double th_max, double th_min, double pD, double pT,
+                                          bool& ftype) {
     if (!isfinite(t.phi) || t.th > th_max) return false;
-    for (int f = 0; f < nf; ++f)
-        if (t.th >= c.sm[hFTH + f] && t.phi >= c.sm[hFPH + f]) return false;
-    const bool sw = D < 0.0 && alpha * pow(-D, kSPh) > pow(th0, kSTh);
-    if (th0 <= th_min && sw) {
+    const int f = c.lane & (kTrackFilter - 1);
+    if (__ballot(c.lane < nf && t.th >= c.sm[hFTH + f] && t.phi >= c.sm[hFPH + f]) != 0ull) return false;
+    // switching condition alpha (-D)^s_phi > theta0^s_theta (pD, pT precomputed once per iteration)
+    if (th0 <= th_min && D < 0.0 && alpha * pD > pT) {
         ftype = true;
         return armijo(t.phi, phi0, alpha, D);
     }
@@ -987,10 +991,16 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             // correction; theta / phi_mu of the current point come from the linearisation pass
             const double th0 = e.th, phi0 = e.cost - c.mu * e.logs, D = si.Dg;
             if (iter == 0) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
+            // (-D)^s_phi and theta0^s_theta only matter when theta0 <= theta_min (switching condition, amin)
+            double pD = 0.0, pT = 0.0;
+            if (th0 <= th_min && D < 0.0) {
+                pD = pow(-D, kSPh);
+                pT = pow(th0, kSTh);
+            }
             double amin = kGTh;
             if (D < 0.0) {
                 amin = fmin(kGTh, kGPh * th0 / (-D));
-                if (th0 <= th_min) amin = fmin(amin, pow(th0, kSTh) / pow(-D, kSPh));
+                if (th0 <= th_min) amin = fmin(amin, pT / pD);
             }
             amin *= 0.05;
             double alpha = si.ap, az = si.az;
@@ -1000,7 +1010,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
             for (int ls = 0; !accepted; ++ls) {
                 const Trial t = phase_trial(c, alpha, rDX, ls == 0);
                 STAMP(PH_MERIT);
-                if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, ftype)) { accepted = 1; break; }
+                if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, pD, pT, ftype)) { accepted = 1; break; }
                 if (ls == 0 && isfinite(t.phi) && t.th >= th0) {
                     phase_soc_rhs(c, alpha);
                     phase_soc_backward(c);
@@ -1008,7 +1018,7 @@ __global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
                     const double as = phase_soc_alpha(c);
                     const Trial ts = phase_trial(c, as, rDXS, false);
                     STAMP(PH_SOC);
-                    if (filter_ok(c, nf, ts, th0, phi0, D, alpha, th_max, th_min, ftype)) {
+                    if (filter_ok(c, nf, ts, th0, phi0, D, alpha, th_max, th_min, pD, pT, ftype)) {
                         accepted = 2;
                         soc = true;
                         alpha = as;

@@ -107,6 +107,8 @@ def lib():
            "tt_interpolate_device": [i, i, i, vp, vp, vp, vp, vp],
            "tt_lqr_score_device": [i, C.POINTER(TTPlant), _dp, _dp, vp, vp, vp, vp, vp, vp, vp]}
     for name, args in sim.items():
+        if os.environ.get("TTMPC_LIB") and not hasattr(L, name):
+            continue  # A/B diagnostics against an older build
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = C.c_int

@@ -37,7 +37,7 @@ def test_introspection_without_gpu():
     from ttmpc import lib
     L = lib()
     assert L.tt_max_horizon() >= 60
-    assert L.tt_lds_bytes(20) == 8 * (157 * 21 + 256 + 32)
+    assert L.tt_lds_bytes(20) == 8 * (157 * 21 + 256)
     assert b"gfx950" in L.tt_version()
 
 
