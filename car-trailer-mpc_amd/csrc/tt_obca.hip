@@ -92,7 +92,6 @@ __device__ __forceinline__ void wave_sync() {
 
 struct Shared {
     double red[4][12];
-    double P[36], PA[36];
     // final-row (plan mode) state, owned by the thread of stage N
     double sf[6], vLf[6], vUf[6], ydf[6], df[6], dsf[2][6], ydpf[2][6], dft[6], dfr[6], Df[6], rf[6];
     double fth[kObcaMaxFilter], fph[kObcaMaxFilter];
@@ -101,9 +100,11 @@ struct Shared {
     unsigned long long stamp[kObcaPhases];
     unsigned long long t0;
 };
+typedef __attribute__((address_space(3))) Shared LShared;  // the kernel's Shared block, LDS-addressed
+
 
 // diagnostic phase clock (thread 0, shader cycles); a no-op unless the caller passed a stamps buffer
-__device__ __forceinline__ void stamp(Shared& sh, bool on, int ph) {
+__device__ __forceinline__ void stamp(LShared& sh, bool on, int ph) {
     if (on && threadIdx.x == 0) {
         const unsigned long long t = clock64();
         sh.stamp[ph] += t - sh.t0;
@@ -113,7 +114,7 @@ __device__ __forceinline__ void stamp(Shared& sh, bool on, int ph) {
 
 // workgroup reduction of NV values with per-value op; result uniform in every thread, fixed order
 template <int NV>
-__device__ __forceinline__ void wg_reduce(Shared& sh, double (&v)[NV], const int (&op)[NV]) {
+__device__ __forceinline__ void wg_reduce(LShared& sh, double (&v)[NV], const int (&op)[NV]) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double r[NV];
 #pragma unroll
@@ -157,9 +158,11 @@ struct LogSum {
 };
 
 // ---------------- per-instance context ----------------
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(3))) Shared LShared;  // the kernel's Shared block, LDS-addressed  // global-qualified: global_load / global_store
 struct Ctx {
     const ObcaArgs* a;
-    double* ws;
+    gdouble* ws;
     double* lds;  // dynamic LDS for the staged sweeps, or nullptr (sweeps read the HBM workspace)
     int N, NP, nbk, tid, b;
     double dt;
@@ -169,8 +172,8 @@ struct Ctx {
     double fL, fU;          // final box
     const double* tgt_x;    // plan: x_goal; track: xref of this instance
     const double* tgt_u;    // track: uref
-    __device__ __forceinline__ double& S(int f, int k) const { return ws[(size_t)f * NP + k]; }
-    __device__ __forceinline__ double& B(int f, int j, int k) const {
+    __device__ __forceinline__ gdouble& S(int f, int k) const { return ws[(size_t)f * NP + k]; }
+    __device__ __forceinline__ gdouble& B(int f, int j, int k) const {
         return ws[(size_t)S_END * NP + ((size_t)f * nbk + j) * NP + k];
     }
     __device__ __forceinline__ bool hlx(int i) const { return (hx >> i) & 1; }
@@ -649,7 +652,7 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, int j, int k, const do
 }
 
 // ======== phase: stage Hessians + gradients (all threads) -> fail flag (uniform) ========
-__device__ __noinline__ bool phase_factor(const Ctx& c, Shared& sh, double mu, double dw) {
+__device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, double dw) {
     const ObcaArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
@@ -746,9 +749,10 @@ struct GSrc {
 };
 // region A per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CR 6  (47);  region B: P 21 | PV 6 | K 12 | KF 2 (41)
 constexpr int LA = 47, LB = 41;
+typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: ds_read / ds_write
 struct LSrc {
-    const double* A;
-    double* B;
+    const lds_double* A;
+    lds_double* B;
     __device__ double QT(int i, int k) const { return A[k * LA + i]; }
     __device__ double QV(int i, int k) const { return A[k * LA + 21 + i]; }
     __device__ double RT(int i, int k) const { return A[k * LA + 27 + i]; }
@@ -786,143 +790,203 @@ __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
 // ======== phase: Riccati backward sweep (wave 0).  Sets sh.flag = 1 if an input block is not PD ========
 // P_N = Q~_N; G = R~ + B'PB, H = B'PA, K = -G^-1 H, P_k = Q~_k + A'PA + H'K   (B = dt [e5 e4])
 // vector: p' = p_{k+1} - P_{k+1} c_{k+1}, kff = -G^-1 (r~ + B'p'), p_k = q~_k + A'p' + H'kff
+//
+// Entry-parallel, branch-free: lane (i, j) < 36 forms PA[i][j] from row i of the P tile, then P_k at the
+// symmetric position (min, max) from column max of the PA tile, so both halves of the P tile are bitwise
+// equal.  Lanes 48..53 carry the vector recursion (row r = lane - 48).  A = I + D with D the 9 dt*J
+// nonzeros; the lane's D coefficients are selects on its column index, not branches.  One wave: LDS
+// operations complete in program order, so the two tiles need only compiler ordering, and the next
+// stage's operands are loaded behind the tile reads.
+struct RicOps {
+    double dj[9], e[6], R0, R1, R3, rv0, rv1, qt, qv;
+};
 template <class Src>
-__device__ __noinline__ void riccati(const Ctx& c, Shared& sh, const Src& src) {
+__device__ __forceinline__ void ric_ops(const Src& src, int k, int sij, int r, bool vec, RicOps& o) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) o.dj[q] = src.AJ(q, k);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) o.e[q] = src.CR(q, k + 1);
+    o.R0 = src.RT(0, k);
+    o.R1 = src.RT(1, k);
+    o.R3 = src.RT(2, k);
+    o.rv0 = src.RV(0, k);
+    o.rv1 = src.RV(1, k);
+    o.qt = src.QT(sij, k);
+    o.qv = vec ? src.QV(r, k) : 0.0;
+}
+// D[q][col] for q = 0..3 (rows 4, 5 of D are zero), as products with 0/1 column indicators so that the
+// coefficients stay in registers (a select of array elements would become a load of a selected address)
+struct ColMask {
+    double m2, m3, m4, m5;
+    __device__ explicit ColMask(int col)
+        : m2(col == 2 ? 1.0 : 0.0), m3(col == 3 ? 1.0 : 0.0), m4(col == 4 ? 1.0 : 0.0), m5(col == 5 ? 1.0 : 0.0) {}
+};
+__device__ __forceinline__ void dcol(const double* dj, const ColMask& m, double& c0, double& c1, double& c2,
+                                     double& c3) {
+    c0 = fma(m.m2, dj[0], m.m5 * dj[1]);
+    c1 = fma(m.m2, dj[2], m.m5 * dj[3]);
+    c2 = fma(m.m4, dj[4], m.m5 * dj[5]);
+    c3 = fma(m.m3, dj[6], fma(m.m4, dj[7], m.m5 * dj[8]));
+}
+__device__ __forceinline__ double2 ldd2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
+template <class Src>
+__device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) {
     const int lane = threadIdx.x, N = c.N;
-    const double dt = c.dt;
-    const int i = lane / 6, j = lane % 6;
-    const bool act = lane < 36;
-    if (act) sh.P[lane] = src.QT(sy6(i, j), N);
-    if (act && i <= j) src.setP(sy6(i, j), N, sh.P[lane]);
-    double pv = lane < 6 ? src.QV(lane, N) : 0.0;
-    if (lane < 6) src.setPV(lane, N, pv);
-    int fail = 0;
-    wave_sync();
-    for (int k = N - 1; k >= 0; --k) {
-        double dj[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) dj[q] = src.AJ(q, k);
-        double e[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k + 1);
-        const double R0 = src.RT(0, k), R1 = src.RT(1, k), R3 = src.RT(2, k);
-        const double rv0 = src.RV(0, k), rv1 = src.RV(1, k);
-        const double qt = act && i <= j ? src.QT(sy6(i, j), k) : 0.0;
-        const double qv = lane < 6 ? src.QV(lane, k) : 0.0;
-        // PA = P + P dJ   (column j of dJ: 2:{0,1} 3:{3} 4:{2,3} 5:{0,1,2,3})
-        double pa = 0.0, pp = 0.0;
-        if (act) {
-            const double* Pr = sh.P + 6 * i;
-            pa = Pr[j];
-            if (j == 2) pa += Pr[0] * dj[0] + Pr[1] * dj[2];
-            else if (j == 3) pa += Pr[3] * dj[6];
-            else if (j == 4) pa += Pr[2] * dj[4] + Pr[3] * dj[7];
-            else if (j == 5) pa += Pr[0] * dj[1] + Pr[1] * dj[3] + Pr[2] * dj[5] + Pr[3] * dj[8];
-            sh.PA[lane] = pa;
-        }
-        if (lane < 6) {
-            pp = pv;
-#pragma unroll
-            for (int q = 0; q < 6; ++q) pp -= sh.P[6 * lane + q] * e[q];
-        }
-        wave_sync();
-        const double G00 = R0 + dt * dt * sh.P[35], G01 = R1 + dt * dt * sh.P[34], G11 = R3 + dt * dt * sh.P[28];
+    const double dt = c.dt, dt2 = dt * dt;
+    const bool act = lane < 36, vec = lane >= 48 && lane < 54;
+    const int i = act ? lane / 6 : 0, j = act ? lane % 6 : 0, r = vec ? lane - 48 : 0;
+    const int ii = min(i, j), jj = max(i, j), sij = sy6(ii, jj);
+    const int row = vec ? r : i;  // row of P this lane reads
+    const ColMask mj(j), mi(ii), mr(r);
+    // the two tiles as LDS-addressed arrays (ds_read / ds_write, not flat accesses through `sh`)
+    __shared__ __attribute__((aligned(16))) double P[48];   // P_{k+1}, row-major, row stride 8
+    __shared__ __attribute__((aligned(16))) double PT[48];  // PA transposed: PT[8 j + r] = PA[r][j]
+    if (act) {
+        const double q = src.QT(sij, N);
+        P[8 * i + j] = q;
+        if (i <= j) src.setP(sij, N, q);
+    }
+    double pv = vec ? src.QV(r, N) : 0.0;
+    if (vec) src.setPV(r, N, pv);
+    bool fail = false;
+    // one stage; `cur` = this stage's operands, `nx` receives stage k-1's (ping-pong, no struct copies)
+    auto stage = [&](int k, const RicOps& cur, RicOps& nx) __attribute__((always_inline)) {
+        // ---- row `row` of P_{k+1}: PA[i][j] (act lanes) and p' = p - P c (vector lanes)
+        const double2 p01 = ldd2(P + 8 * row), p23 = ldd2(P + 8 * row + 2), p45 = ldd2(P + 8 * row + 4);
+        const double pij = P[8 * row + j];
+        const double2 g44 = ldd2(P + 8 * 4 + 4);  // P[4][4], P[4][5]
+        const double p55 = P[8 * 5 + 5];
+        double cj0, cj1, cj2, cj3;
+        dcol(cur.dj, mj, cj0, cj1, cj2, cj3);
+        const double pa = fma(p01.x, cj0, fma(p01.y, cj1, fma(p23.x, cj2, fma(p23.y, cj3, pij))));
+        if (act) PT[8 * j + i] = pa;
+        double pp = pv;
+        pp = fma(-p01.x, cur.e[0], pp);
+        pp = fma(-p01.y, cur.e[1], pp);
+        pp = fma(-p23.x, cur.e[2], pp);
+        pp = fma(-p23.y, cur.e[3], pp);
+        pp = fma(-p45.x, cur.e[4], pp);
+        pp = fma(-p45.y, cur.e[5], pp);
+        asm volatile("" ::: "memory");
+        // ---- reduced input Hessian G = R~ + B'PB and its inverse
+        const double G00 = cur.R0 + dt2 * p55, G01 = cur.R1 + dt2 * g44.y, G11 = cur.R3 + dt2 * g44.x;
         const double det = G00 * G11 - G01 * G01;
-        if (!(G00 > 0.0) || !(det > 0.0)) fail = 1;
-        const double idet = 1.0 / det;
+        fail = fail || !(G00 > 0.0) || !(det > 0.0);
+        const double idet = frcp(det);
         const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
-        double Pk = 0.0;
-        if (act && i <= j) {
-            const double* PAc = sh.PA;
-            double at = PAc[6 * i + j];
-            if (i == 2) at += dj[0] * PAc[0 * 6 + j] + dj[2] * PAc[1 * 6 + j];
-            else if (i == 3) at += dj[6] * PAc[3 * 6 + j];
-            else if (i == 4) at += dj[4] * PAc[2 * 6 + j] + dj[7] * PAc[3 * 6 + j];
-            else if (i == 5) at += dj[1] * PAc[0 * 6 + j] + dj[3] * PAc[1 * 6 + j] + dj[5] * PAc[2 * 6 + j] + dj[8] * PAc[3 * 6 + j];
-            const double H0i = dt * PAc[30 + i], H1i = dt * PAc[24 + i], H0j = dt * PAc[30 + j], H1j = dt * PAc[24 + j];
-            const double K0j = -(Gi00 * H0j + Gi01 * H1j), K1j = -(Gi01 * H0j + Gi11 * H1j);
-            Pk = qt + at + H0i * K0j + H1i * K1j;
-        }
+        // ---- column jj of PA, and PA[4..5][ii] (H at ii); vector lanes: PA[4..5][r]
+        const double2 a01 = ldd2(PT + 8 * jj), a23 = ldd2(PT + 8 * jj + 2), a45 = ldd2(PT + 8 * jj + 4);
+        const double aij = PT[8 * jj + ii];
+        const double2 hi = ldd2(PT + 8 * (vec ? r : ii) + 4);  // PA[4][.], PA[5][.]
+        if (k > 0) ric_ops(src, k - 1, sij, r, vec, nx);  // next stage's operands, behind the tile reads
+        double ci0, ci1, ci2, ci3;
+        dcol(cur.dj, mi, ci0, ci1, ci2, ci3);
+        const double atpa = fma(ci0, a01.x, fma(ci1, a01.y, fma(ci2, a23.x, fma(ci3, a23.y, aij))));
+        const double H0i = dt * hi.y, H1i = dt * hi.x, H0j = dt * a45.y, H1j = dt * a45.x;
+        const double K0j = -fma(Gi00, H0j, Gi01 * H1j), K1j = -fma(Gi01, H0j, Gi11 * H1j);
+        const double Pk = cur.qt + atpa + fma(H0i, K0j, H1i * K1j);
+        // ---- vector recursion: p' from lanes 48..53 to every lane (scalar registers)
         double ppl[6];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, q);
-        const double g0 = rv0 + dt * ppl[5], g1 = rv1 + dt * ppl[4];
-        const double kf0 = -(Gi00 * g0 + Gi01 * g1), kf1 = -(Gi01 * g0 + Gi11 * g1);
-        double pnew = 0.0;
-        if (lane < 6) {
-            const int r = lane;
-            double at = ppl[r];
-            if (r == 2) at += dj[0] * ppl[0] + dj[2] * ppl[1];
-            else if (r == 3) at += dj[6] * ppl[3];
-            else if (r == 4) at += dj[4] * ppl[2] + dj[7] * ppl[3];
-            else if (r == 5) at += dj[1] * ppl[0] + dj[3] * ppl[1] + dj[5] * ppl[2] + dj[8] * ppl[3];
-            pnew = qv + at + dt * sh.PA[30 + r] * kf0 + dt * sh.PA[24 + r] * kf1;
-            const double H0 = dt * sh.PA[30 + lane], H1 = dt * sh.PA[24 + lane];
-            src.setK(lane, k, -(Gi00 * H0 + Gi01 * H1));
-            src.setK(6 + lane, k, -(Gi01 * H0 + Gi11 * H1));
+        for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, 48 + q);
+        const double g0 = fma(dt, ppl[5], cur.rv0), g1 = fma(dt, ppl[4], cur.rv1);
+        const double kf0 = -fma(Gi00, g0, Gi01 * g1), kf1 = -fma(Gi01, g0, Gi11 * g1);
+        double cr0, cr1, cr2, cr3;
+        dcol(cur.dj, mr, cr0, cr1, cr2, cr3);
+        double ppr = ppl[0];
+        ppr = r == 1 ? ppl[1] : ppr;
+        ppr = r == 2 ? ppl[2] : ppr;
+        ppr = r == 3 ? ppl[3] : ppr;
+        ppr = r == 4 ? ppl[4] : ppr;
+        ppr = r == 5 ? ppl[5] : ppr;
+        const double atp = fma(cr0, ppl[0], fma(cr1, ppl[1], fma(cr2, ppl[2], fma(cr3, ppl[3], ppr))));
+        const double pnew = cur.qv + atp + fma(dt * hi.y, kf0, dt * hi.x * kf1);
+        // ---- outputs; the P tile is overwritten after every lane's reads of it were issued
+        if (act) {
+            P[8 * i + j] = Pk;
+            if (i <= j) src.setP(sij, k, Pk);
+        }
+        if (vec) {
+            const double H0 = dt * hi.y, H1 = dt * hi.x;
+            src.setK(r, k, -fma(Gi00, H0, Gi01 * H1));
+            src.setK(6 + r, k, -fma(Gi01, H0, Gi11 * H1));
+            src.setPV(r, k, pnew);
         }
         if (lane == 0) {
             src.setKF(0, k, kf0);
             src.setKF(1, k, kf1);
         }
-        wave_sync();
-        if (act && i <= j) {
-            sh.P[6 * i + j] = Pk;
-            sh.P[6 * j + i] = Pk;
-            src.setP(sy6(i, j), k, Pk);
-        }
         pv = pnew;
-        if (lane < 6) src.setPV(lane, k, pv);
-        wave_sync();
+        asm volatile("" ::: "memory");
+    };
+    RicOps oa, ob;
+    ric_ops(src, N - 1, sij, r, vec, oa);
+    asm volatile("" ::: "memory");
+    int k = N - 1;
+    for (; k >= 1; k -= 2) {
+        stage(k, oa, ob);
+        stage(k - 1, ob, oa);
     }
-    if (lane == 0) sh.flag = fail;
+    if (k == 0) stage(0, oa, ob);
+    // any lane's failure flag (all lanes evaluate the same uniform G; keep it explicit)
+    if (lane == 0) sh.flag = fail ? 1 : 0;
+    wave_sync();
 }
 
 // ======== phase: forward sweep (wave 0) into step buffer buf ========
+// dx_0 = -c_0; du_k = K_k dx_k + kff_k; dx_{k+1} = A_k dx_k + B du_k - c_{k+1}; y+_k = -(P_k dx_k + p_k).
+// The 6-vector recursion is carried redundantly by every lane (wave-uniform registers: no readlane /
+// broadcast on the serial chain); lanes 0..5 then write row r of the stage outputs off the chain.
 template <class Src>
 __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
-    double dx = lane < 6 ? -src.CR(lane, 0) : 0.0;
+    const int r = lane < 6 ? lane : 0;
+    double dx[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) dx[q] = -src.CR(q, 0);
     for (int k = 0;; ++k) {
-        double dxv[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) dxv[q] = readlane_d(dx, q);
         if (lane < 6) {
-            double t = src.PV(lane, k);
+            double t = src.PV(r, k), dxr = dx[0];
 #pragma unroll
-            for (int q = 0; q < 6; ++q) t += src.P(sy6(lane, q), k) * dxv[q];
-            c.S(S_YCP + 6 * buf + lane, k) = -t;
-            c.S(S_DX + 6 * buf + lane, k) = dx;
+            for (int q = 0; q < 6; ++q) t = fma(src.P(sy6(r, q), k), dx[q], t);
+#pragma unroll
+            for (int q = 1; q < 6; ++q) dxr = r == q ? dx[q] : dxr;
+            c.S(S_YCP + 6 * buf + r, k) = -t;
+            c.S(S_DX + 6 * buf + r, k) = dxr;
         }
         if (k == N) break;
         double du0 = src.KF(0, k), du1 = src.KF(1, k);
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
-            du0 += src.K(q, k) * dxv[q];
-            du1 += src.K(6 + q, k) * dxv[q];
+            du0 = fma(src.K(q, k), dx[q], du0);
+            du1 = fma(src.K(6 + q, k), dx[q], du1);
         }
         if (lane == 0) {
             c.S(S_DU + 2 * buf, k) = du0;
             c.S(S_DU + 2 * buf + 1, k) = du1;
         }
-        if (lane < 6) {
-            const int r = lane;
-            double t = dx - src.CR(r, k + 1);
-            if (r == 0) t += src.AJ(0, k) * dxv[2] + src.AJ(1, k) * dxv[5];
-            else if (r == 1) t += src.AJ(2, k) * dxv[2] + src.AJ(3, k) * dxv[5];
-            else if (r == 2) t += src.AJ(4, k) * dxv[4] + src.AJ(5, k) * dxv[5];
-            else if (r == 3) t += src.AJ(6, k) * dxv[3] + src.AJ(7, k) * dxv[4] + src.AJ(8, k) * dxv[5];
-            else if (r == 4) t += dt * du1;
-            else t += dt * du0;
-            dx = t;
-        }
+        double aj[9], e[6];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) aj[q] = src.AJ(q, k);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k + 1);
+        double nx[6];
+        nx[0] = (dx[0] - e[0]) + fma(aj[0], dx[2], aj[1] * dx[5]);
+        nx[1] = (dx[1] - e[1]) + fma(aj[2], dx[2], aj[3] * dx[5]);
+        nx[2] = (dx[2] - e[2]) + fma(aj[4], dx[4], aj[5] * dx[5]);
+        nx[3] = (dx[3] - e[3]) + fma(aj[6], dx[3], fma(aj[7], dx[4], aj[8] * dx[5]));
+        nx[4] = (dx[4] - e[4]) + dt * du1;
+        nx[5] = (dx[5] - e[5]) + dt * du0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) dx[q] = nx[q];
     }
 }
 
 // ======== phase: block step recovery + fraction to boundary + directional derivative ========
 // out: [0] alpha_primal (min), [1] alpha_dual (min), [2] grad phi' d (sum), [3] max relative step
-__device__ __noinline__ void phase_recover(const Ctx& c, Shared& sh, double mu, double dw, double tau, int buf, double (&out)[4]) {
+__device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, double (&out)[4]) {
     const int N = c.N;
     const bool plan = c.plan();
     double ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
@@ -1037,7 +1101,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, Shared& sh, double mu, 
 
 // ======== phase: trial point x + alpha d (step buffer buf) -> theta, phi (barrier objective), bad ========
 // also stores the trial residuals (for second-order corrections)
-__device__ __noinline__ void phase_trial(const Ctx& c, Shared& sh, double mu, double alpha, int buf, double (&out)[3]) {
+__device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, double alpha, int buf, double (&out)[3]) {
     const ObcaArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
@@ -1128,7 +1192,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, Shared& sh, double mu, do
 }
 
 // ======== phase: second-order-correction residual r <- a_soc r + r(trial) ========
-__device__ __noinline__ void phase_soc_resid(const Ctx& c, Shared& sh, double a_soc) {
+__device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a_soc) {
     for (int k = c.tid; k <= c.N; k += T) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = a_soc * c.S(S_CR + i, k) + c.S(S_CT + i, k);
@@ -1142,7 +1206,7 @@ __device__ __noinline__ void phase_soc_resid(const Ctx& c, Shared& sh, double a_
 }
 
 // ======== phase: accept the step ========
-__device__ __noinline__ void phase_update(const Ctx& c, Shared& sh, double mu, double alpha, double az, int buf) {
+__device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
     const int N = c.N;
     for (int k = c.tid; k <= N; k += T) {
 #pragma unroll
@@ -1229,12 +1293,12 @@ __device__ __noinline__ void phase_update(const Ctx& c, Shared& sh, double mu, d
     }
 }
 
-__device__ __forceinline__ bool in_filter(const Shared& sh, double th, double ph) {
+__device__ __forceinline__ bool in_filter(const LShared& sh, double th, double ph) {
     for (int i = 0; i < sh.nf; ++i)
         if (th >= sh.fth[i] && ph >= sh.fph[i]) return true;
     return false;
 }
-__device__ __forceinline__ void add_filter(Shared& sh, double th, double ph) {  // thread 0 only
+__device__ __forceinline__ void add_filter(LShared& sh, double th, double ph) {  // thread 0 only
     int j = 0;
     for (int i = 0; i < sh.nf; ++i)
         if (!(sh.fth[i] >= th && sh.fph[i] >= ph)) { sh.fth[j] = sh.fth[i]; sh.fph[j] = sh.fph[i]; ++j; }
@@ -1250,7 +1314,7 @@ __device__ __forceinline__ void add_filter(Shared& sh, double th, double ph) {  
 // ======== phase: linearisation at the iterate + optimality-error ingredients ========
 // out: [0] dual inf (max) [1] primal inf (max) [2] complementarity (max) [3] sum |y| + sum z
 //      [4] sum z [5] theta = l1 infeasibility [6] cost [7] sum log slacks
-__device__ __noinline__ void phase_lin(const Ctx& c, Shared& sh, double (&red)[8]) {
+__device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[8]) {
     const ObcaArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
@@ -1410,7 +1474,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, Shared& sh, double (&red)[8
 }
 
 // ======== phase: complementarity vs mu (max |z s - mu|) ========
-__device__ __noinline__ double phase_compl(const Ctx& c, Shared& sh, double mu) {
+__device__ __noinline__ double phase_compl(const Ctx& c, LShared& sh, double mu) {
     const int N = c.N;
     double cm[1] = {0.0};
     for (int k = c.tid; k <= N; k += T) {
@@ -1451,7 +1515,7 @@ __device__ __noinline__ double phase_compl(const Ctx& c, Shared& sh, double mu) 
 
 // Newton solve for the current residual arrays (S_CR / B_DR / sh.dfr) with the given dw into buffer buf.
 // Returns false when the Riccati/blocks are not positive definite.
-__device__ __noinline__ bool newton_solve(const Ctx& c, Shared& sh, double mu, double dw, int buf) {
+__device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
     const bool on = c.a->stamps != nullptr;
     stamp(sh, on, OPH_UPD);
     const bool f = phase_factor(c, sh, mu, dw);
@@ -1461,7 +1525,7 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, Shared& sh, double mu, d
         stage_inputs(c, c.lds);
         __syncthreads();
         stamp(sh, on, OPH_COMPL);  // (diagnostic: staging cost booked under 'compl')
-        const LSrc src{c.lds, c.lds + (size_t)LA * c.NP};
+        const LSrc src{(const lds_double*)c.lds, (lds_double*)(c.lds + (size_t)LA * c.NP)};
         if (threadIdx.x < 64) riccati(c, sh, src);
         __syncthreads();
         stamp(sh, on, OPH_RIC);
@@ -1482,7 +1546,8 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, Shared& sh, double mu, d
 
 // ---------------- the kernel ----------------
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void obca_kernel(ObcaArgs args) {
-    __shared__ Shared sh;
+    __shared__ Shared sh_storage;
+    LShared& sh = *(LShared*)&sh_storage;
     extern __shared__ double dyn_lds[];
     const ObcaArgs& a = args;
     Ctx c;
@@ -1493,7 +1558,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     c.NP = a.N + 1;
     c.nbk = 2 * a.M;
     c.tid = threadIdx.x;
-    c.ws = a.ws + (size_t)c.b * obca_ws_doubles(a.N, a.M);
+    c.ws = (gdouble*)(a.ws + (size_t)c.b * obca_ws_doubles(a.N, a.M));
     c.dt = a.dt;
     const int N = c.N, NBK = c.nbk, tid = c.tid;
     const bool plan = a.mode == OBCA_PLAN;
