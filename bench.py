@@ -86,6 +86,14 @@ def cpu_baseline(cfg, B, N, seed, budget_s):
                       f"on {ncores} visible host cores; oracle/c/tt_oracle.c (IPOPT-restated IPM, banded LU)"}
 
 
+def local_device():
+    """GPU of this rank: LOCAL_RANK (one process per GPU).  TTMPC_BENCH_DEVICE pins every rank to one GPU,
+    which only serves to rehearse the multi-rank flow on a one-GPU box (not a measurement setup)."""
+    if os.environ.get("TTMPC_BENCH_DEVICE"):
+        return int(os.environ["TTMPC_BENCH_DEVICE"])
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def rank_seed(rank):
     """Each rank owns a disjoint seeded shard of instances (weak scaling, no data-path collective)."""
     return 1000 * rank + 7
@@ -146,7 +154,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
@@ -269,7 +277,7 @@ def main_c5(args):
     from ttmpc.sharded import ShardedBatch, gpu_shard_solver
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device()
     B_total, N = args.batch or 65536, args.horizon or 20
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -366,7 +374,7 @@ def main_sim(args):
     from ttmpc import simulation as sim
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -505,7 +513,7 @@ def main_obca(args):
     from ttmpc import scenarios as sc
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device()
     dist = None
     if world > 1:
         import torch.distributed as dist
