@@ -158,10 +158,12 @@ struct LogSum {
 };
 
 // ---------------- per-instance context ----------------
-typedef __attribute__((address_space(1))) double gdouble;
-typedef __attribute__((address_space(3))) Shared LShared;  // the kernel's Shared block, LDS-addressed  // global-qualified: global_load / global_store
+typedef __attribute__((address_space(1))) double gdouble;  // global-qualified: global_load / global_store
+// the launch arguments, copied once into LDS: the phases read Q, R, bounds and obstacles with ds_read
+// broadcasts instead of flat loads from the kernel's private copy of the by-value argument
+typedef __attribute__((address_space(3))) const ObcaArgs LArgs;
 struct Ctx {
-    const ObcaArgs* a;
+    LArgs* a;
     gdouble* ws;
     double* lds;  // dynamic LDS for the staged sweeps, or nullptr (sweeps read the HBM workspace)
     int N, NP, nbk, tid, b;
@@ -188,7 +190,7 @@ struct Ctx {
 };
 
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
-__device__ __forceinline__ void model_f(const ObcaArgs& a, const double* x, const double* u, double* fo) {
+__device__ __forceinline__ void model_f(LArgs& a, const double* x, const double* u, double* fo) {
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
     const double t = tan(phi);
     double sth, cth, sps, cps;
@@ -203,7 +205,7 @@ __device__ __forceinline__ void model_f(const ObcaArgs& a, const double* x, cons
 }
 
 // dt*J nonzeros (9) and the dynamics curvature -dt sum_i y_i d2 f_i (7 nonzeros)
-__device__ __forceinline__ void model_lin(const ObcaArgs& a, const double* x, const double* y, double* dj, double* wd) {
+__device__ __forceinline__ void model_lin(LArgs& a, const double* x, const double* y, double* dj, double* wd) {
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
     const double L1 = a.L1, L2 = a.L2, M = a.Mh, dt = a.dt;
     double sn, cs, sp, cp;
@@ -233,7 +235,7 @@ __device__ __forceinline__ void model_lin(const ObcaArgs& a, const double* x, co
 struct Geom {
     double p0, p1, dpt0, dpt1, dpp0, dpp1, ppt0, ppt1, ptp0, ptp1, ppp0, ppp1, ca, sa, angp, hl, hw;
 };
-__device__ __forceinline__ void body_geom(const ObcaArgs& a, const double* xk, int body, Geom& g) {
+__device__ __forceinline__ void body_geom(LArgs& a, const double* xk, int body, Geom& g) {
     double st, ct;
     sincos(xk[2], &st, &ct);
     if (body == 0) {
@@ -259,10 +261,10 @@ __device__ __forceinline__ void body_geom(const ObcaArgs& a, const double* xk, i
 }
 
 // constraint values of block j (obstacle j>>1, body j&1)
-__device__ __forceinline__ void blk_vals(const ObcaArgs& a, const double* xk, int j, const double* w, double* d) {
+__device__ __forceinline__ void blk_vals(LArgs& a, const double* xk, int j, const double* w, double* d) {
     Geom g;
     body_geom(a, xk, j & 1, g);
-    const double* ob = a.obs + 4 * (j >> 1);
+    const auto* ob = a.obs + 4 * (j >> 1);
     const double ex = g.p0 - ob[0], ey = g.p1 - ob[1], hwo = 0.5 * ob[2], hho = 0.5 * ob[3];
     const double aa = w[4] - w[6], cc = w[5] - w[7];
     d[0] = g.hl * (w[0] + w[2]) + g.hw * (w[1] + w[3]) -
@@ -329,10 +331,10 @@ __device__ __forceinline__ void bsub4(const double* L, double* b) {
     }
 }
 
-__device__ __forceinline__ void blk_lin(const ObcaArgs& a, const double* xk, int j, const double* w, const double* y, Blk& k) {
+__device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, int j, const double* w, const double* y, Blk& k) {
     Geom g;
     body_geom(a, xk, j & 1, g);
-    const double* ob = a.obs + 4 * (j >> 1);
+    const auto* ob = a.obs + 4 * (j >> 1);
     const double ex = g.p0 - ob[0], ey = g.p1 - ob[1], hwo = 0.5 * ob[2], hho = 0.5 * ob[3];
     const double aa = w[4] - w[6], cc = w[5] - w[7];
     double nr = sqrt(aa * aa + cc * cc);
@@ -537,10 +539,10 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
 }
 
 // separating-axis dual certificate (see oracle/c/tt_obca.c:dual_certificate)
-__device__ __forceinline__ void dual_certificate(const ObcaArgs& a, const double* xk, int j, double* w) {
+__device__ __forceinline__ void dual_certificate(LArgs& a, const double* xk, int j, double* w) {
     Geom g;
     body_geom(a, xk, j & 1, g);
-    const double* ob = a.obs + 4 * (j >> 1);
+    const auto* ob = a.obs + 4 * (j >> 1);
     double best = -INFINITY, b0 = 1.0, b1 = 0.0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -592,7 +594,7 @@ __device__ __forceinline__ void load_x(const Ctx& c, int k, double* x) {
     for (int i = 0; i < 6; ++i) x[i] = c.S(S_X + i, k);
 }
 __device__ __forceinline__ double stage_cost(const Ctx& c, int k, const double* x, const double* u) {
-    const ObcaArgs& a = *c.a;
+    LArgs& a = *c.a;
     const double* tg = c.plan() ? c.tgt_x : c.tgt_x + 6 * k;
     const double sc = (k == c.N && c.plan()) ? a.tfac : 1.0;
     double e[6], F = 0.0;
@@ -653,7 +655,7 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, int j, int k, const do
 
 // ======== phase: stage Hessians + gradients (all threads) -> fail flag (uniform) ========
 __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, double dw) {
-    const ObcaArgs& a = *c.a;
+    LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
     double fail[1] = {0.0};
@@ -1102,7 +1104,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
 // ======== phase: trial point x + alpha d (step buffer buf) -> theta, phi (barrier objective), bad ========
 // also stores the trial residuals (for second-order corrections)
 __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, double alpha, int buf, double (&out)[3]) {
-    const ObcaArgs& a = *c.a;
+    LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
     double th = 0.0, F = 0.0, logs = 0.0, bad = 0.0;
@@ -1315,7 +1317,7 @@ __device__ __forceinline__ void add_filter(LShared& sh, double th, double ph) { 
 // out: [0] dual inf (max) [1] primal inf (max) [2] complementarity (max) [3] sum |y| + sum z
 //      [4] sum z [5] theta = l1 infeasibility [6] cost [7] sum log slacks
 __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[8]) {
-    const ObcaArgs& a = *c.a;
+    LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
 #pragma unroll
@@ -1549,9 +1551,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     __shared__ Shared sh_storage;
     LShared& sh = *(LShared*)&sh_storage;
     extern __shared__ double dyn_lds[];
-    const ObcaArgs& a = args;
+    __shared__ ObcaArgs args_lds;
+    {
+        const int* src = reinterpret_cast<const int*>(&args);
+        int* dst = reinterpret_cast<int*>(&args_lds);
+        for (int q = threadIdx.x; q < (int)(sizeof(ObcaArgs) / sizeof(int)); q += T) dst[q] = src[q];
+        __syncthreads();
+    }
+    LArgs& a = *(LArgs*)&args_lds;
     Ctx c;
-    c.a = &args;
+    c.a = &a;
     c.lds = obca_lds_bytes(a.N) <= kObcaLdsMax ? dyn_lds : nullptr;
     c.b = blockIdx.x;
     c.N = a.N;
