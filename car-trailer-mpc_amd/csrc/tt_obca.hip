@@ -662,6 +662,13 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
     for (int k = c.tid; k <= N; k += T) {
         double x[6];
         load_x(c, k, x);
+        // the 12 OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
+        double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
+        for (int j = 0; j < c.nbk; ++j) {
+            Blk bk;
+            double fw[8], zf[8], t4[4];
+            if (!block_setup(c, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+        }
         double Qs[21], qv[6];
         const double sc = (k == N && plan) ? a.tfac : 1.0;
 #pragma unroll
@@ -684,12 +691,6 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
             if (c.hux(i)) { sg += c.S(S_ZUX + i, k) / (c.xu[i] - xv); g += mu / (c.xu[i] - xv); }
             Qs[sy6(i, i)] += sg;
             qv[i] = g;
-        }
-        double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
-        for (int j = 0; j < c.nbk; ++j) {
-            Blk bk;
-            double fw[8], zf[8], t4[4];
-            if (!block_setup(c, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {

@@ -219,3 +219,31 @@ def test_reference_call_surface():
     sf, uf = f.solve(x0[0], Xr, Ur)
     assert sf.shape == (6, 21)
     assert f.solve(bad, Xr, Ur) == (None, None)
+
+
+def test_max_horizon_matches_oracle():
+    """The largest horizon whose instance fits one CU's LDS (tt_max_horizon: 127 doubles-stage records)."""
+    import ttmpc
+    from ttmpc.scenarios import synthetic_batch
+    N = ttmpc.lib().tt_max_horizon()
+    assert N >= 120
+    x0, xr, ur = synthetic_batch(32, N, seed=77)
+    X, U, st, it, kk = _gpu_solver(N).solve(x0, xr, ur)
+    zc, stc, itc, kkc = _oracle(N, x0, xr, ur)
+    assert np.array_equal(st, stc) and np.all(st <= 1)
+    assert np.max(np.abs(_z(X, U) - zc) / np.maximum(1.0, np.abs(zc))) <= 1e-7
+
+
+def test_non_finite_reference_is_reported_not_propagated():
+    """A NaN in one instance's reference ends that instance with TT_NONFINITE; its neighbours are untouched."""
+    import ttmpc
+    from ttmpc.scenarios import synthetic_batch
+    N = 20
+    x0, xr, ur = synthetic_batch(6, N, seed=21)
+    X0, U0, st0, _, _ = _gpu_solver(N).solve(x0, xr, ur)
+    xr[2, 7, 1] = np.nan
+    ur[4, 3, 0] = np.inf
+    X, U, st, it, kk = _gpu_solver(N).solve(x0, xr, ur)
+    assert st[2] == ttmpc.TT_NONFINITE and st[4] == ttmpc.TT_NONFINITE
+    ok = [0, 1, 3, 5]
+    assert np.array_equal(st[ok], st0[ok]) and np.array_equal(X[ok], X0[ok]) and np.array_equal(U[ok], U0[ok])
