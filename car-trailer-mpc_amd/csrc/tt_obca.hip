@@ -659,7 +659,7 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
     const int N = c.N;
     const bool plan = c.plan();
     double fail[1] = {0.0};
-    for (int k = c.tid; k <= N; k += T) {
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6];
         load_x(c, k, x);
         // the 12 OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
@@ -993,7 +993,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
     const int N = c.N;
     const bool plan = c.plan();
     double ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
-    for (int k = c.tid; k <= N; k += T) {
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], dx[6];
         load_x(c, k, x);
 #pragma unroll
@@ -1109,7 +1109,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
     const int N = c.N;
     const bool plan = c.plan();
     double th = 0.0, F = 0.0, logs = 0.0, bad = 0.0;
-    for (int k = c.tid; k <= N; k += T) {
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0};
 #pragma unroll
         for (int i = 0; i < 6; ++i) x[i] = c.S(S_X + i, k) + alpha * c.S(S_DX + 6 * buf + i, k);
@@ -1196,7 +1196,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
 
 // ======== phase: second-order-correction residual r <- a_soc r + r(trial) ========
 __device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a_soc) {
-    for (int k = c.tid; k <= c.N; k += T) {
+    for (int k = (int)threadIdx.x; k <= c.N; k += T) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = a_soc * c.S(S_CR + i, k) + c.S(S_CT + i, k);
         for (int j = 0; j < c.nbk; ++j)
@@ -1211,7 +1211,7 @@ __device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a
 // ======== phase: accept the step ========
 __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
     const int N = c.N;
-    for (int k = c.tid; k <= N; k += T) {
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double x = c.S(S_X + i, k), d = c.S(S_DX + 6 * buf + i, k);
@@ -1324,7 +1324,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
     for (int i = 0; i < 8; ++i) red[i] = 0.0;
     const double* xinit = a.x0 + 6 * (size_t)c.b;
-    for (int k = c.tid; k <= N; k += T) {
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0}, gl[6];
         load_x(c, k, x);
         if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
@@ -1480,7 +1480,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 __device__ __noinline__ double phase_compl(const Ctx& c, LShared& sh, double mu) {
     const int N = c.N;
     double cm[1] = {0.0};
-    for (int k = c.tid; k <= N; k += T) {
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
         double m = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -1597,6 +1597,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     c.rhi = a.eq_tol + RELAX;
     c.fL = -a.fin_tol - RELAX;
     c.fU = a.fin_tol + RELAX;
+    // the phases read the (uniform) context from an LDS copy instead of this thread's private copy
+    __shared__ Ctx cs_storage;
+    if (threadIdx.x == 0) cs_storage = c;
+    __syncthreads();
+    const Ctx& cs = cs_storage;
     const int st = 8 + 16 * a.M;
     const size_t nz = obca_n(N, a.M);
     const double* zg = a.zg ? a.zg + (size_t)c.b * nz : nullptr;
@@ -1708,7 +1713,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         for (iter = 0;; ++iter) {
             double red[8];
             stamp(sh, ston, OPH_UPD);
-            phase_lin(c, sh, red);
+            phase_lin(cs, sh, red);
             stamp(sh, ston, OPH_LIN);
             const double dinf = red[0], pinf = red[1], c0 = red[2];
             const double th0 = red[5];
@@ -1726,7 +1731,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; break; }
             // ---- barrier update (monotone, Fiacco-McCormick) ----
             while (mu > a.tol / 10.0 * 1.0000001) {
-                const double Emu = fmax(fmax(dinf / sd, pinf), phase_compl(c, sh, mu) / sc);
+                const double Emu = fmax(fmax(dinf / sd, pinf), phase_compl(cs, sh, mu) / sc);
                 stamp(sh, ston, OPH_COMPL);
                 if (!(Emu <= kappa_eps * mu)) break;
                 mu = fmax(a.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
@@ -1751,14 +1756,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             double dw = 0.0;
             bool ok = false;
             for (int attempt = 0; attempt < 40; ++attempt) {
-                if (newton_solve(c, sh, mu, dw, 0)) { ok = true; break; }
+                if (newton_solve(cs, sh, mu, dw, 0)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
                 if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
             }
             if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
             if (dw > 0) dw_last = dw;
             double rec[4];
-            phase_recover(c, sh, mu, dw, tau, 0, rec);
+            phase_recover(cs, sh, mu, dw, tau, 0, rec);
             stamp(sh, ston, OPH_REC);
             const double ap = rec[0], Dm = rec[2], rel = rec[3];
             double az = rec[1];
@@ -1779,7 +1784,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             bool ftype = false;
             for (int ls = 0; !accepted; ++ls) {
                 double tr[3];
-                phase_trial(c, sh, mu, alpha, 0, tr);
+                phase_trial(cs, sh, mu, alpha, 0, tr);
                 stamp(sh, ston, OPH_TRIAL);
                 const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
                 bool okls = false;
@@ -1807,15 +1812,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     for (int p = 0; p < 4; ++p) {
                         if (p > 0 && th_t > 0.99 * th_old) break;
                         th_old = th_t;
-                        phase_soc_resid(c, sh, a_soc);
+                        phase_soc_resid(cs, sh, a_soc);
                         __syncthreads();
-                        if (!newton_solve(c, sh, mu, dw, 1)) break;
+                        if (!newton_solve(cs, sh, mu, dw, 1)) break;
                         double rs[4];
-                        phase_recover(c, sh, mu, dw, tau, 1, rs);
+                        phase_recover(cs, sh, mu, dw, tau, 1, rs);
                         stamp(sh, ston, OPH_REC);
                         a_soc = rs[0];
                         double t2[3];
-                        phase_trial(c, sh, mu, a_soc, 1, t2);
+                        phase_trial(cs, sh, mu, a_soc, 1, t2);
                         stamp(sh, ston, OPH_TRIAL);
                         th_t = t2[0];
                         bool ok2 = false;
@@ -1838,7 +1843,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 if (tid == 0) add_filter(sh, (1.0 - g_th) * th0, phi0 - g_ph * th0);
             }
             __syncthreads();
-            phase_update(c, sh, mu, alpha, az, buf);
+            phase_update(cs, sh, mu, alpha, az, buf);
             __syncthreads();
             stamp(sh, ston, OPH_UPD);
         }
