@@ -187,6 +187,8 @@ struct Ctx {
     double mu, tau;
     __device__ __forceinline__ double& r(int row, int k) const { return sm[HEAD + k * SR + row]; }
     __device__ __forceinline__ double& h(int i) const { return sm[i]; }
+    // bit 16 of a specialised bound pattern: Q and R are diagonal (the reference's Q = I, R = 10 I)
+    static constexpr bool kDiag = BM >= 0 && ((BM >> 16) & 1);
     __device__ __forceinline__ bool hl(int v) const {
         if constexpr (BM >= 0) return (BM >> v) & 1;
         else return sm[hLB + v] > -INFINITY;
@@ -308,14 +310,21 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
             if (v >= 6 && k == N) break;
             double gf;
             if (v < 6) {
-                gf = 0.0;
+                if constexpr (Ctx<BM>::kDiag) {
+                    gf = c.h(hQW + v * 7) * dxr[v];
+                } else {
+                    gf = 0.0;
 #pragma unroll
-                for (int j = 0; j < 6; ++j) gf += c.h(hQW + v * 6 + j) * dxr[j];
+                    for (int j = 0; j < 6; ++j) gf += c.h(hQW + v * 6 + j) * dxr[j];
+                }
                 cost += dxr[v] * gf;
                 gf *= 2.0;
             } else {
                 const int rr = v - 6;
-                gf = c.h(hRW + rr * 2) * du0 + c.h(hRW + rr * 2 + 1) * du1;
+                if constexpr (Ctx<BM>::kDiag)
+                    gf = c.h(hRW + rr * 3) * (rr == 0 ? du0 : du1);
+                else
+                    gf = c.h(hRW + rr * 2) * du0 + c.h(hRW + rr * 2 + 1) * du1;
                 cost += (rr == 0 ? du0 : du1) * gf;
                 gf *= 2.0;
             }
@@ -706,16 +715,24 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
         double dxr[6], cost = 0.0, th = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.r(rXR + i, k);
+        if constexpr (Ctx<BM>::kDiag) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            double s = 0.0;
+            for (int i = 0; i < 6; ++i) cost += dxr[i] * (c.h(hQW + i * 7) * dxr[i]);
+        } else {
 #pragma unroll
-            for (int j = 0; j < 6; ++j) s += c.h(hQW + i * 6 + j) * dxr[j];
-            cost += dxr[i] * s;
+            for (int i = 0; i < 6; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < 6; ++j) s += c.h(hQW + i * 6 + j) * dxr[j];
+                cost += dxr[i] * s;
+            }
         }
         if (k < N) {
             const double e0 = u[0] - c.r(rUR, k), e1 = u[1] - c.r(rUR + 1, k);
-            cost += e0 * (c.h(hRW) * e0 + c.h(hRW + 1) * e1) + e1 * (c.h(hRW + 2) * e0 + c.h(hRW + 3) * e1);
+            if constexpr (Ctx<BM>::kDiag)
+                cost += e0 * (c.h(hRW) * e0) + e1 * (c.h(hRW + 3) * e1);
+            else
+                cost += e0 * (c.h(hRW) * e0 + c.h(hRW + 1) * e1) + e1 * (c.h(hRW + 2) * e0 + c.h(hRW + 3) * e1);
         }
         LogSum ls;
 #pragma unroll
@@ -1091,11 +1108,21 @@ hipError_t launch(const TrackArgs& a, hipStream_t stream) {
 // simulation.py:411-414) and the OBCA box (theta free too: trajectory_animation.py:77-80).
 constexpr int kMaskMPC = 0xFCFC;
 constexpr int kMaskOBCA = 0xF8F8;
+constexpr int kDiagBit = 1 << 16;  // Q, R diagonal: the cost and its gradient skip the off-diagonal terms
+
+// Q and R diagonal after symmetrisation (the kernel's weights are 0.5 (Q + Q'), 0.5 (R + R'))
+bool diagonal_weights(const TrackArgs& a) {
+    for (int i = 0; i < 6; ++i)
+        for (int j = i + 1; j < 6; ++j)
+            if (0.5 * (a.Q[i * 6 + j] + a.Q[j * 6 + i]) != 0.0) return false;
+    return 0.5 * (a.R[1] + a.R[2]) == 0.0;
+}
 
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     const int m = bound_mask(a);
-    if (m == kMaskMPC) return launch<kMaskMPC>(a, stream);
-    if (m == kMaskOBCA) return launch<kMaskOBCA>(a, stream);
+    const bool d = diagonal_weights(a);
+    if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
+    if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);
     return launch<-1>(a, stream);
 }
 

@@ -247,3 +247,25 @@ def test_non_finite_reference_is_reported_not_propagated():
     assert st[2] == ttmpc.TT_NONFINITE and st[4] == ttmpc.TT_NONFINITE
     ok = [0, 1, 3, 5]
     assert np.array_equal(st[ok], st0[ok]) and np.array_equal(X[ok], X0[ok]) and np.array_equal(U[ok], U0[ok])
+
+
+def test_non_diagonal_weights_match_oracle():
+    """Dense (non-diagonal) Q and R take the general weight path of the kernel (the reference's diagonal
+    Q = I, R = 10 I take the specialised one); both must agree with the oracle."""
+    import ttmpc
+    from oracle import c_oracle as co
+    from oracle import ttmpc_oracle as to
+    from ttmpc.scenarios import synthetic_batch
+    N = 20
+    rng = np.random.default_rng(5)
+    A = rng.normal(size=(6, 6))
+    Q = np.eye(6) + 0.1 * (A @ A.T)
+    R = np.array([[10.0, 1.5], [1.5, 8.0]])
+    x0, xr, ur = synthetic_batch(64, N, seed=55)
+    s = ttmpc.BatchSolver(N, P, Q, R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB, to.MPC_UUB)
+    X, U, st, it, kk = s.solve(x0, xr, ur)
+    nlp = to.TrackingNLP(N)
+    Pp = co.make_problem(N, P, Q, R, nlp.xlb, nlp.xub, nlp.ulb, nlp.uub)
+    zc, stc, itc, kkc = co.solve_batch(Pp, x0, xr, ur)
+    assert np.array_equal(st, stc) and np.all(st <= 1)
+    assert np.max(np.abs(_z(X, U) - zc) / np.maximum(1.0, np.abs(zc))) <= 1e-7
