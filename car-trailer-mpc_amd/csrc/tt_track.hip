@@ -642,14 +642,14 @@ __device__ __forceinline__ void phase_soc_backward(const Ctx<BM>& c) {
 }
 
 struct StepInfo {
-    double ap, az, ymax, Dg, rel;
+    double ap, az, Dg, rel;
 };
 
 // ============ new multipliers y+ = -(P dx + p), step bounds, merit slope (stage-parallel) ============
 template <int BM>
 __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool primal_pieces) {
     const int N = c.N;
-    double ap = 1.0, az = 1.0, ymax = 0.0, Dg = 0.0, rel = 0.0;
+    double ap = 1.0, az = 1.0, Dg = 0.0, rel = 0.0;
     for (int k = c.lane; k <= N; k += W) {
         double dx[6];
 #pragma unroll
@@ -660,14 +660,13 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
 #pragma unroll
             for (int j = 0; j < 6; ++j) s += c.r(rPS + sym_idx(i, j), k) * dx[j];
             c.r(rYP + i, k) = -s;
-            ymax = fmax(ymax, fabs(s));
         }
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
             const double d = c.r(dzr + v, k), xv = c.r(rX + v, k);
             Dg += c.gr(v, k) * d;
-            rel = fmax(rel, fabs(d) / (1.0 + fabs(xv)));
+            rel = fmax(rel, fabs(d) * frcp(1.0 + fabs(xv)));  // only tested against 1e-15
             if (c.hl(v)) {
                 const double s = xv - c.lb(v), rs = frcp(s), zl = c.r(rZL + v, k);
                 ftb(s, d, c.tau, ap);
@@ -684,11 +683,10 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
     r.az = wmin(az);
     r.ap = wmin(ap);
     if (primal_pieces) {
-        r.ymax = wmax(ymax);
         r.Dg = wsum(Dg);
         r.rel = wmax(rel);
     } else {
-        r.ymax = r.Dg = r.rel = 0.0;
+        r.Dg = r.rel = 0.0;
     }
     __syncthreads();
     return r;
