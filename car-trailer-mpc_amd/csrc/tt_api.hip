@@ -245,7 +245,7 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
     a.kkt = d_kkt_res;
     a.status = d_status;
     a.iters = d_iters;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);
     e = ttmpc::launch_track(a, s);
     if (e != hipSuccess) return hip_fail(h, e, "track kernel launch");
     return 0;
@@ -306,7 +306,7 @@ int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_x
     a.status = d_status;
     a.iters = d_iters;
     a.stamps = d_stamps;
-    hipError_t e = ttmpc::launch_track(a, stream ? static_cast<hipStream_t>(stream) : h->stream);
+    hipError_t e = ttmpc::launch_track(a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(h, e, "stamped launch");
 }
 #endif
@@ -371,7 +371,7 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
     a.kkt = d_kkt_res;
     a.ws = h->d_ows;
     a.stamps = g_obca_stamps;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : h->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);
     e = ttmpc::launch_obca(a, s);
     if (e != hipSuccess) return hip_fail(h, e, "OBCA kernel launch");
     return 0;

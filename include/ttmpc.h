@@ -77,8 +77,9 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
                    const double* wq_wr, const double* z_guess, double* x_out, double* u_out, int* status,
                    int* iters, double* kkt_res);
 
-/* Same with DEVICE pointers (already resident in HBM), enqueued on `stream` (hipStream_t, NULL =
- * the handle's stream); asynchronous.  Used by the bench and by device-resident callers. */
+/* Same with DEVICE pointers (already resident in HBM), enqueued on `stream` (hipStream_t; NULL = the
+ * default stream, as in every HIP API -- e.g. torch's default stream); asynchronous.  Used by the bench
+ * and by device-resident callers. */
 int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xref, const double* d_uref,
                           const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out,
                           int* d_status, int* d_iters, double* d_kkt_res, void* stream);
@@ -99,7 +100,7 @@ int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, co
 int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
                         const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
                         int* status, int* iters, double* kkt_res);
-/* Same with DEVICE pointers, asynchronous on `stream` (NULL = the handle's stream). */
+/* Same with DEVICE pointers, asynchronous on `stream` (NULL = the default stream). */
 int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
                                const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
                                double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream);
