@@ -146,6 +146,7 @@ def main():
                     help="comma-separated rocprofv3 --pmc CSVs (FETCH_SIZE, WRITE_SIZE) of this config; "
                          "default: the committed profiles/ pair when the config is the default C2")
     ap.add_argument("--max-iter", type=int, default=1000, help="OBCA configs: IPOPT max_iter (reference: 5000)")
+    ap.add_argument("--graph", action="store_true", help="sim: replay one captured closed-loop step (hipGraph)")
     args = ap.parse_args()
     if args.config in ("c4", "cobs"):
         return main_obca(args)
@@ -402,16 +403,40 @@ def main_sim(args):
     while len(k_list) < args.warmup + args.steps:
         k_list.append(int(np.floor(t_sim / dt)))
         t_sim += dt
-    for k in k_list[: args.warmup]:
-        cl.step(k)
+    if args.graph:
+        # the step index, the k sequence and the noise of every step on the device; one captured step
+        K = args.warmup + args.steps
+        d_ks = torch.tensor(k_list, dtype=torch.int32, device=dev)
+        d_step = torch.zeros(1, dtype=torch.int32, device=dev)
+        noise_all = torch.randn((K, B, 6), generator=cl.gen, dtype=torch.float64, device=dev)
+        noise_all.mul_(sim.DISTURBANCE_PARAMS["process_noise_std"])
+        logs = (torch.empty((K + 1, B, 6), dtype=torch.float64, device=dev),
+                torch.empty((K, B, 2), dtype=torch.float64, device=dev),
+                torch.zeros((K, B), dtype=torch.int32, device=dev), torch.zeros((K, B), dtype=torch.int32, device=dev),
+                torch.zeros((K, B), dtype=torch.int32, device=dev))
+        torch.cuda.synchronize(dev)
+        with torch.cuda.stream(cl.stream):
+            cl._graph_step(True, d_ks, d_step, noise_all, logs)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=cl.stream):
+            cl._graph_step(False, d_ks, d_step, noise_all, logs)
+        run_step = lambda k: graph.replay()  # noqa: E731
+        warm_steps = k_list[1: args.warmup]
+    else:
+        run_step = cl.step
+        warm_steps = k_list[: args.warmup]
+    with torch.cuda.stream(cl.stream):
+        for k in warm_steps:
+            run_step(k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(cl.stream)
-    for k in k_list[args.warmup:]:
-        cl.step(k)
+    with torch.cuda.stream(cl.stream):  # graph replay() launches on the current stream
+        for k in k_list[args.warmup:]:
+            run_step(k)
     e1.record(cl.stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -447,7 +472,8 @@ def main_sim(args):
         "data": "the reference's committed OBCA plan (data/state_traj.txt, do_interpolation 0.1 -> 0.05) with "
                 "B perturbed starts, DISTURBANCE_PARAMS of simulation.py, device-drawn measurement noise",
         "config": {"workload": f"sim: B={B} closed loops/GPU, N={N}, steps {args.warmup}+{args.steps} of the "
-                               "simulation.py loop (window, SAT collision check, solve, disturbed plant update)",
+                               "simulation.py loop (window, SAT collision check, solve, disturbed plant update)"
+                               + (", one captured step replayed as a hipGraph" if args.graph else ""),
                    "batch_per_gpu": B, "horizon": N, "parallelism": f"dp{world} (independent instances)"},
         "solver": {"converged_or_acceptable_last_step": ok_total, "instances": B_total,
                    "status_counts_last_step": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},

@@ -62,6 +62,68 @@ __global__ void __launch_bounds__(kThreads) sim_window_kernel(int B, int N, int 
     }
 }
 
+// ---- the same window for a step index read from the device (hipGraph replay of a closed-loop step):
+// k = ks[*step] (the reference's float-accumulated clock, precomputed), noise = noise_all[*step]
+__global__ void __launch_bounds__(kThreads) sim_window_indexed_kernel(int B, int N, const int* __restrict__ ks,
+                                                                      const int* __restrict__ step, int Np,
+                                                                      const double* __restrict__ px,
+                                                                      const double* __restrict__ pu, int per_instance,
+                                                                      const double* __restrict__ state,
+                                                                      const double* __restrict__ noise_all,
+                                                                      double* __restrict__ xmeas,
+                                                                      double* __restrict__ xr, double* __restrict__ ur) {
+    const int j = *step;
+    const int k = ks[j];
+    const double* noise = noise_all ? noise_all + (size_t)j * B * 6 : nullptr;
+    const long long t = (long long)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= (long long)B * (N + 1)) return;
+    const int b = (int)(t / (N + 1)), jj = (int)(t % (N + 1));
+    const size_t pb = per_instance ? (size_t)b : 0;
+    const double* src = px + (pb * (Np + 1) + min(k + jj, Np)) * 6;
+    double* dst = xr + ((size_t)b * (N + 1) + jj) * 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dst[i] = src[i];
+    if (jj < N) {
+        double* du = ur + ((size_t)b * N + jj) * 2;
+        if (k < Np) {
+            const double* su = pu + (pb * Np + min(k + jj, Np - 1)) * 2;
+            du[0] = su[0];
+            du[1] = su[1];
+        } else {
+            du[0] = 0.0;
+            du[1] = 0.0;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double v = state[(size_t)b * 6 + i];
+            xmeas[(size_t)b * 6 + i] = noise ? v + noise[(size_t)b * 6 + i] : v;
+        }
+    }
+}
+
+// closed-loop logs at the device step index: S[step+1] = state, Ua[step] = applied control, status /
+// iterations / collision flag of the step
+__global__ void __launch_bounds__(kThreads) sim_log_kernel(int B, const int* __restrict__ step,
+                                                           const double* __restrict__ state,
+                                                           const double* __restrict__ ua, const int* __restrict__ st,
+                                                           const int* __restrict__ it, const int* __restrict__ fl,
+                                                           double* __restrict__ S, double* __restrict__ Ua,
+                                                           int* __restrict__ Ss, int* __restrict__ Si,
+                                                           int* __restrict__ Sc) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= B) return;
+    const size_t j = (size_t)*step;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) S[((j + 1) * B + b) * 6 + i] = state[(size_t)b * 6 + i];
+    Ua[(j * B + b) * 2] = ua[(size_t)b * 2];
+    Ua[(j * B + b) * 2 + 1] = ua[(size_t)b * 2 + 1];
+    Ss[j * B + b] = st[b];
+    Si[j * B + b] = it ? it[b] : 0;
+    Sc[j * B + b] = fl ? fl[b] : 0;
+}
+__global__ void sim_advance_kernel(int* step) { *step += 1; }
+
 // ---- SAT collision: check_obb_aabb_collision for truck and trailer, every pose, every obstacle ------
 // Evaluated literally as the reference does (corners = R local + c, projections min/max of corners . axis,
 // strict '<' gap test, touching = collision), without FMA contraction so the arithmetic is numpy's.
@@ -278,6 +340,32 @@ int tt_sim_window_device(int B, int N, int k, int Np, const double* plan_x, cons
     hipLaunchKernelGGL(sim_window_kernel, dim3(grid_for(tot)), dim3(kThreads), 0, (hipStream_t)stream, B, N, k, Np,
                        plan_x, plan_u, per_instance, state, meas_noise, x_meas, xref, uref);
     return launched("sim_window_kernel");
+}
+
+int tt_sim_window_indexed_device(int B, int N, const int* ks, const int* step, int Np, const double* plan_x,
+                                 const double* plan_u, int per_instance, const double* state, const double* noise_all,
+                                 double* x_meas, double* xref, double* uref, void* stream) {
+    if (B < 0 || N < 1 || Np < 1 || !ks || !step || !plan_x || !plan_u || !state || !x_meas || !xref || !uref)
+        return -EINVAL;
+    if (B == 0) return 0;
+    const long long tot = (long long)B * (N + 1);
+    hipLaunchKernelGGL(sim_window_indexed_kernel, dim3(grid_for(tot)), dim3(kThreads), 0, (hipStream_t)stream, B, N,
+                       ks, step, Np, plan_x, plan_u, per_instance, state, noise_all, x_meas, xref, uref);
+    return launched("sim_window_indexed_kernel");
+}
+
+int tt_sim_log_advance_device(int B, int* step, const double* state, const double* u_applied, const int* status,
+                              const int* iters, const int* flag, double* S, double* Ua, int* Ss, int* Si, int* Sc,
+                              void* stream) {
+    if (B < 0 || !step || !state || !u_applied || !status || !S || !Ua || !Ss || !Si || !Sc) return -EINVAL;
+    if (B > 0) {
+        hipLaunchKernelGGL(sim_log_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, step, state,
+                           u_applied, status, iters, flag, S, Ua, Ss, Si, Sc);
+        const int rc = launched("sim_log_kernel");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(sim_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+    return launched("sim_advance_kernel");
 }
 
 int tt_collision_device(int B, int K, const double* poses, long long stride_b, int stride_k, const double* obstacles,

@@ -105,7 +105,9 @@ def lib():
            "tt_warm_start_device": [i, i, vp, vp, vp, vp, i, vp, vp],
            "tt_record_solution_device": [i, i, vp, vp, vp, vp, vp, vp],
            "tt_interpolate_device": [i, i, i, vp, vp, vp, vp, vp],
-           "tt_lqr_score_device": [i, C.POINTER(TTPlant), _dp, _dp, vp, vp, vp, vp, vp, vp, vp]}
+           "tt_lqr_score_device": [i, C.POINTER(TTPlant), _dp, _dp, vp, vp, vp, vp, vp, vp, vp],
+           "tt_sim_window_indexed_device": [i, i, vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp],
+           "tt_sim_log_advance_device": [i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]}
     for name, args in sim.items():
         if os.environ.get("TTMPC_LIB") and not hasattr(L, name):
             continue  # A/B diagnostics against an older build
@@ -120,7 +122,8 @@ EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_
                     "tt_obca_solve_batch_device", "tt_obca_n", "tt_obca_workspace_bytes", "tt_destroy",
                     "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version", "tt_sim_window_device",
                     "tt_collision_device", "tt_plant_update_device", "tt_warm_start_device",
-                    "tt_record_solution_device", "tt_interpolate_device", "tt_lqr_score_device")
+                    "tt_record_solution_device", "tt_interpolate_device", "tt_lqr_score_device",
+                    "tt_sim_window_indexed_device", "tt_sim_log_advance_device")
 
 
 def _ptr(a):

@@ -233,6 +233,83 @@ class ClosedLoop:
                          stream=s)
         self.first = False
 
+    # ---------------- hipGraph replay of the closed loop ----------------
+    def _graph_step(self, first, d_ks, d_step, noise_all, logs):
+        """Enqueue one closed-loop step whose step index lives on the device (replayable)."""
+        L, s, B, N = lib(), self.stream, self.B, self.N
+        sp = C.c_void_p(s.cuda_stream)
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        Np = self.plan_u.shape[-2]
+        per = int(self.plan_x.shape[0] != 1)
+        _check(L.tt_sim_window_indexed_device(B, N, d_ks.data_ptr(), d_step.data_ptr(), int(Np),
+                                              self.plan_x.data_ptr(), self.plan_u.data_ptr(), per,
+                                              self.state.data_ptr(), ptr(noise_all), self.x_meas.data_ptr(),
+                                              self.xref.data_ptr(), self.uref.data_ptr(), sp),
+               "tt_sim_window_indexed_device")
+        if self.check_collision:
+            collision_flags(self.xref if first else self.X, self.obstacles, self.params, self.flag, stream=s)
+        zg = 0
+        if self.warm:
+            _check(L.tt_warm_start_device(B, N, self.last.data_ptr(), self.have.data_ptr(), self.xref.data_ptr(),
+                                          self.uref.data_ptr(), int(self.bug_compatible), self.zg.data_ptr(), sp),
+                   "tt_warm_start_device")
+            zg = self.zg.data_ptr()
+        self.solver.solve_device(B, self.x_meas.data_ptr(), self.xref.data_ptr(), self.uref.data_ptr(),
+                                 self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(), self.it.data_ptr(),
+                                 self.kkt.data_ptr(), z_guess=zg, stream=s.cuda_stream)
+        if self.warm:
+            _check(L.tt_record_solution_device(B, N, self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(),
+                                               self.last.data_ptr(), self.have.data_ptr(), sp),
+                   "tt_record_solution_device")
+        plant_update(self.state, self.U, self.params, self.dist, self.st, self.zero_on_fail, self.u_applied, stream=s)
+        S, Ua, Ss, Si, Sc = logs
+        _check(L.tt_sim_log_advance_device(B, d_step.data_ptr(), self.state.data_ptr(), self.u_applied.data_ptr(),
+                                           self.st.data_ptr(), self.it.data_ptr(),
+                                           self.flag.data_ptr() if self.check_collision else None, S.data_ptr(),
+                                           Ua.data_ptr(), Ss.data_ptr(), Si.data_ptr(), Sc.data_ptr(), sp),
+               "tt_sim_log_advance_device")
+
+    def run_graph(self, x_init, T_sim, noise=None):
+        """run() with the per-step launches captured once into a hipGraph (torch.cuda.CUDAGraph on this
+        loop's stream) and replayed: step 0 runs eagerly (its collision check looks at the first window,
+        simulation.py:503-506), steps 1.. replay the captured step.  The step index, the reference's k
+        sequence and the measurement noise of every step are device-resident.  Not available with a switch
+        solver (its compaction needs the host).  Same logs as run()."""
+        if self.switch is not None:
+            raise ValueError("run_graph does not support the switch solver; use run()")
+        ks = step_indices(T_sim, float(self.params["dt"]))
+        self.reset(x_init)
+        B, K, d, s = self.B, len(ks), self.dev, self.stream
+        d_ks = torch.tensor(ks, dtype=torch.int32, device=d)
+        d_step = torch.zeros(1, dtype=torch.int32, device=d)
+        noise_all = None
+        if self.measurement_noise and self.dist is not None:
+            if noise is None:
+                noise_all = torch.randn((K, B, 6), generator=self.gen, dtype=torch.float64, device=d)
+                noise_all.mul_(float(self.dist.get("process_noise_std", 0.0)))
+            else:
+                noise_all = _dev(np.asarray(noise, dtype=np.float64).reshape(K, B, 6), d)
+        logs = (torch.empty((K + 1, B, 6), dtype=torch.float64, device=d),
+                torch.empty((K, B, 2), dtype=torch.float64, device=d),
+                torch.zeros((K, B), dtype=torch.int32, device=d), torch.zeros((K, B), dtype=torch.int32, device=d),
+                torch.zeros((K, B), dtype=torch.int32, device=d))
+        logs[0][0].copy_(self.state)
+        torch.cuda.synchronize(d)
+        with torch.cuda.stream(s):
+            self._graph_step(True, d_ks, d_step, noise_all, logs)
+        if K > 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._graph_step(False, d_ks, d_step, noise_all, logs)
+            with torch.cuda.stream(s):  # replay() launches on the current stream
+                for _ in range(K - 1):
+                    g.replay()
+        torch.cuda.synchronize(d)
+        self.first = False
+        S, Ua, Ss, Si, Sc = (t.cpu().numpy() for t in logs)
+        return {"k": np.array(ks), "states": S, "controls": Ua, "status": Ss, "iters": Si,
+                "collide": Sc.astype(bool), "success": Ss <= TT_ACCEPTABLE}
+
     def _switch_solve(self, s):
         """USE_SWITCH_MPC: instances whose check collided use MPCTrackingControlObs (simulation.py:506-512)."""
         idx = torch.nonzero(self.flag, as_tuple=True)[0]

@@ -131,6 +131,17 @@ typedef struct {
 int tt_sim_window_device(int B, int N, int k, int Np, const double* plan_x, const double* plan_u, int per_instance,
                          const double* state, const double* meas_noise, double* x_meas, double* xref, double* uref,
                          void* stream);
+/* Graph-replayable closed-loop step (hipGraph capture of window -> check -> solve -> plant -> log):
+ * the step index lives on the device.  tt_sim_window_indexed_device reads k = ks[*step] (the reference's
+ * step sequence, precomputed host-side) and the measurement noise noise_all[*step] ([K][B][6] or NULL);
+ * tt_sim_log_advance_device writes S[*step+1] = state [K+1][B][6], Ua[*step] = u_applied [K][B][2], the
+ * status / iterations / collision flag [K][B] (iters, flag may be NULL), then increments *step. */
+int tt_sim_window_indexed_device(int B, int N, const int* ks, const int* step, int Np, const double* plan_x,
+                                 const double* plan_u, int per_instance, const double* state, const double* noise_all,
+                                 double* x_meas, double* xref, double* uref, void* stream);
+int tt_sim_log_advance_device(int B, int* step, const double* state, const double* u_applied, const int* status,
+                              const int* iters, const int* flag, double* S, double* Ua, int* Ss, int* Si, int* Sc,
+                              void* stream);
 /* check_trajectory_collision (simulation.py:363-385) of K poses per instance, pose (b, j) at
  * poses + b*stride_b + j*stride_k (doubles; x, y, theta, psi first), against M axis-aligned obstacles
  * (device [M][4]: cx, cy, w, h).  flag[b] = 1 if any pose's truck or trailer touches an obstacle. */

@@ -245,3 +245,26 @@ def test_obca_plans_feed_tracking_batch_on_device(golden_ref):
     for b in range(B):
         S2, U2 = to.do_interpolation(X[b].T, Uu[b].T, 0.1, 0.05)
         assert np.array_equal(Xr.cpu().numpy()[b], S2.T) and np.array_equal(Ur.cpu().numpy()[b], U2.T)
+
+
+@pytest.mark.parametrize("warm", [False, True])
+def test_graph_replay_equals_eager_loop(plan, golden_ref, warm):
+    """run_graph (one captured step replayed through a hipGraph, step index on the device) reproduces the
+    eager run() bit for bit, disturbances, noise, collision checks and the NMPC warm start included."""
+    import ttmpc
+    from oracle import ttmpc_oracle as to
+    from ttmpc import simulation as sim
+    S, U = plan
+    N, B, T = 20, 32, 1.0
+    rng = np.random.default_rng(12)
+    x0 = S[:, 0][None] + rng.normal(scale=[0.3, 0.3, 0.02, 0.02, 0.0, 0.0], size=(B, 6))
+    K = len(to.step_indices(T, 0.05))
+    noise = rng.normal(scale=0.002, size=(K, B, 6))
+    variant = ttmpc.TT_VARIANT_NMPC if warm else ttmpc.TT_VARIANT_TRACK
+    mk = lambda: ttmpc.BatchSolver(N, P, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB,  # noqa: E731
+                                   to.MPC_UUB, variant=variant)
+    kw = dict(obstacles=golden_ref["obstacles"], warm_start=warm, zero_on_fail=warm)
+    eager = sim.ClosedLoop(mk(), S, U, P, sim.DISTURBANCE_PARAMS, **kw).run(x0, T, noise=noise)
+    graph = sim.ClosedLoop(mk(), S, U, P, sim.DISTURBANCE_PARAMS, **kw).run_graph(x0, T, noise=noise)
+    for key in ("states", "controls", "status", "iters", "collide"):
+        assert np.array_equal(eager[key], graph[key]), key
