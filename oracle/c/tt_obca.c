@@ -29,7 +29,8 @@
  * IPOPT's 1e-4 / x100 / x8 / /3 schedule).  Globalisation: IPOPT's filter line search with up to
  * four second-order corrections; where IPOPT would enter its restoration phase we take the
  * smallest tried step and reset the filter (only the iterate path can differ, not the KKT point).
- * IPOPT's gradient-based NLP scaling is not applied (documented in DESIGN.md).
+ * IPOPT's gradient-based NLP scaling is not applied: it is the identity at the bench workloads' starting
+ * points (all gradients < 100; DESIGN.md §1, tests/test_obca_oracle.py).
  */
 #include "tt_obca.h"
 
