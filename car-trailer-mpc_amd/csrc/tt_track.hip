@@ -919,8 +919,8 @@ __device__ __forceinline__ void phase_init(const Ctx<BM>& c) {
     __syncthreads();
 }
 
-template <int BM>
-__global__ __launch_bounds__(W) void track_kernel(TrackArgs a) {
+template <int BM, int OCC>
+__global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void track_kernel(TrackArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int b = blockIdx.x;
     const int N = a.N, S = N + 1;
@@ -1087,16 +1087,16 @@ int bound_mask(const TrackArgs& a) {
     return m;
 }
 
-template <int BM>
+template <int BM, int OCC = 1>
 hipError_t launch(const TrackArgs& a, hipStream_t stream) {
     const int bytes = lds_bytes(a.N);
     static int configured = 0;
     if (bytes > 64 * 1024 && configured < bytes) {
-        hipError_t e = hipFuncSetAttribute((const void*)track_kernel<BM>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+        hipError_t e = hipFuncSetAttribute((const void*)track_kernel<BM, OCC>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
         configured = bytes;
     }
-    hipLaunchKernelGGL(track_kernel<BM>, dim3(a.B), dim3(W), bytes, stream, a);
+    hipLaunchKernelGGL((track_kernel<BM, OCC>), dim3(a.B), dim3(W), bytes, stream, a);
     return hipGetLastError();
 }
 
@@ -1119,6 +1119,7 @@ bool diagonal_weights(const TrackArgs& a) {
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     const int m = bound_mask(a);
     const bool d = diagonal_weights(a);
+    if (m == kMaskMPC && d && a.B > 4096) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
     if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);
     return launch<-1>(a, stream);

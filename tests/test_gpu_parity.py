@@ -297,3 +297,18 @@ def test_c5_full_batch_through_the_sharded_path():
     sb.step()
     X2, U2, st2, _, _ = sb.results()
     assert np.array_equal(X, X2) and np.array_equal(U, U2) and np.array_equal(st, st2)
+
+
+def test_occupancy_build_is_bitwise_the_latency_build():
+    """Large batches (B > 4096, reference box, diagonal weights) launch the two-waves-per-SIMD build of
+    track_kernel; it runs the same instruction stream with a different register allocation, so every
+    instance must come out bit-identical to the same instance solved in a small (one-wave) batch."""
+    from ttmpc.scenarios import synthetic_batch
+    N, B = 20, 4608
+    x0, xr, ur = synthetic_batch(B, N, seed=77, psi_range=0.6)
+    s = _gpu_solver(N)
+    big = s.solve(x0, xr, ur)
+    for lo in range(0, B, 1152):
+        small = s.solve(x0[lo:lo + 1152], xr[lo:lo + 1152], ur[lo:lo + 1152])
+        for a, b in zip(big, small):
+            assert np.array_equal(a[lo:lo + 1152], b)
