@@ -30,6 +30,10 @@ struct Handle {
     double *d_x0 = nullptr, *d_xref = nullptr, *d_uref = nullptr, *d_w = nullptr, *d_zg = nullptr;
     double *d_xo = nullptr, *d_uo = nullptr, *d_kkt = nullptr;
     int *d_st = nullptr, *d_it = nullptr;
+    // tracking host calls: one packed device input / output block and its pinned host mirror, so a
+    // host-pointer solve is one H2D, the launch and one D2H (bytes)
+    size_t stage_in = 0, stage_out = 0;
+    char *d_sin = nullptr, *d_sout = nullptr, *h_sin = nullptr, *h_sout = nullptr;
     std::string err;
 };
 
@@ -61,6 +65,31 @@ void free_ws(Handle* h) {
     if (h->d_it) (void)hipFree(h->d_it);
     h->d_st = h->d_it = nullptr;
     h->cap = 0;
+}
+
+void free_stage(Handle* h) {
+    if (h->d_sin) (void)hipFree(h->d_sin);
+    if (h->d_sout) (void)hipFree(h->d_sout);
+    if (h->h_sin) (void)hipHostFree(h->h_sin);
+    if (h->h_sout) (void)hipHostFree(h->h_sout);
+    h->d_sin = h->d_sout = h->h_sin = h->h_sout = nullptr;
+    h->stage_in = h->stage_out = 0;
+}
+
+int ensure_stage(Handle* h, size_t in_bytes, size_t out_bytes) {
+    if (in_bytes <= h->stage_in && out_bytes <= h->stage_out) return 0;
+    free_stage(h);
+    hipError_t e = hipMalloc((void**)&h->d_sin, in_bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_sout, out_bytes);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sin, in_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sout, out_bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        free_stage(h);
+        return fail(h, -ENOMEM, "staging allocation failed (%s bytes)", std::to_string(in_bytes + out_bytes).c_str());
+    }
+    h->stage_in = in_bytes;
+    h->stage_out = out_bytes;
+    return 0;
 }
 
 bool is_obca(const tt_config& c) { return c.variant == TT_VARIANT_TRACK_OBCA || c.variant == TT_VARIANT_OBCA_PLAN; }
@@ -259,34 +288,52 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
     if (B < 0) return fail(h, -EINVAL, "B must be >= 0%s");
     if (B == 0) return 0;
     if (!x0 || !xref || !uref || !x_out || !u_out || !status) return fail(h, -EINVAL, "NULL host buffer%s");
+    if (h->cfg.variant == TT_VARIANT_OBCA_PLAN)
+        return fail(h, -EINVAL, "plan handles solve through tt_plan_batch / tt_obca_solve_batch%s");
+    if (is_obca(h->cfg))  // MPC+OBCA handle: its own host path (workspace, z_guess layout)
+        return tt_obca_solve_batch(handle, B, x0, nullptr, xref, uref, z_guess, x_out, u_out, nullptr, status, iters,
+                                   kkt_res);
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
-    int rc = ensure_ws(h, B);
+    // packed layout, instance-major within each array: in  = x0 | xref | uref | [wq_wr] | [z_guess]
+    //                                                   out = X | U | kkt | status, iters (int32)
+    const size_t N = h->cfg.N, b = (size_t)B, nz = 8 * N + 6;
+    const size_t sizes[5] = {b * 6, b * (N + 1) * 6, b * N * 2, wq_wr ? b * 8 : 0, z_guess ? b * nz : 0};
+    const double* srcs[5] = {x0, xref, uref, wq_wr, z_guess};
+    size_t in_d = 0;
+    for (size_t v : sizes) in_d += v;
+    const size_t nxo = b * (N + 1) * 6, nuo = b * N * 2, out_d = nxo + nuo + b + b;  // 2 x int32 per instance = 1 double
+    int rc = ensure_stage(h, in_d * 8, out_d * 8);
     if (rc) return rc;
-    const size_t N = h->cfg.N, nz = is_obca(h->cfg) ? ttmpc::obca_n(h->cfg.N, h->cfg.M) : 8 * N + 6, b = (size_t)B;
+    double* hin = reinterpret_cast<double*>(h->h_sin);
+    const double* dptr[5];
+    size_t off = 0;
+    for (int a = 0; a < 5; ++a) {
+        if (sizes[a]) memcpy(hin + off, srcs[a], sizes[a] * 8);
+        dptr[a] = reinterpret_cast<const double*>(h->d_sin) + off;
+        off += sizes[a];
+    }
     hipStream_t s = h->stream;
-#define H2D(d, hp, bytes) \
-    if (e == hipSuccess) e = hipMemcpyAsync((d), (hp), (bytes), hipMemcpyHostToDevice, s)
-#define D2H(hp, d, bytes) \
-    if (e == hipSuccess) e = hipMemcpyAsync((hp), (d), (bytes), hipMemcpyDeviceToHost, s)
-    H2D(h->d_x0, x0, b * 6 * 8);
-    H2D(h->d_xref, xref, b * (N + 1) * 6 * 8);
-    H2D(h->d_uref, uref, b * N * 2 * 8);
-    if (wq_wr) H2D(h->d_w, wq_wr, b * 8 * 8);
-    if (z_guess) H2D(h->d_zg, z_guess, b * nz * 8);
+    e = hipMemcpyAsync(h->d_sin, h->h_sin, in_d * 8, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(h, e, "H2D copy");
-    rc = tt_solve_batch_device(h, B, h->d_x0, h->d_xref, h->d_uref, wq_wr ? h->d_w : nullptr,
-                               z_guess ? h->d_zg : nullptr, h->d_xo, h->d_uo, h->d_st, h->d_it, h->d_kkt, s);
+    double* dxo = reinterpret_cast<double*>(h->d_sout);
+    double* duo = dxo + nxo;
+    double* dkk = duo + nuo;
+    int* dst = reinterpret_cast<int*>(dkk + b);
+    int* dit = dst + b;
+    rc = tt_solve_batch_device(h, B, dptr[0], dptr[1], dptr[2], wq_wr ? dptr[3] : nullptr,
+                               z_guess ? dptr[4] : nullptr, dxo, duo, dst, dit, dkk, s);
     if (rc) return rc;
-    D2H(x_out, h->d_xo, b * (N + 1) * 6 * 8);
-    D2H(u_out, h->d_uo, b * N * 2 * 8);
-    D2H(status, h->d_st, b * 4);
-    if (iters) D2H(iters, h->d_it, b * 4);
-    if (kkt_res) D2H(kkt_res, h->d_kkt, b * 8);
-#undef H2D
-#undef D2H
+    e = hipMemcpyAsync(h->h_sout, h->d_sout, out_d * 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(h, e, "solve");
+    const double* ho = reinterpret_cast<const double*>(h->h_sout);
+    memcpy(x_out, ho, nxo * 8);
+    memcpy(u_out, ho + nxo, nuo * 8);
+    if (kkt_res) memcpy(kkt_res, ho + nxo + nuo, b * 8);
+    const int* hi = reinterpret_cast<const int*>(ho + nxo + nuo + b);
+    memcpy(status, hi, b * 4);
+    if (iters) memcpy(iters, hi + b, b * 4);
     return 0;
 }
 
@@ -447,6 +494,7 @@ void tt_destroy(void* handle) {
     (void)hipSetDevice(h->device);
     free_ws(h);
     free_ows(h);
+    free_stage(h);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
