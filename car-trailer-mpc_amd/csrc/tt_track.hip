@@ -53,6 +53,7 @@ constexpr int hQW = 0, hRW = 36, hXI = 40, hLB = 46, hUB = 54;
 // dump: sink of branch-free predicated stores, one slot per lane pair (l, l+32: different LDS halves)
 constexpr int hDUMP = 64, hFTH = 96, hFPH = 112;  // filter entries (theta, phi), kTrackFilter each
 static_assert(hFTH + kTrackFilter == hFPH && hFPH + kTrackFilter <= 128, "filter fits the head");
+static_assert(HEAD >= SR, "stage -1 of the Riccati prefetch addresses head words");
 // (128..255: the P and transposed-PA tiles of the Riccati sweep, see phase_riccati)
 // rows
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
@@ -446,6 +447,7 @@ __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
 struct EpMap {
     int dj[6], di[6];
     int hs, ps;
+    int gj0, gj1, gi0, gi1;  // rows of g_u at the affine column / row (j or i = 6), the zero pad elsewhere
     double q2, dg;
     __device__ __forceinline__ static int dslot(int m, int n) {  // row of D[m][n] (PAD = 0)
         return (m < 6 && n < 6 && d_idx(m, n) >= 0) ? rAJ + d_idx(m, n) : (m < 6 && n == 6) ? rBH + m : PAD;
@@ -462,12 +464,16 @@ struct EpMap {
         q2 = (i < 6 && j < 6) ? 2.0 * QW[i * 6 + j] : 0.0;
         dg = (i == j && i < 6) ? 1.0 : 0.0;
         ps = (i <= j && j < 6) ? rPS + sym_idx(i, j) : (i < 6 && j == 6) ? rPV + i : -1;
+        gj0 = j == 6 ? rHG + 6 : PAD;
+        gj1 = j == 6 ? rHG + 7 : PAD;
+        gi0 = i == 6 ? rHG + 6 : PAD;
+        gi1 = i == 6 ? rHG + 7 : PAD;
     }
 };
 
 // stage operands (independent of P^_{k+1}): fetched one stage ahead so LDS latency hides
 struct EpOps {
-    double dj[6], di[6], h, sgu0, sgu1, gu0, gu1;
+    double dj[6], di[6], h, sgu0, sgu1, gj0, gj1, gi0, gi1;
 };
 template <int BM>
 __device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k, double dw) {
@@ -480,8 +486,10 @@ __device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k,
     o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
     o.sgu0 = c.r(rSG + 6, k);
     o.sgu1 = c.r(rSG + 7, k);
-    o.gu0 = c.r(rHG + 6, k);
-    o.gu1 = c.r(rHG + 7, k);
+    o.gj0 = c.r(m.gj0, k);
+    o.gj1 = c.r(m.gj1, k);
+    o.gi0 = c.r(m.gi0, k);
+    o.gi1 = c.r(m.gi1, k);
     return o;
 }
 
@@ -539,8 +547,8 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         fb = fma(o.di[5], c45.y, fb);
         const double F = fa + fb;
         // G[0][.] = dt PA[5][.] + S, G[1][.] = dt PA[4][.] + S;  M = H_uu^-1 G;  P^_k = F - G' M
-        const double g0j = fma(dt, c45.y, j == 6 ? o.gu0 : 0.0), g1j = fma(dt, c45.x, j == 6 ? o.gu1 : 0.0);
-        const double g0i = fma(dt, gi.y, i == 6 ? o.gu0 : 0.0), g1i = fma(dt, gi.x, i == 6 ? o.gu1 : 0.0);
+        const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
+        const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
         const double m0 = fma(i00, g0j, i01 * g1j), m1 = fma(i01, g0j, i11 * g1j);
         Pij = F - fma(g0i, m0, g1i * m1);
         PF[c.lane] = Pij;
@@ -555,7 +563,7 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     int k = N - 1;
     for (; k >= 1; k -= 2) {
         stage(k, oa, ob, k - 1);
-        stage(k - 1, ob, oa, k > 1 ? k - 2 : 0);
+        stage(k - 1, ob, oa, k - 2);  // k - 2 = -1 prefetches harmless head words (HEAD >= SR)
     }
     if (k == 0) stage(0, oa, ob, 0);
     __syncthreads();
