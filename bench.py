@@ -226,7 +226,7 @@ def main():
     traffic_src = None
     csvs = [p for p in args.traffic_csv.split(",") if p]
     if not csvs and args.config == "c2" and B == 1024 and N == 20:
-        csvs = [str(REPO / "profiles" / "r01" / "pmc_head" / f) for f in ("fetch_counter_collection.csv",
+        csvs = [str(REPO / "profiles" / "r01" / "final3" / f) for f in ("fetch_counter_collection.csv",
                                                                           "write_counter_collection.csv")]
     if csvs and all(Path(p).exists() for p in csvs):
         traffic = read_traffic(csvs)
