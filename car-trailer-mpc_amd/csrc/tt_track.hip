@@ -1135,7 +1135,10 @@ bool diagonal_weights(const TrackArgs& a) {
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     const int m = bound_mask(a);
     const bool d = diagonal_weights(a);
-    if (m == kMaskMPC && d && a.B > 4096) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
+    // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 23); at N = 40 the
+    // 52 KB per wave caps a CU at 3 and the occupancy build's spills are pure cost (C3 2.01 -> 2.14 ms).
+    const bool occ_room = 5 * lds_bytes(a.N) <= 160 * 1024;
+    if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
     if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);
