@@ -12,23 +12,36 @@
  *   plan  : J = sum_{k<N} u'Ru + (x-g)'Q(x-g) + (x_N-g)'(100Q)(x_N-g), |x_N - g| <= 1e-2  (168-183)
  *   track : J = sum_{k<N} (u-ur)'R(u-ur) + (x-xr)'Q(x-xr) + (x_N-xr_N)'Q(x_N-xr_N)   mpc_control_obs.py:31-41
  *
- * Algorithm: the same restatement of IPOPT's primal-dual barrier method as tt_oracle.c (IPOPT defaults
- * of trajectory_optimization.py:196-199: tol 1e-8, acceptable 1e-6 x 15, monotone mu from 0.1,
- * bound_relax_factor 1e-8 on variable AND constraint bounds, bound_push/frac 1e-2, kappa_sigma 1e10),
- * extended by IPOPT's slack formulation of inequality rows: d(x) - s = 0, d_L <= s <= d_U, with
- * multipliers y_d and slack-bound multipliers v_L, v_U.
+ * Algorithm: the reference calls IPOPT with its defaults (trajectory_optimization.py:195-205,
+ * mpc_control_obs.py:203-211); this file restates that algorithm:
+ *   * primal-dual barrier method in slack form (d(x) - s = 0, d_L <= s <= d_U, multipliers y_d and
+ *     slack-bound multipliers v_L, v_U): tol 1e-8, acceptable 1e-6 x 15, monotone mu from 0.1,
+ *     bound_relax_factor 1e-8 on variable AND constraint bounds, bound_push/frac 1e-2, kappa_sigma 1e10;
+ *   * initial constraint multipliers by least squares (constr_mult_init_max 1000: discarded if larger);
+ *   * inertia correction with IPOPT's delta_w schedule (1e-4 / x100 / x8 / /3, cap 1e20);
+ *   * filter line search (Waechter & Biegler 2006) with up to four second-order corrections;
+ *   * the soft restoration phase (soft_resto_pderror_reduction_factor 0.9999, max_soft_resto_iters 10);
+ *   * the feasibility restoration phase MinC_1Nrm: the restoration NLP
+ *         min rho sum(p + n) + zeta/2 ||D_R (xbar - xbar_R)||^2   s.t.  r(xbar, s) - p + n = 0,  p, n >= 0
+ *     over every constraint row r (dynamics, OBCA rows, final box) with rho 1000, zeta = sqrt(mu_R),
+ *     D_R = diag(min(1, 1/|xbar_R|)), mu_R = max(mu, ||r||_inf), p/n started at the closed-form barrier
+ *     minimiser; solved by the same barrier / filter machinery; left when the original infeasibility is
+ *     reduced to 0.9 of its value at entry and the point is acceptable to the (augmented) original
+ *     filter; bound multipliers then updated with the whole restoration change as one Newton step
+ *     (reset to 1 above 1000), constraint multipliers reset to 0 (constr_mult_reset_threshold 0).
+ *     A failed step computation activates the restoration phase (IPOPT's fallback mechanism); a failed
+ *     restoration line search resets p/n to the closed form (IPOPT's restoration of the restoration).
  *
  * Newton system (new-multiplier form, D = Sigma_s + delta_w):
  *   (W + Sigma_x + dw) dx + J_c' y_c+ + J_d' y_d+ = -grad phi_x
- *   D ds - y_d+ = -grad phi_s,  J_c dx = -c,  J_d dx - ds = -(d - s)
- * Slacks and y_d are eliminated (y_d+ = D (J_d dx + r_d), r_d = d - s + D^-1 grad phi_s); every OBCA block
- * (8 duals mu/lam, 4 rows) couples only to (X, Y, theta, psi) of its stage, so its 8x8 block
- * K = W_ww + Sigma_w + dw + Jw' D Jw is Cholesky-factorised and Schur-eliminated into the 6x6 stage
- * Hessian; the remaining stage-wise LQ problem is solved by a Riccati recursion.  Inertia test: every
- * K and every Riccati input block R~ + B'PB must be positive definite (otherwise dw is raised with
- * IPOPT's 1e-4 / x100 / x8 / /3 schedule).  Globalisation: IPOPT's filter line search with up to
- * four second-order corrections; where IPOPT would enter its restoration phase we take the
- * smallest tried step and reset the filter (only the iterate path can differ, not the KKT point).
+ *   D ds - y_d+ = -grad phi_s,  J_c dx - E_c y_c+ = -r_c,  J_d dx - ds - E_p y_d+ = -(d - s)
+ * (E = 0 outside the restoration phase; inside it the eliminated p/n give E = 1/D_p + 1/D_n per row.)
+ * Slacks and y_d are eliminated; every OBCA block (8 duals mu/lam, 4 rows) couples only to
+ * (X, Y, theta, psi) of its stage, so its 8x8 block K = W_ww + Sigma_w + dw + Jw' E^-1 Jw is
+ * Cholesky-factorised and Schur-eliminated into the 6x6 stage Hessian; the remaining stage-wise LQ
+ * problem is solved by a Riccati recursion (soft dynamics rows inside the restoration phase:
+ * P~ = P - P S M^-1 S P, M = I + S P S, S = E_c^1/2).  Inertia test: every K, every M and every Riccati
+ * input block R~ + B'P~B must be positive definite.
  * IPOPT's gradient-based NLP scaling is not applied: it is the identity at the bench workloads' starting
  * points (all gradients < 100; DESIGN.md §1, tests/test_obca_oracle.py).
  */
@@ -49,12 +62,27 @@
 #define NR 4
 #define RELAX 1e-8
 #define TTO_MAXF 64
+#define RHO 1000.0              /* resto_penalty_parameter */
+#define KAPPA_RESTO 0.9         /* required_infeasibility_reduction */
+#define BOUND_MULT_RESET 1000.0 /* bound_mult_reset_threshold */
+#define CONSTR_MULT_INIT_MAX 1000.0
+#define SOFT_RESTO_FACTOR 0.9999
+#define MAX_SOFT_RESTO 10
 
 static int isfree(double b) { return !isfinite(b) || fabs(b) >= 1e19; }
 
 typedef struct {
+    double th[TTO_MAXF], ph[TTO_MAXF];
+    int n;
+} filter_t;
+
+enum { M_ORIG = 0, M_RESTO = 1 };
+
+typedef struct {
     const tto_obca_problem* P;
     int N, M, nbk, nb, n, mode;
+    int R;          /* M_ORIG / M_RESTO: which NLP the Newton machinery assembles */
+    int lsq;        /* least-squares multiplier system: unit Hessian, gradients grad f - z */
     double Qc[36], Rc[4];
     double xl[6], xu[6], ul[2], uu[2];
     char hxl[6], hxu[6], hul[2], huu[2];
@@ -66,21 +94,36 @@ typedef struct {
     double *x, *u, *w, *s, *zLx, *zUx, *zLu, *zUu, *zw, *vL, *vU, *yc, *yd;
     double sf[6], vLf[6], vUf[6], ydf[6];
     /* linearisation */
-    double *A, *c, *d, *gx, *gu, *Wd, *Jx, *Jw, *Hxx, *Hxw, *Hww;
+    double *A, *c, *d, *gx, *gu, *gw, *Wd, *Jx, *Jw, *Hxx, *Hxw, *Hww;
     double df[6];
+    double *rc0, *rd0; /* residual rows at the iterate: c - (p - n), d - s - (p - n) */
+    double rf0[6];
     /* factorisation */
-    double *Dd, *L, *V, *Qt, *Rt, *Pm, *G, *H, *K;
-    double Df[6];
+    double *Dd, *Ed, *L, *V, *Qt, *Rt, *Pm, *G, *H, *K;
+    double Dsf[6], Dfe[6];
+    double *Sd, *Mch, *Ptl, *ptl; /* soft dynamics rows (restoration) */
     /* rhs + step */
-    double *qt, *rt, *vv, *rd, *pv, *kf, *Yb, *LT, *Gm, *tv;
+    double *qt, *rt, *vv, *rd, *pv, *kf, *Yb, *LT, *Gm, *tv, *rct;
     double rf[6];
     double *dx, *du, *dw, *ds, *ycp, *ydp, *dzLx, *dzUx, *dzLu, *dzUu, *dzw, *dvL, *dvU;
     double dsf[6], ydpf[6], dvLf[6], dvUf[6];
     /* trial + soc */
     double *xt, *ut, *wt, *st, *ct, *dtr, *cr, *dr;
-    double sft[6], dft[6], dfr[6];
-    double fth[TTO_MAXF], fph[TTO_MAXF];
-    int nf;
+    double sft[6], dft[6];
+    /* restoration phase: one elastic pair (p, n) per constraint row.  Row index: dynamics 6k+i,
+     * OBCA rows nrc + 4 bi + r, final rows nrc + nrd + i. */
+    int nrc, nrd, nrow;
+    double rho, zeta;
+    double *xR, *uR, *wR, *sR, sfR[6];
+    double *dRx, *dRu, *dRw;
+    double *pr, *nr, *zp, *zn, *dpr, *dnr, *dzp, *dzn, *prt, *nrt, *Dpr, *Dnr, *gpn;
+    /* original multipliers saved at entry into the restoration phase */
+    double *szLx, *szUx, *szLu, *szUu, *szw, *svL, *svU, svLf[6], svUf[6];
+    /* last acceptable iterate (IPOPT's stored acceptable point) */
+    double *xacc, *uacc, *wacc;
+    int have_acc;
+    /* soft restoration / SOC save area */
+    double* sv;
     double* mem;
 } ws_t;
 
@@ -251,39 +294,30 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     W->nbk = 2 * P->M;
     W->nb = (P->N + 1) * W->nbk;
     W->n = P->N * (8 + 16 * P->M) + 6 + 16 * P->M;
-    const size_t N1 = (size_t)P->N + 1, N = (size_t)P->N, nb = (size_t)W->nb;
+    W->nrc = 6 * (P->N + 1);
+    W->nrd = 4 * W->nb;
+    W->nrow = W->nrc + W->nrd + (P->mode == TTO_OBCA_PLAN ? 6 : 0);
+    const size_t N1 = (size_t)P->N + 1, N = (size_t)P->N, nb = (size_t)W->nb, nr = (size_t)W->nrow;
+    const size_t nsv = N1 * 6 * 4 + N * 2 * 3 + nb * 8 * 2 + nb * 4 * 4 + 2 * nr + 64; /* soft-resto snapshot */
     size_t tot = 0;
-#define NEED(cnt) tot += (cnt)
-    /* count */
-    NEED(N1 * 6); NEED(N * 2); NEED(nb * 8); NEED(nb * 4);              /* x u w s */
-    NEED(N1 * 6 * 2); NEED(N * 2 * 2); NEED(nb * 8); NEED(nb * 4 * 2);  /* zLx zUx zLu zUu zw vL vU */
-    NEED(N1 * 6); NEED(nb * 4);                                          /* yc yd */
-    NEED(N * 36); NEED(N1 * 6); NEED(nb * 4); NEED(N1 * 6); NEED(N * 2); NEED(N * 36);  /* A c d gx gu Wd */
-    NEED(nb * 16); NEED(nb * 32); NEED(nb * 16); NEED(nb * 32); NEED(nb * 16);          /* Jx Jw Hxx Hxw Hww */
-    NEED(nb * 4); NEED(nb * 64); NEED(nb * 32); NEED(N1 * 36); NEED(N * 4);              /* Dd L V Qt Rt */
-    NEED(N1 * 36); NEED(N * 4); NEED(N * 12); NEED(N * 12);                              /* Pm G H K */
-    NEED(N1 * 6); NEED(N * 2); NEED(nb * 8); NEED(nb * 4); NEED(N1 * 6); NEED(N * 2);    /* qt rt vv rd pv kf */
-    NEED(N1 * 6); NEED(N * 2); NEED(nb * 8); NEED(nb * 4); NEED(N1 * 6); NEED(nb * 4);   /* dx du dw ds ycp ydp */
-    NEED(N1 * 6 * 2); NEED(N * 2 * 2); NEED(nb * 8); NEED(nb * 4 * 2);                   /* dz* dzw dvL dvU */
-    NEED(N1 * 6); NEED(N * 2); NEED(nb * 8); NEED(nb * 4); NEED(N1 * 6); NEED(nb * 4);   /* xt ut wt st ct dtr */
-    NEED(N1 * 6); NEED(nb * 4);                                                           /* cr dr */
-    NEED(nb * 32); NEED(nb * 16); NEED(nb * 16); NEED(nb * 4);                           /* Yb LT Gm tv */
-#undef NEED
-    W->mem = (double*)calloc(tot, sizeof(double));
-    if (!W->mem) return -1;
-    double* q = W->mem;
-#define TAKE(ptr, cnt) (ptr = q, q += (cnt))
+    double** slots[256];
+    size_t cnts[256];
+    int ns = 0;
+#define TAKE(ptr, cnt) (slots[ns] = &(ptr), cnts[ns] = (cnt), tot += (cnt), ++ns)
     TAKE(W->x, N1 * 6); TAKE(W->u, N * 2); TAKE(W->w, nb * 8); TAKE(W->s, nb * 4);
     TAKE(W->zLx, N1 * 6); TAKE(W->zUx, N1 * 6); TAKE(W->zLu, N * 2); TAKE(W->zUu, N * 2); TAKE(W->zw, nb * 8);
     TAKE(W->vL, nb * 4); TAKE(W->vU, nb * 4);
     TAKE(W->yc, N1 * 6); TAKE(W->yd, nb * 4);
     TAKE(W->A, N * 36); TAKE(W->c, N1 * 6); TAKE(W->d, nb * 4); TAKE(W->gx, N1 * 6); TAKE(W->gu, N * 2);
-    TAKE(W->Wd, N * 36);
+    TAKE(W->gw, nb * 8); TAKE(W->Wd, N * 36);
     TAKE(W->Jx, nb * 16); TAKE(W->Jw, nb * 32); TAKE(W->Hxx, nb * 16); TAKE(W->Hxw, nb * 32); TAKE(W->Hww, nb * 16);
-    TAKE(W->Dd, nb * 4); TAKE(W->L, nb * 64); TAKE(W->V, nb * 32); TAKE(W->Qt, N1 * 36); TAKE(W->Rt, N * 4);
+    TAKE(W->rc0, N1 * 6); TAKE(W->rd0, nb * 4);
+    TAKE(W->Dd, nb * 4); TAKE(W->Ed, nb * 4); TAKE(W->L, nb * 64); TAKE(W->V, nb * 32); TAKE(W->Qt, N1 * 36);
+    TAKE(W->Rt, N * 4);
     TAKE(W->Pm, N1 * 36); TAKE(W->G, N * 4); TAKE(W->H, N * 12); TAKE(W->K, N * 12);
+    TAKE(W->Sd, N1 * 6); TAKE(W->Mch, N1 * 36); TAKE(W->Ptl, N1 * 36); TAKE(W->ptl, N1 * 6);
     TAKE(W->qt, N1 * 6); TAKE(W->rt, N * 2); TAKE(W->vv, nb * 8); TAKE(W->rd, nb * 4); TAKE(W->pv, N1 * 6);
-    TAKE(W->kf, N * 2);
+    TAKE(W->kf, N * 2); TAKE(W->rct, N1 * 6);
     TAKE(W->dx, N1 * 6); TAKE(W->du, N * 2); TAKE(W->dw, nb * 8); TAKE(W->ds, nb * 4); TAKE(W->ycp, N1 * 6);
     TAKE(W->ydp, nb * 4);
     TAKE(W->dzLx, N1 * 6); TAKE(W->dzUx, N1 * 6); TAKE(W->dzLu, N * 2); TAKE(W->dzUu, N * 2); TAKE(W->dzw, nb * 8);
@@ -292,7 +326,20 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->dtr, nb * 4);
     TAKE(W->cr, N1 * 6); TAKE(W->dr, nb * 4);
     TAKE(W->Yb, nb * 32); TAKE(W->LT, nb * 16); TAKE(W->Gm, nb * 16); TAKE(W->tv, nb * 4);
+    TAKE(W->xR, N1 * 6); TAKE(W->uR, N * 2); TAKE(W->wR, nb * 8); TAKE(W->sR, nb * 4);
+    TAKE(W->dRx, N1 * 6); TAKE(W->dRu, N * 2); TAKE(W->dRw, nb * 8);
+    TAKE(W->pr, nr); TAKE(W->nr, nr); TAKE(W->zp, nr); TAKE(W->zn, nr); TAKE(W->dpr, nr); TAKE(W->dnr, nr);
+    TAKE(W->dzp, nr); TAKE(W->dzn, nr); TAKE(W->prt, nr); TAKE(W->nrt, nr); TAKE(W->Dpr, nr); TAKE(W->Dnr, nr);
+    TAKE(W->gpn, nr);
+    TAKE(W->szLx, N1 * 6); TAKE(W->szUx, N1 * 6); TAKE(W->szLu, N * 2); TAKE(W->szUu, N * 2); TAKE(W->szw, nb * 8);
+    TAKE(W->svL, nb * 4); TAKE(W->svU, nb * 4);
+    TAKE(W->xacc, N1 * 6); TAKE(W->uacc, N * 2); TAKE(W->wacc, nb * 8);
+    TAKE(W->sv, 4 * (N1 * 6 + N * 2 + nb * 8 + nb * 4) + 2 * nr + nsv);
 #undef TAKE
+    W->mem = (double*)calloc(tot, sizeof(double));
+    if (!W->mem) return -1;
+    double* q = W->mem;
+    for (int i = 0; i < ns; ++i) { *slots[i] = q; q += cnts[i]; }
     return 0;
 }
 
@@ -317,8 +364,26 @@ static double cost_eval(const ws_t* W, const double* x, const double* u) {
     return F;
 }
 
-static void cost_grad(ws_t* W) {
+/* restoration objective rho sum(p + n) + zeta/2 ||D_R (xbar - xbar_R)||^2 */
+static double resto_obj(const ws_t* W, const double* x, const double* u, const double* w, const double* p,
+                        const double* n) {
+    double F = 0.0, Q = 0.0;
+    for (int i = 0; i < W->nrow; ++i) F += p[i] + n[i];
+    for (int i = 0; i < 6 * (W->N + 1); ++i) { const double e = x[i] - W->xR[i]; Q += W->dRx[i] * e * e; }
+    for (int i = 0; i < 2 * W->N; ++i) { const double e = u[i] - W->uR[i]; Q += W->dRu[i] * e * e; }
+    for (int i = 0; i < 8 * W->nb; ++i) { const double e = w[i] - W->wR[i]; Q += W->dRw[i] * e * e; }
+    return W->rho * F + 0.5 * W->zeta * Q;
+}
+
+static void obj_grad(ws_t* W) {
     const tto_obca_problem* P = W->P;
+    if (W->R == M_RESTO) {
+        for (int i = 0; i < 6 * (W->N + 1); ++i) W->gx[i] = W->zeta * W->dRx[i] * (W->x[i] - W->xR[i]);
+        for (int i = 0; i < 2 * W->N; ++i) W->gu[i] = W->zeta * W->dRu[i] * (W->u[i] - W->uR[i]);
+        for (int i = 0; i < 8 * W->nb; ++i) W->gw[i] = W->zeta * W->dRw[i] * (W->w[i] - W->wR[i]);
+        return;
+    }
+    memset(W->gw, 0, 8 * (size_t)W->nb * sizeof(double));
     for (int k = 0; k <= W->N; ++k) {
         const double* tgt = W->mode == TTO_OBCA_PLAN ? W->xgoal : W->xref + 6 * k;
         const double sc = (k == W->N && W->mode == TTO_OBCA_PLAN) ? P->tfac : 1.0;
@@ -356,9 +421,31 @@ static void obca_cons(const ws_t* W, const double* x, const double* w, double* d
         for (int i = 0; i < 6; ++i) df[i] = x[6 * W->N + i] - W->xgoal[i];
 }
 
-/* barrier value over every bounded component; returns 0 and sets *bad if any slack is <= 0 */
+/* residual rows r - (p - n) from raw values c, d, df and slacks s, sf (p, n NULL: original residuals) */
+static void residuals(const ws_t* W, const double* c, const double* d, const double* s, const double* df,
+                      const double* sf, const double* p, const double* n, double* rc, double* rd, double* rf) {
+    for (int i = 0; i < W->nrc; ++i) rc[i] = c[i] - (p ? p[i] - n[i] : 0.0);
+    for (int i = 0; i < W->nrd; ++i) rd[i] = d[i] - s[i] - (p ? p[W->nrc + i] - n[W->nrc + i] : 0.0);
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            const int ro = W->nrc + W->nrd + i;
+            rf[i] = df[i] - sf[i] - (p ? p[ro] - n[ro] : 0.0);
+        }
+}
+
+static double infeas1(const ws_t* W, const double* rc, const double* rd, const double* rf) {
+    double t = 0.0;
+    for (int i = 0; i < W->nrc; ++i) t += fabs(rc[i]);
+    for (int i = 0; i < W->nrd; ++i) t += fabs(rd[i]);
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) t += fabs(rf[i]);
+    return t;
+}
+
+/* barrier value over every bounded component (p, n: the restoration's elastic variables, or NULL);
+ * returns 0 and sets *bad if any slack is <= 0 */
 static double barrier(const ws_t* W, const double* x, const double* u, const double* w, const double* s,
-                      const double* sf, double mu, int* bad) {
+                      const double* sf, const double* p, const double* n, double mu, int* bad) {
     double b = 0.0;
     *bad = 0;
 #define BL(val, lo) do { double t_ = (val) - (lo); if (!(t_ > 0)) { *bad = 1; return 0; } b -= mu * log(t_); } while (0)
@@ -383,19 +470,11 @@ static double barrier(const ws_t* W, const double* x, const double* u, const dou
     }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) { BL(sf[i], W->fL); BU(sf[i], W->fU); }
+    if (p)
+        for (int i = 0; i < W->nrow; ++i) { BL(p[i], 0.0); BL(n[i], 0.0); }
 #undef BL
 #undef BU
     return b;
-}
-
-static double infeas1(const ws_t* W, const double* c, const double* d, const double* s, const double* df,
-                      const double* sf) {
-    double t = 0.0;
-    for (int i = 0; i < 6 * (W->N + 1); ++i) t += fabs(c[i]);
-    for (int i = 0; i < 4 * W->nb; ++i) t += fabs(d[i] - s[i]);
-    if (W->mode == TTO_OBCA_PLAN)
-        for (int i = 0; i < 6; ++i) t += fabs(df[i] - sf[i]);
-    return t;
 }
 
 /* ------------------------------------------------------------------ small dense helpers */
@@ -444,9 +523,11 @@ static double sig_u(const ws_t* W, int k, int i) {
     if (W->huu[i]) s += W->zUu[2 * k + i] / (W->uu[i] - v);
     return s;
 }
+/* gradient of the barrier objective; in the least-squares multiplier mode: grad f - z_L + z_U */
 static double bgrad_x(const ws_t* W, int k, int i, double mu) {
     const double v = W->x[6 * k + i];
     double g = W->gx[6 * k + i];
+    if (W->lsq) return g - (W->hxl[i] ? W->zLx[6 * k + i] : 0.0) + (W->hxu[i] ? W->zUx[6 * k + i] : 0.0);
     if (W->hxl[i]) g -= mu / (v - W->xl[i]);
     if (W->hxu[i]) g += mu / (W->xu[i] - v);
     return g;
@@ -454,15 +535,27 @@ static double bgrad_x(const ws_t* W, int k, int i, double mu) {
 static double bgrad_u(const ws_t* W, int k, int i, double mu) {
     const double v = W->u[2 * k + i];
     double g = W->gu[2 * k + i];
+    if (W->lsq) return g - (W->hul[i] ? W->zLu[2 * k + i] : 0.0) + (W->huu[i] ? W->zUu[2 * k + i] : 0.0);
     if (W->hul[i]) g -= mu / (v - W->ul[i]);
     if (W->huu[i]) g += mu / (W->uu[i] - v);
     return g;
 }
-static double bgrad_s(const ws_t* W, int r, double sv, double mu) {
+static double bgrad_w(const ws_t* W, int v, double mu) {
+    if (W->lsq) return W->gw[v] - W->zw[v];
+    return W->gw[v] - mu / (W->w[v] + RELAX);
+}
+static double bgrad_s(const ws_t* W, int bi, int r, double mu) {
+    const int v = 4 * bi + r;
+    if (W->lsq) return (W->hrL[r] ? -W->vL[v] : 0.0) + (W->hrU[r] ? W->vU[v] : 0.0);
+    const double sv = W->s[v];
     double g = 0.0;
     if (W->hrL[r]) g -= mu / (sv - W->rL[r]);
     if (W->hrU[r]) g += mu / (W->rU[r] - sv);
     return g;
+}
+static double bgrad_sf(const ws_t* W, int i, double mu) {
+    if (W->lsq) return -W->vLf[i] + W->vUf[i];
+    return -mu / (W->sf[i] - W->fL) + mu / (W->fU - W->sf[i]);
 }
 static double sig_s(const ws_t* W, int bi, int r) {
     const double sv = W->s[4 * bi + r];
@@ -472,10 +565,10 @@ static double sig_s(const ws_t* W, int bi, int r) {
     return s;
 }
 
-/* linearise at the current iterate (values, Jacobians, y-weighted Hessians) */
+/* linearise at the current iterate (values, Jacobians, y-weighted Hessians) + residual rows */
 static void linearise(ws_t* W) {
     const tto_obca_problem* P = W->P;
-    cost_grad(W);
+    obj_grad(W);
     dyn_cons(W, W->x, W->u, W->c);
     for (int k = 0; k < W->N; ++k) {
         jac_A(P, W->x + 6 * k, W->A + 36 * k);
@@ -490,24 +583,40 @@ static void linearise(ws_t* W) {
         }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) W->df[i] = W->x[6 * W->N + i] - W->xgoal[i];
+    const int rs = W->R == M_RESTO;
+    residuals(W, W->c, W->d, W->s, W->df, W->sf, rs ? W->pr : NULL, rs ? W->nr : NULL, W->rc0, W->rd0, W->rf0);
 }
 
 /* One OBCA block's elimination into its stage Hessian Q (6x6, rows/cols X,Y,theta,psi touched).
  * Local system in (dw, y+):  M = [[A, C'], [C, -E]],  A = W_ww + Sigma_w + dw (8x8), C = Jw (4x8),
- * E = D^-1 (D = Sigma_s + dw), coupled to dx^ by b1 = W_wx (8x4) and b2 = Jx (4x4).  With A = L L',
- * Y = L^-1 C', Z = L^-1 b1, T = E + Y'Y = L_T L_T', G = Y'Z - b2, the Schur complement onto dx^ is
+ * E = D^-1 (D = Sigma_s + dw; plus 1/D_p + 1/D_n in the restoration phase), coupled to dx^ by
+ * b1 = W_wx (8x4) and b2 = Jx (4x4).  With A = L L', Y = L^-1 C', Z = L^-1 b1, T = E + Y'Y = L_T L_T',
+ * G = Y'Z - b2, the Schur complement onto dx^ is
  *     W_xx - Z'Z + G' T^-1 G
  * which never forms C' D C: with D ~ 1e10 on the near-equality range rows that product cancels
  * catastrophically, while T stays well conditioned.  Inertia: A must be positive definite. */
 static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     const double *Jx = W->Jx + 16 * bi, *Jw = W->Jw + 32 * bi;
     double* D = W->Dd + 4 * bi;
-    for (int r = 0; r < 4; ++r) D[r] = sig_s(W, bi, r) + dw;
+    double* E = W->Ed + 4 * bi;
+    for (int r = 0; r < 4; ++r) {
+        D[r] = W->lsq ? 1.0 : sig_s(W, bi, r) + dw;
+        E[r] = 1.0 / D[r];
+        if (W->R == M_RESTO) {
+            const int ro = W->nrc + 4 * bi + r;
+            E[r] += 1.0 / W->Dpr[ro] + 1.0 / W->Dnr[ro];
+        }
+    }
     double* Lb = W->L + 64 * bi;
     memset(Lb, 0, 64 * sizeof(double));
-    for (int a = 0; a < 4; ++a)
-        for (int b = 0; b < 4; ++b) Lb[(4 + a) * 8 + 4 + b] = W->Hww[16 * bi + a * 4 + b];
-    for (int e = 0; e < 8; ++e) Lb[e * 8 + e] += W->zw[8 * bi + e] / (W->w[8 * bi + e] + RELAX) + dw;
+    if (!W->lsq)
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b) Lb[(4 + a) * 8 + 4 + b] = W->Hww[16 * bi + a * 4 + b];
+    for (int e = 0; e < 8; ++e) {
+        if (W->lsq) { Lb[e * 8 + e] = 1.0; continue; }
+        Lb[e * 8 + e] += W->zw[8 * bi + e] / (W->w[8 * bi + e] + RELAX) + dw;
+        if (W->R == M_RESTO) Lb[e * 8 + e] += W->zeta * W->dRw[8 * bi + e];
+    }
     if (chol(Lb, 8) != 0) return 1;
     double *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *LT = W->LT + 16 * bi, *Gm = W->Gm + 16 * bi;
     for (int r = 0; r < 4; ++r) {
@@ -518,13 +627,13 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     }
     for (int q = 0; q < 4; ++q) {
         double col[8];
-        for (int a = 0; a < 8; ++a) col[a] = W->Hxw[32 * bi + q * 8 + a];
+        for (int a = 0; a < 8; ++a) col[a] = W->lsq ? 0.0 : W->Hxw[32 * bi + q * 8 + a];
         fsub(Lb, 8, col);
         for (int a = 0; a < 8; ++a) Zb[a * 4 + q] = col[a];
     }
     for (int r = 0; r < 4; ++r)
         for (int c = 0; c < 4; ++c) {
-            double t = (r == c) ? 1.0 / D[r] : 0.0, g = -Jx[r * 4 + c];
+            double t = (r == c) ? E[r] : 0.0, g = -Jx[r * 4 + c];
             for (int a = 0; a < 8; ++a) { t += Yb[a * 4 + r] * Yb[a * 4 + c]; g += Yb[a * 4 + r] * Zb[a * 4 + c]; }
             LT[r * 4 + c] = t;
             Gm[r * 4 + c] = g;
@@ -540,12 +649,51 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     }
     for (int p = 0; p < 4; ++p)
         for (int q = 0; q < 4; ++q) {
-            double t = W->Hxx[16 * bi + p * 4 + q];
+            double t = W->lsq ? 0.0 : W->Hxx[16 * bi + p * 4 + q];
             for (int a = 0; a < 8; ++a) t -= Zb[a * 4 + p] * Zb[a * 4 + q];
             for (int r = 0; r < 4; ++r) t += Gm[r * 4 + p] * TG[r * 4 + q];
             Q[p * 6 + q] += t;
         }
     return 0;
+}
+
+/* soft dynamics rows (restoration): M_k = I + S P_k S (Cholesky into Mch), P~_k = P_k - P S M^-1 S P */
+static int soften(ws_t* W, int k) {
+    const double* Pk = W->Pm + 36 * k;
+    double* Pt = W->Ptl + 36 * k;
+    if (W->R != M_RESTO) { memcpy(Pt, Pk, 36 * sizeof(double)); return 0; }
+    const double* S = W->Sd + 6 * k;
+    double* Mk = W->Mch + 36 * k;
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) Mk[i * 6 + j] = (i == j ? 1.0 : 0.0) + S[i] * Pk[i * 6 + j] * S[j];
+    if (chol(Mk, 6) != 0) return 1;
+    /* X = M^-1 S P (column by column), P~ = P - (P S) X */
+    double X[36];
+    for (int j = 0; j < 6; ++j) {
+        double col[6];
+        for (int i = 0; i < 6; ++i) col[i] = S[i] * Pk[i * 6 + j];
+        fsub(Mk, 6, col);
+        bsub(Mk, 6, col);
+        for (int i = 0; i < 6; ++i) X[i * 6 + j] = col[i];
+    }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double t = Pk[i * 6 + j];
+            for (int l = 0; l < 6; ++l) t -= Pk[i * 6 + l] * S[l] * X[l * 6 + j];
+            Pt[i * 6 + j] = t;
+        }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < i; ++j) Pt[i * 6 + j] = Pt[j * 6 + i] = 0.5 * (Pt[i * 6 + j] + Pt[j * 6 + i]);
+    return 0;
+}
+/* v <- v - S M^-1 S b   (the soft-row correction applied to a vector) */
+static void soft_apply(const ws_t* W, int k, const double* b, double* v) {
+    const double* S = W->Sd + 6 * k;
+    double t[6];
+    for (int i = 0; i < 6; ++i) t[i] = S[i] * b[i];
+    fsub(W->Mch + 36 * k, 6, t);
+    bsub(W->Mch + 36 * k, 6, t);
+    for (int i = 0; i < 6; ++i) v[i] -= S[i] * t[i];
 }
 
 /* matrices: block eliminations, stage Hessians, Riccati factorisation.  0 = inertia ok */
@@ -554,41 +702,65 @@ static int factor(ws_t* W, double dw) {
     const int N = W->N;
     const double dt = P->dt;
     int fail = 0;
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            W->Dpr[i] = W->lsq ? 1.0 : W->zp[i] / W->pr[i] + dw;
+            W->Dnr[i] = W->lsq ? 1.0 : W->zn[i] / W->nr[i] + dw;
+        }
     for (int k = 0; k <= N; ++k) {
         double* Q = W->Qt + 36 * k;
         const double sc = (k == N && W->mode == TTO_OBCA_PLAN) ? P->tfac : 1.0;
-        for (int i = 0; i < 36; ++i) Q[i] = 2.0 * sc * W->Qc[i] + (k < N ? W->Wd[36 * k + i] : 0.0);
-        for (int i = 0; i < 6; ++i) Q[i * 6 + i] += sig_x(W, k, i) + dw;
+        if (W->lsq) {
+            for (int i = 0; i < 36; ++i) Q[i] = (i % 7 == 0) ? 1.0 : 0.0;
+        } else if (W->R == M_ORIG) {
+            for (int i = 0; i < 36; ++i) Q[i] = 2.0 * sc * W->Qc[i] + (k < N ? W->Wd[36 * k + i] : 0.0);
+            for (int i = 0; i < 6; ++i) Q[i * 6 + i] += sig_x(W, k, i) + dw;
+        } else {
+            for (int i = 0; i < 36; ++i) Q[i] = k < N ? W->Wd[36 * k + i] : 0.0;
+            for (int i = 0; i < 6; ++i) Q[i * 6 + i] += W->zeta * W->dRx[6 * k + i] + sig_x(W, k, i) + dw;
+        }
         for (int j = 0; j < W->nbk; ++j) {
             const int bi = k * W->nbk + j;
             if (block_factor(W, bi, dw, Q) != 0) fail = 1;
         }
         if (k == N && W->mode == TTO_OBCA_PLAN)
             for (int i = 0; i < 6; ++i) {
-                double s = dw;
-                s += W->vLf[i] / (W->sf[i] - W->fL) + W->vUf[i] / (W->fU - W->sf[i]);
-                W->Df[i] = s;
-                Q[i * 6 + i] += s;
+                double s = W->lsq ? 1.0 : dw + W->vLf[i] / (W->sf[i] - W->fL) + W->vUf[i] / (W->fU - W->sf[i]);
+                W->Dsf[i] = s;
+                double E = 1.0 / s;
+                if (W->R == M_RESTO) {
+                    const int ro = W->nrc + W->nrd + i;
+                    E += 1.0 / W->Dpr[ro] + 1.0 / W->Dnr[ro];
+                }
+                W->Dfe[i] = 1.0 / E;
+                Q[i * 6 + i] += W->Dfe[i];
             }
         if (k < N) {
             double* R = W->Rt + 4 * k;
-            for (int i = 0; i < 4; ++i) R[i] = 2.0 * W->Rc[i];
-            for (int i = 0; i < 2; ++i) R[i * 2 + i] += sig_u(W, k, i) + dw;
+            if (W->lsq) { R[0] = R[3] = 1.0; R[1] = R[2] = 0.0; continue; }
+            for (int i = 0; i < 4; ++i) R[i] = W->R == M_ORIG ? 2.0 * W->Rc[i] : 0.0;
+            for (int i = 0; i < 2; ++i)
+                R[i * 2 + i] += sig_u(W, k, i) + dw + (W->R == M_RESTO ? W->zeta * W->dRu[2 * k + i] : 0.0);
         }
     }
     if (fail) return 1;
-    /* Riccati: P_N = Q~_N; G = R~ + B'PB, H = B'PA, K = -G^-1 H, P = Q~ + A'PA + H'K */
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrc; ++i) W->Sd[i] = sqrt(1.0 / W->Dpr[i] + 1.0 / W->Dnr[i]);
+    /* Riccati: P_N = Q~_N; G = R~ + B'P~B, H = B'P~A, K = -G^-1 H, P = Q~ + A'P~A + H'K  (P~ = P unless the
+     * dynamics rows are soft) */
     memcpy(W->Pm + 36 * N, W->Qt + 36 * N, 36 * sizeof(double));
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Pn = W->Pm + 36 * (k + 1);
-        const double* A = W->A + 36 * k;
+    for (int k = N; k >= 1; --k) {
+        if (soften(W, k) != 0) return 1;
+        const double* Pn = W->Ptl + 36 * k;
+        const double* A = W->A + 36 * (k - 1);
+        const int kk = k - 1;
         /* B = dt [e5 e4]: rows of B'X = dt * (X row 5, X row 4) */
-        double* G = W->G + 4 * k;
-        G[0] = W->Rt[4 * k + 0] + dt * dt * Pn[5 * 6 + 5];
-        G[1] = W->Rt[4 * k + 1] + dt * dt * Pn[5 * 6 + 4];
-        G[2] = W->Rt[4 * k + 2] + dt * dt * Pn[4 * 6 + 5];
-        G[3] = W->Rt[4 * k + 3] + dt * dt * Pn[4 * 6 + 4];
-        double* H = W->H + 12 * k;
+        double* G = W->G + 4 * kk;
+        G[0] = W->Rt[4 * kk + 0] + dt * dt * Pn[5 * 6 + 5];
+        G[1] = W->Rt[4 * kk + 1] + dt * dt * Pn[5 * 6 + 4];
+        G[2] = W->Rt[4 * kk + 2] + dt * dt * Pn[4 * 6 + 5];
+        G[3] = W->Rt[4 * kk + 3] + dt * dt * Pn[4 * 6 + 4];
+        double* H = W->H + 12 * kk;
         for (int j = 0; j < 6; ++j) {
             double h0 = 0.0, h1 = 0.0;
             for (int i = 0; i < 6; ++i) { h0 += Pn[5 * 6 + i] * A[i * 6 + j]; h1 += Pn[4 * 6 + i] * A[i * 6 + j]; }
@@ -597,7 +769,7 @@ static int factor(ws_t* W, double dw) {
         }
         G[1] = G[2] = 0.5 * (G[1] + G[2]);
         if (chol(G, 2) != 0) return 1;
-        double* Kk = W->K + 12 * k;
+        double* Kk = W->K + 12 * kk;
         for (int j = 0; j < 6; ++j) {
             double col[2] = {H[j], H[6 + j]};
             fsub(G, 2, col);
@@ -605,7 +777,7 @@ static int factor(ws_t* W, double dw) {
             Kk[j] = -col[0];
             Kk[6 + j] = -col[1];
         }
-        double* Pk = W->Pm + 36 * k;
+        double* Pk = W->Pm + 36 * kk;
         double PA[36];
         for (int i = 0; i < 6; ++i)
             for (int j = 0; j < 6; ++j) {
@@ -615,7 +787,7 @@ static int factor(ws_t* W, double dw) {
             }
         for (int i = 0; i < 6; ++i)
             for (int j = 0; j < 6; ++j) {
-                double t = W->Qt[36 * k + i * 6 + j];
+                double t = W->Qt[36 * kk + i * 6 + j];
                 for (int l = 0; l < 6; ++l) t += A[l * 6 + i] * PA[l * 6 + j];
                 t += H[i] * Kk[j] + H[6 + i] * Kk[6 + j];
                 Pk[i * 6 + j] = t;
@@ -623,15 +795,25 @@ static int factor(ws_t* W, double dw) {
         for (int i = 0; i < 6; ++i)
             for (int j = 0; j < i; ++j) Pk[i * 6 + j] = Pk[j * 6 + i] = 0.5 * (Pk[i * 6 + j] + Pk[j * 6 + i]);
     }
+    if (soften(W, 0) != 0) return 1;
     return 0;
 }
 
-/* right-hand side + back-substitution.  cres: dynamics residual ((N+1)*6), dres: OBCA row residual d - s
- * (nb*4), fres: final row residual d_f - s_f (6).  Fills dx du dw ds ycp ydp dsf ydpf. */
+/* right-hand side + back-substitution.  cres: dynamics residual rows ((N+1)*6), dres: OBCA residual rows
+ * (nb*4), fres: final residual rows (6) -- all in the form r - (p - n) of the current system.
+ * Fills dx du dw ds ycp ydp dsf ydpf (and dp dn in the restoration phase). */
 static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres, const double* fres) {
     const tto_obca_problem* P = W->P;
     const int N = W->N;
     const double dt = P->dt;
+    const int rs = W->R == M_RESTO;
+    if (rs)
+        for (int i = 0; i < W->nrow; ++i) {
+            const double gp = W->rho - (W->lsq ? W->zp[i] : mu / W->pr[i]);
+            const double gn = W->rho - (W->lsq ? W->zn[i] : mu / W->nr[i]);
+            W->gpn[i] = gp / W->Dpr[i] - gn / W->Dnr[i];
+        }
+    for (int i = 0; i < W->nrc; ++i) W->rct[i] = cres[i] + (rs ? W->gpn[i] : 0.0);
     for (int k = 0; k <= N; ++k) {
         double* q = W->qt + 6 * k;
         for (int i = 0; i < 6; ++i) q[i] = bgrad_x(W, k, i, mu);
@@ -639,9 +821,10 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             const int bi = k * W->nbk + j;
             const double *D = W->Dd + 4 * bi, *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *Gm = W->Gm + 16 * bi;
             double* rd = W->rd + 4 * bi;
-            for (int r = 0; r < 4; ++r) rd[r] = dres[4 * bi + r] + bgrad_s(W, r, W->s[4 * bi + r], mu) / D[r];
+            for (int r = 0; r < 4; ++r)
+                rd[r] = dres[4 * bi + r] + bgrad_s(W, bi, r, mu) / D[r] + (rs ? W->gpn[W->nrc + 4 * bi + r] : 0.0);
             double* zf = W->vv + 8 * bi;
-            for (int a = 0; a < 8; ++a) zf[a] = -mu / (W->w[8 * bi + a] + RELAX);
+            for (int a = 0; a < 8; ++a) zf[a] = bgrad_w(W, 8 * bi + a, mu);
             fsub(W->L + 64 * bi, 8, zf);
             double* t = W->tv + 4 * bi;
             for (int r = 0; r < 4; ++r) {
@@ -660,43 +843,69 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
         }
         if (k == N && W->mode == TTO_OBCA_PLAN)
             for (int i = 0; i < 6; ++i) {
-                const double gs = -mu / (W->sf[i] - W->fL) + mu / (W->fU - W->sf[i]);
-                W->rf[i] = fres[i] + gs / W->Df[i];
-                q[i] += W->Df[i] * W->rf[i];
+                W->rf[i] = fres[i] + bgrad_sf(W, i, mu) / W->Dsf[i] + (rs ? W->gpn[W->nrc + W->nrd + i] : 0.0);
+                q[i] += W->Dfe[i] * W->rf[i];
             }
         if (k < N)
             for (int i = 0; i < 2; ++i) W->rt[2 * k + i] = bgrad_u(W, k, i, mu);
     }
-    /* Riccati vector pass */
+    /* Riccati vector pass (p~ = p - P S M^-1 S p for soft rows) */
     memcpy(W->pv + 6 * N, W->qt + 6 * N, 6 * sizeof(double));
-    for (int k = N - 1; k >= 0; --k) {
-        const double* Pn = W->Pm + 36 * (k + 1);
-        const double* pn = W->pv + 6 * (k + 1);
-        const double* A = W->A + 36 * k;
-        const double* e = cres + 6 * (k + 1);
+    for (int k = N;; --k) {
+        double* pt = W->ptl + 6 * k;
+        memcpy(pt, W->pv + 6 * k, 6 * sizeof(double));
+        if (rs) {
+            double Pp[6];
+            for (int i = 0; i < 6; ++i) Pp[i] = W->pv[6 * k + i];
+            /* pt -= P S M^-1 S p  */
+            const double* S = W->Sd + 6 * k;
+            double t[6];
+            for (int i = 0; i < 6; ++i) t[i] = S[i] * Pp[i];
+            fsub(W->Mch + 36 * k, 6, t);
+            bsub(W->Mch + 36 * k, 6, t);
+            for (int i = 0; i < 6; ++i) {
+                double a = 0.0;
+                for (int l = 0; l < 6; ++l) a += W->Pm[36 * k + i * 6 + l] * S[l] * t[l];
+                pt[i] -= a;
+            }
+        }
+        if (k == 0) break;
+        const int kk = k - 1;
+        const double* Pn = W->Ptl + 36 * k;
+        const double* A = W->A + 36 * kk;
+        const double* e = W->rct + 6 * k;
         double pp[6];
         for (int i = 0; i < 6; ++i) {
-            double t = pn[i];
+            double t = pt[i];
             for (int j = 0; j < 6; ++j) t -= Pn[i * 6 + j] * e[j];
             pp[i] = t;
         }
-        double g[2] = {W->rt[2 * k] + dt * pp[5], W->rt[2 * k + 1] + dt * pp[4]};
-        fsub(W->G + 4 * k, 2, g);
-        bsub(W->G + 4 * k, 2, g);
-        W->kf[2 * k] = -g[0];
-        W->kf[2 * k + 1] = -g[1];
-        const double* H = W->H + 12 * k;
+        double g[2] = {W->rt[2 * kk] + dt * pp[5], W->rt[2 * kk + 1] + dt * pp[4]};
+        fsub(W->G + 4 * kk, 2, g);
+        bsub(W->G + 4 * kk, 2, g);
+        W->kf[2 * kk] = -g[0];
+        W->kf[2 * kk + 1] = -g[1];
+        const double* H = W->H + 12 * kk;
         for (int i = 0; i < 6; ++i) {
-            double t = W->qt[6 * k + i];
+            double t = W->qt[6 * kk + i];
             for (int l = 0; l < 6; ++l) t += A[l * 6 + i] * pp[l];
-            t += H[i] * W->kf[2 * k] + H[6 + i] * W->kf[2 * k + 1];
-            W->pv[6 * k + i] = t;
+            t += H[i] * W->kf[2 * kk] + H[6 + i] * W->kf[2 * kk + 1];
+            W->pv[6 * kk + i] = t;
         }
     }
-    /* forward sweep */
-    for (int i = 0; i < 6; ++i) W->dx[i] = -cres[i];
+    /* forward sweep: yhat = A dx + B du - r~;  dx = yhat (hard rows) or yhat - S M^-1 S (P yhat + p) */
+    for (int i = 0; i < 6; ++i) W->dx[i] = -W->rct[i];
     for (int k = 0; k <= N; ++k) {
-        const double* dxk = W->dx + 6 * k;
+        double* dxk = W->dx + 6 * k;
+        if (rs) {
+            double b[6];
+            for (int i = 0; i < 6; ++i) {
+                double t = W->pv[6 * k + i];
+                for (int j = 0; j < 6; ++j) t += W->Pm[36 * k + i * 6 + j] * dxk[j];
+                b[i] = t;
+            }
+            soft_apply(W, k, b, dxk);
+        }
         for (int i = 0; i < 6; ++i) {
             double t = W->pv[6 * k + i];
             for (int j = 0; j < 6; ++j) t += W->Pm[36 * k + i * 6 + j] * dxk[j];
@@ -711,7 +920,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
         const double* A = W->A + 36 * k;
         double* dxn = W->dx + 6 * (k + 1);
         for (int i = 0; i < 6; ++i) {
-            double t = -cres[6 * (k + 1) + i];
+            double t = -W->rct[6 * (k + 1) + i];
             for (int j = 0; j < 6; ++j) t += A[i * 6 + j] * dxk[j];
             dxn[i] = t;
         }
@@ -743,81 +952,19 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             }
             bsub(W->L + 64 * bi, 8, t8);
             for (int a = 0; a < 8; ++a) W->dw[8 * bi + a] = -t8[a];
-            for (int r = 0; r < 4; ++r) W->ds[4 * bi + r] = (yp[r] - bgrad_s(W, r, W->s[4 * bi + r], mu)) / D[r];
+            for (int r = 0; r < 4; ++r) W->ds[4 * bi + r] = (yp[r] - bgrad_s(W, bi, r, mu)) / D[r];
         }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) {
-            const double gs = -mu / (W->sf[i] - W->fL) + mu / (W->fU - W->sf[i]);
-            W->ydpf[i] = W->Df[i] * (W->dx[6 * N + i] + W->rf[i]);
-            W->dsf[i] = (W->ydpf[i] - gs) / W->Df[i];
+            W->ydpf[i] = W->Dfe[i] * (W->dx[6 * N + i] + W->rf[i]);
+            W->dsf[i] = (W->ydpf[i] - bgrad_sf(W, i, mu)) / W->Dsf[i];
         }
-}
-
-/* TTO_CHECK diagnostic: residual of the un-condensed first Newton row block (primal stationarity) */
-static double check_newton(ws_t* W, double mu, double dwreg) {
-    const tto_obca_problem* P = W->P;
-    const int N = W->N;
-    double worst = 0.0, wx = 0.0, ww = 0.0, wr = 0.0, wu = 0.0;
-    for (int k = 0; k <= N; ++k) {
-        double r[6], rs[6];
-        for (int i = 0; i < 6; ++i) {
-            double t = bgrad_x(W, k, i, mu) + W->ycp[6 * k + i];
-            double sc = fabs(bgrad_x(W, k, i, mu)) + fabs(W->ycp[6 * k + i]);
-            const double tf = (k == N && W->mode == TTO_OBCA_PLAN) ? P->tfac : 1.0;
-            for (int j = 0; j < 6; ++j) {
-                const double e = (2.0 * tf * W->Qc[i * 6 + j] + (k < N ? W->Wd[36 * k + i * 6 + j] : 0.0)) * W->dx[6 * k + j];
-                t += e; sc += fabs(e);
-            }
-            t += (sig_x(W, k, i) + dwreg) * W->dx[6 * k + i];
-            sc += fabs((sig_x(W, k, i) + dwreg) * W->dx[6 * k + i]);
-            if (k < N)
-                for (int l = 0; l < 6; ++l) { t -= W->A[36 * k + l * 6 + i] * W->ycp[6 * (k + 1) + l]; sc += fabs(W->A[36 * k + l * 6 + i] * W->ycp[6 * (k + 1) + l]); }
-            if (k == N && W->mode == TTO_OBCA_PLAN) { t += W->ydpf[i]; sc += fabs(W->ydpf[i]); }
-            r[i] = t; rs[i] = sc;
+    if (rs) /* elastic variables: D_p dp - y+ = -(rho - mu/p),  D_n dn + y+ = -(rho - mu/n) */
+        for (int i = 0; i < W->nrow; ++i) {
+            const double yp = i < W->nrc ? W->ycp[i] : i < W->nrc + W->nrd ? W->ydp[i - W->nrc] : W->ydpf[i - W->nrc - W->nrd];
+            W->dpr[i] = (yp - (W->rho - mu / W->pr[i])) / W->Dpr[i];
+            W->dnr[i] = (-yp - (W->rho - mu / W->nr[i])) / W->Dnr[i];
         }
-        for (int j = 0; j < W->nbk; ++j) {
-            const int bi = k * W->nbk + j;
-            for (int q = 0; q < 4; ++q) {
-                double t = 0.0;
-                double sc = 0.0;
-                for (int p = 0; p < 4; ++p) { double e = W->Hxx[16 * bi + q * 4 + p] * W->dx[6 * k + p]; t += e; sc += fabs(e); }
-                for (int a = 0; a < 8; ++a) { double e = W->Hxw[32 * bi + q * 8 + a] * W->dw[8 * bi + a]; t += e; sc += fabs(e); }
-                for (int rr = 0; rr < 4; ++rr) { double e = W->Jx[16 * bi + rr * 4 + q] * W->ydp[4 * bi + rr]; t += e; sc += fabs(e); }
-                r[q] += t; rs[q] += sc;
-            }
-            /* w rows */
-            for (int a = 0; a < 8; ++a) {
-                double t1 = -mu / (W->w[8 * bi + a] + RELAX), t2 = (W->zw[8 * bi + a] / (W->w[8 * bi + a] + RELAX) + dwreg) * W->dw[8 * bi + a];
-                double t = t1 + t2, sc = fabs(t1) + fabs(t2);
-                for (int q = 0; q < 4; ++q) { double e = W->Hxw[32 * bi + q * 8 + a] * W->dx[6 * k + q]; t += e; sc += fabs(e); }
-                if (a >= 4)
-                    for (int b = 0; b < 4; ++b) { double e = W->Hww[16 * bi + (a - 4) * 4 + b] * W->dw[8 * bi + 4 + b]; t += e; sc += fabs(e); }
-                for (int rr = 0; rr < 4; ++rr) { double e = W->Jw[32 * bi + rr * 8 + a] * W->ydp[4 * bi + rr]; t += e; sc += fabs(e); }
-                ww = fmax(ww, fabs(t) / (sc + 1e-300));
-            }
-            /* linearised OBCA rows: J dx - ds + (d - s) */
-            for (int rr = 0; rr < 4; ++rr) {
-                double t = W->d[4 * bi + rr] - W->s[4 * bi + rr] - W->ds[4 * bi + rr];
-                double sc = fabs(W->d[4 * bi + rr]) + fabs(W->s[4 * bi + rr]) + fabs(W->ds[4 * bi + rr]);
-                for (int q = 0; q < 4; ++q) { double e = W->Jx[16 * bi + rr * 4 + q] * W->dx[6 * k + q]; t += e; sc += fabs(e); }
-                for (int a = 0; a < 8; ++a) { double e = W->Jw[32 * bi + rr * 8 + a] * W->dw[8 * bi + a]; t += e; sc += fabs(e); }
-                wr = fmax(wr, fabs(t) / (sc + 1e-300));
-            }
-        }
-        for (int i = 0; i < 6; ++i) wx = fmax(wx, fabs(r[i]) / (rs[i] + 1e-300));
-        if (k < N)
-            for (int i = 0; i < 2; ++i) {
-                double t = bgrad_u(W, k, i, mu) + (sig_u(W, k, i) + dwreg) * W->du[2 * k + i];
-                double sc = fabs(bgrad_u(W, k, i, mu)) + fabs((sig_u(W, k, i) + dwreg) * W->du[2 * k + i]);
-                for (int j = 0; j < 2; ++j) { t += 2.0 * W->Rc[i * 2 + j] * W->du[2 * k + j]; sc += fabs(2.0 * W->Rc[i * 2 + j] * W->du[2 * k + j]); }
-                t -= P->dt * W->ycp[6 * (k + 1) + (i == 0 ? 5 : 4)];
-                sc += fabs(P->dt * W->ycp[6 * (k + 1) + (i == 0 ? 5 : 4)]);
-                wu = fmax(wu, fabs(t) / (sc + 1e-300));
-            }
-    }
-    fprintf(stderr, "   check: x %.2e w %.2e rows %.2e u %.2e\n", wx, ww, wr, wu);
-    worst = fmax(fmax(wx, ww), fmax(wr, wu));
-    return worst;
 }
 
 /* ------------------------------------------------------------------ solver */
@@ -859,12 +1006,11 @@ static void default_guess(const ws_t* W, double* z) {
     }
 }
 
-/* Dual warm start: for body/obstacle pair j at pose x_k, pick the unit direction n among the 8 face
- * normals (obstacle +-e_x, +-e_y; body +-R e_x, +-R e_y) maximising the separation
+/* Dual warm start (opt-in, dual_init = 1): for body/obstacle pair j at pose x_k, pick the unit direction
+ * n among the 8 face normals (obstacle +-e_x, +-e_y; body +-R e_x, +-R e_y) maximising the separation
  * gap(n) = n'p - h_B(-R'n) - h_O(n), and set lam = 0.99 (n+_x, n+_y, n-_x, n-_y) (so A'lam = 0.99 n),
  * mu = 0.99 (m+_x, m+_y, m-_x, m-_y) with m = -R'n (so G'mu + R'A'lam = 0).  Then d2 = d3 = 0,
- * d4 = -0.01 and d1 = d_min - 0.99 gap(n): the OBCA rows are satisfied wherever the guess pose is
- * separated by more than d_min (the dual certificate of the reference's own constraint rows). */
+ * d4 = -0.01 and d1 = d_min - 0.99 gap(n). */
 static void dual_certificate(const tto_obca_problem* P, const double* xk, int j, double* wv) {
     geom_t g;
     body_geom(P, xk, j & 1, &g);
@@ -954,40 +1100,49 @@ static void mult_steps(ws_t* W, double mu) {
             W->dvLf[i] = mu / (W->sf[i] - W->fL) - W->vLf[i] - W->vLf[i] / (W->sf[i] - W->fL) * W->dsf[i];
             W->dvUf[i] = mu / (W->fU - W->sf[i]) - W->vUf[i] + W->vUf[i] / (W->fU - W->sf[i]) * W->dsf[i];
         }
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            W->dzp[i] = mu / W->pr[i] - W->zp[i] - W->zp[i] / W->pr[i] * W->dpr[i];
+            W->dzn[i] = mu / W->nr[i] - W->zn[i] - W->zn[i] / W->nr[i] * W->dnr[i];
+        }
 }
 
 #define FTB_P(val, lo, step, tau, a) do { if ((step) < 0) a = fmin(a, -(tau) * ((val) - (lo)) / (step)); } while (0)
 #define FTB_PU(val, hi, step, tau, a) do { if ((step) > 0) a = fmin(a, (tau) * ((hi) - (val)) / (step)); } while (0)
 #define FTB_D(zv, step, tau, a) do { if ((step) < 0) a = fmin(a, -(tau) * (zv) / (step)); } while (0)
 
-static double ftb_primal(const ws_t* W, const double* dx, const double* du, const double* dw, const double* ds,
-                         const double* dsf, double tau) {
+static double ftb_primal(const ws_t* W, double tau) {
     double a = 1.0;
     for (int k = 0; k <= W->N; ++k) {
         for (int i = 0; i < 6; ++i) {
             const int v = 6 * k + i;
-            if (W->hxl[i]) FTB_P(W->x[v], W->xl[i], dx[v], tau, a);
-            if (W->hxu[i]) FTB_PU(W->x[v], W->xu[i], dx[v], tau, a);
+            if (W->hxl[i]) FTB_P(W->x[v], W->xl[i], W->dx[v], tau, a);
+            if (W->hxu[i]) FTB_PU(W->x[v], W->xu[i], W->dx[v], tau, a);
         }
         if (k < W->N)
             for (int i = 0; i < 2; ++i) {
                 const int v = 2 * k + i;
-                if (W->hul[i]) FTB_P(W->u[v], W->ul[i], du[v], tau, a);
-                if (W->huu[i]) FTB_PU(W->u[v], W->uu[i], du[v], tau, a);
+                if (W->hul[i]) FTB_P(W->u[v], W->ul[i], W->du[v], tau, a);
+                if (W->huu[i]) FTB_PU(W->u[v], W->uu[i], W->du[v], tau, a);
             }
     }
     for (int bi = 0; bi < W->nb; ++bi) {
-        for (int e = 0; e < 8; ++e) FTB_P(W->w[8 * bi + e], -RELAX, dw[8 * bi + e], tau, a);
+        for (int e = 0; e < 8; ++e) FTB_P(W->w[8 * bi + e], -RELAX, W->dw[8 * bi + e], tau, a);
         for (int r = 0; r < 4; ++r) {
             const int v = 4 * bi + r;
-            if (W->hrL[r]) FTB_P(W->s[v], W->rL[r], ds[v], tau, a);
-            if (W->hrU[r]) FTB_PU(W->s[v], W->rU[r], ds[v], tau, a);
+            if (W->hrL[r]) FTB_P(W->s[v], W->rL[r], W->ds[v], tau, a);
+            if (W->hrU[r]) FTB_PU(W->s[v], W->rU[r], W->ds[v], tau, a);
         }
     }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) {
-            FTB_P(W->sf[i], W->fL, dsf[i], tau, a);
-            FTB_PU(W->sf[i], W->fU, dsf[i], tau, a);
+            FTB_P(W->sf[i], W->fL, W->dsf[i], tau, a);
+            FTB_PU(W->sf[i], W->fU, W->dsf[i], tau, a);
+        }
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            FTB_P(W->pr[i], 0.0, W->dpr[i], tau, a);
+            FTB_P(W->nr[i], 0.0, W->dnr[i], tau, a);
         }
     return a;
 }
@@ -1020,16 +1175,28 @@ static double ftb_dual(const ws_t* W, double tau) {
             FTB_D(W->vLf[i], W->dvLf[i], tau, a);
             FTB_D(W->vUf[i], W->dvUf[i], tau, a);
         }
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            FTB_D(W->zp[i], W->dzp[i], tau, a);
+            FTB_D(W->zn[i], W->dzn[i], tau, a);
+        }
     return a;
 }
 
-/* scaled optimality error at the current iterate (IPOPT eq. (5)); cmu = complementarity vs mu */
-static void opt_error(ws_t* W, double mu, double* E0, double* Emu, double* dinf_o, double* pinf_o, int* finite) {
+/* scaled optimality error at the current iterate (IPOPT eq. (5)) of the current system (original or
+ * restoration NLP); also the 1-norm primal-dual system error at mu (soft restoration test) */
+typedef struct { double E0, Emu, dinf, pinf, pderr; int finite; } opterr_t;
+
+static opterr_t opt_error(ws_t* W, double mu) {
     const tto_obca_problem* P = W->P;
     const int N = W->N;
-    double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0;
+    const int rs = W->R == M_RESTO;
+    double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0, d1 = 0.0, p1 = 0.0, cm1 = 0.0;
     long nb_ = 0, my = 0;
-    *finite = 1;
+    opterr_t o;
+    o.finite = 1;
+#define DINF(t) do { const double t_ = (t); dinf = fmax(dinf, fabs(t_)); d1 += fabs(t_); if (!isfinite(t_)) o.finite = 0; } while (0)
+#define CMPL(z, sl) do { const double z_ = (z), s_ = (sl); c0 = fmax(c0, fabs(z_ * s_)); cmu = fmax(cmu, fabs(z_ * s_ - mu)); cm1 += fabs(z_ * s_ - mu); sz += z_; ++nb_; } while (0)
     for (int k = 0; k <= N; ++k) {
         double gl[6];
         for (int i = 0; i < 6; ++i) {
@@ -1043,96 +1210,106 @@ static void opt_error(ws_t* W, double mu, double* E0, double* Emu, double* dinf_
             for (int q = 0; q < 4; ++q)
                 for (int r = 0; r < 4; ++r) gl[q] += W->Jx[16 * bi + r * 4 + q] * W->yd[4 * bi + r];
             for (int a = 0; a < 8; ++a) {
-                double t = -W->zw[8 * bi + a];
+                double t = W->gw[8 * bi + a] - W->zw[8 * bi + a];
                 for (int r = 0; r < 4; ++r) t += W->Jw[32 * bi + r * 8 + a] * W->yd[4 * bi + r];
-                dinf = fmax(dinf, fabs(t));
-                if (!isfinite(t)) *finite = 0;
-                const double sl = W->w[8 * bi + a] + RELAX, zz = W->zw[8 * bi + a];
-                c0 = fmax(c0, fabs(zz * sl)); cmu = fmax(cmu, fabs(zz * sl - mu)); sz += zz; ++nb_;
+                DINF(t);
+                CMPL(W->zw[8 * bi + a], W->w[8 * bi + a] + RELAX);
             }
             for (int r = 0; r < 4; ++r) {
                 const int v = 4 * bi + r;
-                const double t = -W->yd[v] - W->vL[v] + W->vU[v];
-                dinf = fmax(dinf, fabs(t));
-                pinf = fmax(pinf, fabs(W->d[v] - W->s[v]));
+                DINF(-W->yd[v] - W->vL[v] + W->vU[v]);
+                pinf = fmax(pinf, fabs(W->rd0[v]));
+                p1 += fabs(W->rd0[v]);
                 sy += fabs(W->yd[v]); ++my;
-                if (W->hrL[r]) { const double sl = W->s[v] - W->rL[r]; c0 = fmax(c0, fabs(W->vL[v] * sl)); cmu = fmax(cmu, fabs(W->vL[v] * sl - mu)); sz += W->vL[v]; ++nb_; }
-                if (W->hrU[r]) { const double sl = W->rU[r] - W->s[v]; c0 = fmax(c0, fabs(W->vU[v] * sl)); cmu = fmax(cmu, fabs(W->vU[v] * sl - mu)); sz += W->vU[v]; ++nb_; }
+                if (W->hrL[r]) CMPL(W->vL[v], W->s[v] - W->rL[r]);
+                if (W->hrU[r]) CMPL(W->vU[v], W->rU[r] - W->s[v]);
             }
         }
         for (int i = 0; i < 6; ++i) {
             const int v = 6 * k + i;
             gl[i] += -W->zLx[v] + W->zUx[v];
-            dinf = fmax(dinf, fabs(gl[i]));
-            if (!isfinite(gl[i])) *finite = 0;
-            if (W->hxl[i]) { const double sl = W->x[v] - W->xl[i]; c0 = fmax(c0, fabs(W->zLx[v] * sl)); cmu = fmax(cmu, fabs(W->zLx[v] * sl - mu)); sz += W->zLx[v]; ++nb_; }
-            if (W->hxu[i]) { const double sl = W->xu[i] - W->x[v]; c0 = fmax(c0, fabs(W->zUx[v] * sl)); cmu = fmax(cmu, fabs(W->zUx[v] * sl - mu)); sz += W->zUx[v]; ++nb_; }
-            pinf = fmax(pinf, fabs(W->c[v]));
+            DINF(gl[i]);
+            if (W->hxl[i]) CMPL(W->zLx[v], W->x[v] - W->xl[i]);
+            if (W->hxu[i]) CMPL(W->zUx[v], W->xu[i] - W->x[v]);
+            pinf = fmax(pinf, fabs(W->rc0[v]));
+            p1 += fabs(W->rc0[v]);
             sy += fabs(W->yc[v]); ++my;
         }
         if (k < N)
             for (int i = 0; i < 2; ++i) {
                 const int v = 2 * k + i;
-                double t = W->gu[v] - P->dt * W->yc[6 * (k + 1) + (i == 0 ? 5 : 4)] - W->zLu[v] + W->zUu[v];
-                dinf = fmax(dinf, fabs(t));
-                if (!isfinite(t)) *finite = 0;
-                if (W->hul[i]) { const double sl = W->u[v] - W->ul[i]; c0 = fmax(c0, fabs(W->zLu[v] * sl)); cmu = fmax(cmu, fabs(W->zLu[v] * sl - mu)); sz += W->zLu[v]; ++nb_; }
-                if (W->huu[i]) { const double sl = W->uu[i] - W->u[v]; c0 = fmax(c0, fabs(W->zUu[v] * sl)); cmu = fmax(cmu, fabs(W->zUu[v] * sl - mu)); sz += W->zUu[v]; ++nb_; }
+                DINF(W->gu[v] - P->dt * W->yc[6 * (k + 1) + (i == 0 ? 5 : 4)] - W->zLu[v] + W->zUu[v]);
+                if (W->hul[i]) CMPL(W->zLu[v], W->u[v] - W->ul[i]);
+                if (W->huu[i]) CMPL(W->zUu[v], W->uu[i] - W->u[v]);
             }
     }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) {
-            const double t = -W->ydf[i] - W->vLf[i] + W->vUf[i];
-            dinf = fmax(dinf, fabs(t));
-            pinf = fmax(pinf, fabs(W->df[i] - W->sf[i]));
+            DINF(-W->ydf[i] - W->vLf[i] + W->vUf[i]);
+            pinf = fmax(pinf, fabs(W->rf0[i]));
+            p1 += fabs(W->rf0[i]);
             sy += fabs(W->ydf[i]); ++my;
-            const double sl = W->sf[i] - W->fL, su = W->fU - W->sf[i];
-            c0 = fmax(c0, fmax(fabs(W->vLf[i] * sl), fabs(W->vUf[i] * su)));
-            cmu = fmax(cmu, fmax(fabs(W->vLf[i] * sl - mu), fabs(W->vUf[i] * su - mu)));
-            sz += W->vLf[i] + W->vUf[i];
-            nb_ += 2;
+            CMPL(W->vLf[i], W->sf[i] - W->fL);
+            CMPL(W->vUf[i], W->fU - W->sf[i]);
         }
-    if (!isfinite(pinf)) *finite = 0;
+    if (rs) /* elastic variables: rho - y - z_p = 0, rho + y - z_n = 0 */
+        for (int i = 0; i < W->nrow; ++i) {
+            const double y = i < W->nrc ? W->yc[i] : i < W->nrc + W->nrd ? W->yd[i - W->nrc] : W->ydf[i - W->nrc - W->nrd];
+            DINF(W->rho - y - W->zp[i]);
+            DINF(W->rho + y - W->zn[i]);
+            CMPL(W->zp[i], W->pr[i]);
+            CMPL(W->zn[i], W->nr[i]);
+        }
+#undef DINF
+#undef CMPL
+    if (!isfinite(pinf)) o.finite = 0;
     const double smax = 100.0;
     const double sd = fmax(smax, (sy + sz) / (double)(my + nb_)) / smax;
     const double sc = nb_ ? fmax(smax, sz / (double)nb_) / smax : 1.0;
-    *E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
-    *Emu = fmax(fmax(dinf / sd, pinf), cmu / sc);
-    if (dinf_o) *dinf_o = dinf;
-    if (pinf_o) *pinf_o = pinf;
+    o.E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
+    o.Emu = fmax(fmax(dinf / sd, pinf), cmu / sc);
+    o.dinf = dinf;
+    o.pinf = pinf;
+    o.pderr = d1 + p1 + cm1;
+    return o;
 }
 
-/* theta (l1 infeasibility) and barrier objective phi at the trial point (xt, ut, wt, st, sft) */
+/* trial point (xt, ut, wt, st, sft, prt, nrt) of the current system: theta (l1 norm of the residual rows,
+ * stored into ct / dtr / dft for second-order corrections) and the barrier objective phi */
 static void trial_eval(ws_t* W, double mu, double* th, double* ph) {
     int bad = 0;
-    const double b = barrier(W, W->xt, W->ut, W->wt, W->st, W->sft, mu, &bad);
+    const int rs = W->R == M_RESTO;
+    const double b = barrier(W, W->xt, W->ut, W->wt, W->st, W->sft, rs ? W->prt : NULL, rs ? W->nrt : NULL, mu, &bad);
     if (bad) { *th = INFINITY; *ph = INFINITY; return; }
+    /* raw values into the residual buffers, then subtract slacks / elastic variables in place */
     dyn_cons(W, W->xt, W->ut, W->ct);
-    obca_cons(W, W->xt, W->wt, W->dtr, W->dft);
-    *th = infeas1(W, W->ct, W->dtr, W->st, W->dft, W->sft);
-    *ph = cost_eval(W, W->xt, W->ut) + b;
+    double dfr[6] = {0};
+    obca_cons(W, W->xt, W->wt, W->dtr, dfr);
+    residuals(W, W->ct, W->dtr, W->st, dfr, W->sft, rs ? W->prt : NULL, rs ? W->nrt : NULL, W->ct, W->dtr, W->dft);
+    *th = infeas1(W, W->ct, W->dtr, W->dft);
+    *ph = (rs ? resto_obj(W, W->xt, W->ut, W->wt, W->prt, W->nrt) : cost_eval(W, W->xt, W->ut)) + b;
 }
 
-static int in_filter(const ws_t* W, double th, double ph) {
-    for (int i = 0; i < W->nf; ++i)
-        if (th >= W->fth[i] && ph >= W->fph[i]) return 1;
+static int in_filter(const filter_t* F, double th, double ph) {
+    for (int i = 0; i < F->n; ++i)
+        if (th >= F->th[i] && ph >= F->ph[i]) return 1;
     return 0;
 }
 
 /* add a filter entry; entries it dominates are dropped; when full the oldest is evicted */
-static void add_filter(ws_t* W, double th, double ph) {
+static void add_filter(filter_t* F, double th, double ph) {
     int j = 0;
-    for (int i = 0; i < W->nf; ++i)
-        if (!(W->fth[i] >= th && W->fph[i] >= ph)) { W->fth[j] = W->fth[i]; W->fph[j] = W->fph[i]; ++j; }
-    W->nf = j;
-    if (W->nf == TTO_MAXF) {
-        memmove(W->fth, W->fth + 1, (TTO_MAXF - 1) * sizeof(double));
-        memmove(W->fph, W->fph + 1, (TTO_MAXF - 1) * sizeof(double));
-        --W->nf;
+    for (int i = 0; i < F->n; ++i)
+        if (!(F->th[i] >= th && F->ph[i] >= ph)) { F->th[j] = F->th[i]; F->ph[j] = F->ph[i]; ++j; }
+    F->n = j;
+    if (F->n == TTO_MAXF) {
+        memmove(F->th, F->th + 1, (TTO_MAXF - 1) * sizeof(double));
+        memmove(F->ph, F->ph + 1, (TTO_MAXF - 1) * sizeof(double));
+        --F->n;
     }
-    W->fth[W->nf] = th;
-    W->fph[W->nf] = ph;
-    ++W->nf;
+    F->th[F->n] = th;
+    F->ph[F->n] = ph;
+    ++F->n;
 }
 
 static void clamp_mult(double* z, double sl, double mu) {
@@ -1140,12 +1317,555 @@ static void clamp_mult(double* z, double sl, double mu) {
     *z = fmax(fmin(*z, ks * mu / sl), mu / (ks * sl));
 }
 
+/* ------------------------------------------------------------------ iterate moves */
+static void set_trial(ws_t* W, double a) {
+    const size_t nx_ = 6 * (size_t)(W->N + 1), nu_ = 2 * (size_t)W->N, nw_ = 8 * (size_t)W->nb, ns_ = 4 * (size_t)W->nb;
+    for (size_t i = 0; i < nx_; ++i) W->xt[i] = W->x[i] + a * W->dx[i];
+    for (size_t i = 0; i < nu_; ++i) W->ut[i] = W->u[i] + a * W->du[i];
+    for (size_t i = 0; i < nw_; ++i) W->wt[i] = W->w[i] + a * W->dw[i];
+    for (size_t i = 0; i < ns_; ++i) W->st[i] = W->s[i] + a * W->ds[i];
+    for (int i = 0; i < 6; ++i) W->sft[i] = W->sf[i] + a * W->dsf[i];
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) { W->prt[i] = W->pr[i] + a * W->dpr[i]; W->nrt[i] = W->nr[i] + a * W->dnr[i]; }
+}
+
+/* accept the step: primal alpha, constraint multipliers alpha (new-multiplier form), bound multipliers az
+ * followed by the kappa_sigma safeguard */
+static void take_step(ws_t* W, double mu, double alpha, double az) {
+    const int N = W->N;
+    const size_t nx_ = 6 * (size_t)(N + 1), nu_ = 2 * (size_t)N, nw_ = 8 * (size_t)W->nb, ns_ = 4 * (size_t)W->nb;
+    for (size_t i = 0; i < nx_; ++i) W->x[i] += alpha * W->dx[i];
+    for (size_t i = 0; i < nu_; ++i) W->u[i] += alpha * W->du[i];
+    for (size_t i = 0; i < nw_; ++i) W->w[i] += alpha * W->dw[i];
+    for (size_t i = 0; i < ns_; ++i) W->s[i] += alpha * W->ds[i];
+    for (size_t i = 0; i < nx_; ++i) W->yc[i] += alpha * (W->ycp[i] - W->yc[i]);
+    for (size_t i = 0; i < ns_; ++i) W->yd[i] += alpha * (W->ydp[i] - W->yd[i]);
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            W->sf[i] += alpha * W->dsf[i];
+            W->ydf[i] += alpha * (W->ydpf[i] - W->ydf[i]);
+            W->vLf[i] += az * W->dvLf[i];
+            W->vUf[i] += az * W->dvUf[i];
+            clamp_mult(&W->vLf[i], W->sf[i] - W->fL, mu);
+            clamp_mult(&W->vUf[i], W->fU - W->sf[i], mu);
+        }
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < 6; ++i) {
+            const int v = 6 * k + i;
+            if (W->hxl[i]) { W->zLx[v] += az * W->dzLx[v]; clamp_mult(&W->zLx[v], W->x[v] - W->xl[i], mu); }
+            if (W->hxu[i]) { W->zUx[v] += az * W->dzUx[v]; clamp_mult(&W->zUx[v], W->xu[i] - W->x[v], mu); }
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) {
+                const int v = 2 * k + i;
+                if (W->hul[i]) { W->zLu[v] += az * W->dzLu[v]; clamp_mult(&W->zLu[v], W->u[v] - W->ul[i], mu); }
+                if (W->huu[i]) { W->zUu[v] += az * W->dzUu[v]; clamp_mult(&W->zUu[v], W->uu[i] - W->u[v], mu); }
+            }
+    }
+    for (int bi = 0; bi < W->nb; ++bi) {
+        for (int e = 0; e < 8; ++e) {
+            const int v = 8 * bi + e;
+            W->zw[v] += az * W->dzw[v];
+            clamp_mult(&W->zw[v], W->w[v] + RELAX, mu);
+        }
+        for (int r = 0; r < 4; ++r) {
+            const int v = 4 * bi + r;
+            if (W->hrL[r]) { W->vL[v] += az * W->dvL[v]; clamp_mult(&W->vL[v], W->s[v] - W->rL[r], mu); }
+            if (W->hrU[r]) { W->vU[v] += az * W->dvU[v]; clamp_mult(&W->vU[v], W->rU[r] - W->s[v], mu); }
+        }
+    }
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            W->pr[i] += alpha * W->dpr[i];
+            W->nr[i] += alpha * W->dnr[i];
+            W->zp[i] += az * W->dzp[i];
+            W->zn[i] += az * W->dzn[i];
+            clamp_mult(&W->zp[i], W->pr[i], mu);
+            clamp_mult(&W->zn[i], W->nr[i], mu);
+        }
+}
+
+/* full iterate snapshot (soft restoration trial), behind the second-order-correction save area */
+static void snapshot(ws_t* W, int restore) {
+    double* o = W->sv + 4 * (6 * ((size_t)W->N + 1) + 2 * (size_t)W->N + 8 * (size_t)W->nb + 4 * (size_t)W->nb) +
+                2 * (size_t)W->nrow;
+    const size_t N1 = (size_t)W->N + 1, N = (size_t)W->N, nb = (size_t)W->nb;
+#define SV(ptr, cnt) do { if (restore) memcpy(ptr, o, (cnt) * 8); else memcpy(o, ptr, (cnt) * 8); o += (cnt); } while (0)
+    SV(W->x, N1 * 6); SV(W->u, N * 2); SV(W->w, nb * 8); SV(W->s, nb * 4);
+    SV(W->zLx, N1 * 6); SV(W->zUx, N1 * 6); SV(W->zLu, N * 2); SV(W->zUu, N * 2); SV(W->zw, nb * 8);
+    SV(W->vL, nb * 4); SV(W->vU, nb * 4); SV(W->yc, N1 * 6); SV(W->yd, nb * 4);
+    SV(W->sf, 6); SV(W->vLf, 6); SV(W->vUf, 6); SV(W->ydf, 6);
+#undef SV
+}
+
+/* ------------------------------------------------------------------ restoration phase */
+/* closed-form minimiser of rho (p + n) - mu (ln p + ln n) subject to p - n = r  (IPOPT's p/n start) */
+static void pn_closed_form(double r, double mu, double rho, double* p, double* n) {
+    const double S = sqrt(mu * mu + rho * rho * r * r);
+    const double a = mu - rho * r, b = mu + rho * r;
+    *n = a >= 0.0 ? (a + S) / (2.0 * rho) : mu * r / (S - a);
+    *p = b >= 0.0 ? (b + S) / (2.0 * rho) : -mu * r / (S - b);
+}
+
+static double row_resid_max(const ws_t* W) {
+    double m = 0.0;
+    for (int i = 0; i < W->nrc; ++i) m = fmax(m, fabs(W->rc0[i]));
+    for (int i = 0; i < W->nrd; ++i) m = fmax(m, fabs(W->rd0[i]));
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) m = fmax(m, fabs(W->rf0[i]));
+    return m;
+}
+
+static void set_pn(ws_t* W, double muR) {
+    for (int i = 0; i < W->nrow; ++i) {
+        const double r = i < W->nrc ? W->c[i] : i < W->nrc + W->nrd ? W->d[i - W->nrc] - W->s[i - W->nrc]
+                                                                    : W->df[i - W->nrc - W->nrd] - W->sf[i - W->nrc - W->nrd];
+        pn_closed_form(r, muR, W->rho, &W->pr[i], &W->nr[i]);
+        W->zp[i] = muR / W->pr[i];
+        W->zn[i] = muR / W->nr[i];
+    }
+}
+
+/* enter the restoration phase at the current (linearised, original) iterate; returns mu_R */
+static double enter_resto(ws_t* W, double mu) {
+    const size_t N1 = (size_t)W->N + 1, N = (size_t)W->N, nb = (size_t)W->nb;
+    memcpy(W->xR, W->x, N1 * 6 * 8); memcpy(W->uR, W->u, N * 2 * 8); memcpy(W->wR, W->w, nb * 8 * 8);
+    memcpy(W->sR, W->s, nb * 4 * 8); memcpy(W->sfR, W->sf, 48);
+    memcpy(W->szLx, W->zLx, N1 * 6 * 8); memcpy(W->szUx, W->zUx, N1 * 6 * 8); memcpy(W->szLu, W->zLu, N * 2 * 8);
+    memcpy(W->szUu, W->zUu, N * 2 * 8); memcpy(W->szw, W->zw, nb * 8 * 8); memcpy(W->svL, W->vL, nb * 4 * 8);
+    memcpy(W->svU, W->vU, nb * 4 * 8); memcpy(W->svLf, W->vLf, 48); memcpy(W->svUf, W->vUf, 48);
+    for (size_t i = 0; i < N1 * 6; ++i) W->dRx[i] = fmin(1.0, 1.0 / fabs(W->x[i]));
+    for (size_t i = 0; i < N * 2; ++i) W->dRu[i] = fmin(1.0, 1.0 / fabs(W->u[i]));
+    for (size_t i = 0; i < nb * 8; ++i) W->dRw[i] = fmin(1.0, 1.0 / fabs(W->w[i]));
+    for (size_t i = 0; i < N1 * 6; ++i) W->dRx[i] *= W->dRx[i];
+    for (size_t i = 0; i < N * 2; ++i) W->dRu[i] *= W->dRu[i];
+    for (size_t i = 0; i < nb * 8; ++i) W->dRw[i] *= W->dRw[i];
+    const double muR = fmax(mu, row_resid_max(W));
+    W->rho = RHO;
+    W->zeta = sqrt(muR);
+    set_pn(W, muR);
+    /* bound multipliers of the shared variables: min(rho, z); constraint multipliers 0 */
+    for (size_t i = 0; i < N1 * 6; ++i) { W->zLx[i] = fmin(W->zLx[i], W->rho); W->zUx[i] = fmin(W->zUx[i], W->rho); }
+    for (size_t i = 0; i < N * 2; ++i) { W->zLu[i] = fmin(W->zLu[i], W->rho); W->zUu[i] = fmin(W->zUu[i], W->rho); }
+    for (size_t i = 0; i < nb * 8; ++i) W->zw[i] = fmin(W->zw[i], W->rho);
+    for (size_t i = 0; i < nb * 4; ++i) { W->vL[i] = fmin(W->vL[i], W->rho); W->vU[i] = fmin(W->vU[i], W->rho); }
+    for (int i = 0; i < 6; ++i) { W->vLf[i] = fmin(W->vLf[i], W->rho); W->vUf[i] = fmin(W->vUf[i], W->rho); }
+    memset(W->yc, 0, N1 * 6 * 8);
+    memset(W->yd, 0, nb * 4 * 8);
+    memset(W->ydf, 0, 48);
+    W->R = M_RESTO;
+    return muR;
+}
+
+/* leave the restoration phase: original bound multipliers updated by the complementarity Newton step of
+ * the whole restoration change (fraction to the boundary tau), reset to 1 when above 1000; constraint
+ * multipliers 0 */
+static void leave_resto(ws_t* W, double mu, double tau) {
+    const int N = W->N;
+    double a = 1.0, zmax = 0.0;
+#define DZL(z, sl0, d) (mu / (sl0) - (z) - (z) / (sl0) * (d))
+    /* pass 1: fraction to the boundary; pass 2: apply */
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int k = 0; k <= N; ++k) {
+            for (int i = 0; i < 6; ++i) {
+                const int v = 6 * k + i;
+                const double d = W->x[v] - W->xR[v];
+                if (W->hxl[i]) { const double dz = DZL(W->szLx[v], W->xR[v] - W->xl[i], d); if (!pass) FTB_D(W->szLx[v], dz, tau, a); else W->zLx[v] = W->szLx[v] + a * dz; }
+                if (W->hxu[i]) { const double dz = DZL(W->szUx[v], W->xu[i] - W->xR[v], -d); if (!pass) FTB_D(W->szUx[v], dz, tau, a); else W->zUx[v] = W->szUx[v] + a * dz; }
+            }
+            if (k < N)
+                for (int i = 0; i < 2; ++i) {
+                    const int v = 2 * k + i;
+                    const double d = W->u[v] - W->uR[v];
+                    if (W->hul[i]) { const double dz = DZL(W->szLu[v], W->uR[v] - W->ul[i], d); if (!pass) FTB_D(W->szLu[v], dz, tau, a); else W->zLu[v] = W->szLu[v] + a * dz; }
+                    if (W->huu[i]) { const double dz = DZL(W->szUu[v], W->uu[i] - W->uR[v], -d); if (!pass) FTB_D(W->szUu[v], dz, tau, a); else W->zUu[v] = W->szUu[v] + a * dz; }
+                }
+        }
+        for (int bi = 0; bi < W->nb; ++bi) {
+            for (int e = 0; e < 8; ++e) {
+                const int v = 8 * bi + e;
+                const double dz = DZL(W->szw[v], W->wR[v] + RELAX, W->w[v] - W->wR[v]);
+                if (!pass) FTB_D(W->szw[v], dz, tau, a); else W->zw[v] = W->szw[v] + a * dz;
+            }
+            for (int r = 0; r < 4; ++r) {
+                const int v = 4 * bi + r;
+                const double d = W->s[v] - W->sR[v];
+                if (W->hrL[r]) { const double dz = DZL(W->svL[v], W->sR[v] - W->rL[r], d); if (!pass) FTB_D(W->svL[v], dz, tau, a); else W->vL[v] = W->svL[v] + a * dz; }
+                if (W->hrU[r]) { const double dz = DZL(W->svU[v], W->rU[r] - W->sR[v], -d); if (!pass) FTB_D(W->svU[v], dz, tau, a); else W->vU[v] = W->svU[v] + a * dz; }
+            }
+        }
+        if (W->mode == TTO_OBCA_PLAN)
+            for (int i = 0; i < 6; ++i) {
+                const double d = W->sf[i] - W->sfR[i];
+                const double dl = DZL(W->svLf[i], W->sfR[i] - W->fL, d), du = DZL(W->svUf[i], W->fU - W->sfR[i], -d);
+                if (!pass) { FTB_D(W->svLf[i], dl, tau, a); FTB_D(W->svUf[i], du, tau, a); }
+                else { W->vLf[i] = W->svLf[i] + a * dl; W->vUf[i] = W->svUf[i] + a * du; }
+            }
+    }
+#undef DZL
+    /* kappa_sigma safeguard, then the reset test */
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < 6; ++i) {
+            const int v = 6 * k + i;
+            if (W->hxl[i]) { clamp_mult(&W->zLx[v], W->x[v] - W->xl[i], mu); zmax = fmax(zmax, W->zLx[v]); }
+            if (W->hxu[i]) { clamp_mult(&W->zUx[v], W->xu[i] - W->x[v], mu); zmax = fmax(zmax, W->zUx[v]); }
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) {
+                const int v = 2 * k + i;
+                if (W->hul[i]) { clamp_mult(&W->zLu[v], W->u[v] - W->ul[i], mu); zmax = fmax(zmax, W->zLu[v]); }
+                if (W->huu[i]) { clamp_mult(&W->zUu[v], W->uu[i] - W->u[v], mu); zmax = fmax(zmax, W->zUu[v]); }
+            }
+    }
+    for (int bi = 0; bi < W->nb; ++bi) {
+        for (int e = 0; e < 8; ++e) { clamp_mult(&W->zw[8 * bi + e], W->w[8 * bi + e] + RELAX, mu); zmax = fmax(zmax, W->zw[8 * bi + e]); }
+        for (int r = 0; r < 4; ++r) {
+            const int v = 4 * bi + r;
+            if (W->hrL[r]) { clamp_mult(&W->vL[v], W->s[v] - W->rL[r], mu); zmax = fmax(zmax, W->vL[v]); }
+            if (W->hrU[r]) { clamp_mult(&W->vU[v], W->rU[r] - W->s[v], mu); zmax = fmax(zmax, W->vU[v]); }
+        }
+    }
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            clamp_mult(&W->vLf[i], W->sf[i] - W->fL, mu);
+            clamp_mult(&W->vUf[i], W->fU - W->sf[i], mu);
+            zmax = fmax(zmax, fmax(W->vLf[i], W->vUf[i]));
+        }
+    if (zmax > BOUND_MULT_RESET) {
+        for (int k = 0; k <= N; ++k) {
+            for (int i = 0; i < 6; ++i) { W->zLx[6 * k + i] = W->hxl[i] ? 1.0 : 0.0; W->zUx[6 * k + i] = W->hxu[i] ? 1.0 : 0.0; }
+            if (k < N)
+                for (int i = 0; i < 2; ++i) { W->zLu[2 * k + i] = W->hul[i] ? 1.0 : 0.0; W->zUu[2 * k + i] = W->huu[i] ? 1.0 : 0.0; }
+        }
+        for (int bi = 0; bi < W->nb; ++bi) {
+            for (int e = 0; e < 8; ++e) W->zw[8 * bi + e] = 1.0;
+            for (int r = 0; r < 4; ++r) { W->vL[4 * bi + r] = W->hrL[r] ? 1.0 : 0.0; W->vU[4 * bi + r] = W->hrU[r] ? 1.0 : 0.0; }
+        }
+        for (int i = 0; i < 6; ++i) W->vLf[i] = W->vUf[i] = 1.0;
+    }
+    memset(W->yc, 0, 6 * ((size_t)N + 1) * 8);
+    memset(W->yd, 0, 4 * (size_t)W->nb * 8);
+    memset(W->ydf, 0, 48);
+    W->R = M_ORIG;
+}
+
+/* least-squares constraint multipliers at the starting point (IPOPT constr_mult_init_max):
+ * [[I, J'], [J, 0]] [d; y] = [-(grad f - z_L + z_U); 0], slack rows with unit Hessian */
+static void ls_multipliers(ws_t* W) {
+    const size_t N1 = (size_t)W->N + 1, nb = (size_t)W->nb;
+    W->lsq = 1;
+    linearise(W); /* y = 0: no curvature terms */
+    double zero6[6] = {0};
+    for (size_t i = 0; i < N1 * 6; ++i) W->cr[i] = 0.0;
+    for (size_t i = 0; i < nb * 4; ++i) W->dr[i] = 0.0;
+    int ok = factor(W, 0.0) == 0;
+    if (ok) {
+        solve_rhs(W, 0.0, W->cr, W->dr, zero6);
+        double m = 0.0;
+        for (size_t i = 0; i < N1 * 6; ++i) m = fmax(m, fabs(W->ycp[i]));
+        for (size_t i = 0; i < nb * 4; ++i) m = fmax(m, fabs(W->ydp[i]));
+        if (W->mode == TTO_OBCA_PLAN)
+            for (int i = 0; i < 6; ++i) m = fmax(m, fabs(W->ydpf[i]));
+        ok = isfinite(m) && m <= CONSTR_MULT_INIT_MAX;
+    }
+    if (ok) {
+        memcpy(W->yc, W->ycp, N1 * 6 * 8);
+        memcpy(W->yd, W->ydp, nb * 4 * 8);
+        memcpy(W->ydf, W->ydpf, 48);
+    }
+    W->lsq = 0;
+}
+
+/* ------------------------------------------------------------------ one barrier solve (original or restoration) */
+typedef struct {
+    double mu, tau, th_max, th_min, dw_last;
+    int acc_count;
+    filter_t F;
+} ipm_state_t;
+
+static void ipm_reset(ipm_state_t* S, double mu) {
+    S->mu = mu;
+    S->tau = fmax(0.99, 1.0 - mu);
+    S->th_max = S->th_min = 0.0;
+    S->dw_last = 0.0;
+    S->acc_count = 0;
+    S->F.n = 0;
+}
+
+static double dir_deriv(ws_t* W, double mu, double* rel_out) {
+    const int N = W->N;
+    double Dm = 0.0, rel = 0.0;
+    for (int k = 0; k <= N; ++k) {
+        for (int i = 0; i < 6; ++i) {
+            Dm += bgrad_x(W, k, i, mu) * W->dx[6 * k + i];
+            rel = fmax(rel, fabs(W->dx[6 * k + i]) / (1.0 + fabs(W->x[6 * k + i])));
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) {
+                Dm += bgrad_u(W, k, i, mu) * W->du[2 * k + i];
+                rel = fmax(rel, fabs(W->du[2 * k + i]) / (1.0 + fabs(W->u[2 * k + i])));
+            }
+    }
+    for (int bi = 0; bi < W->nb; ++bi) {
+        for (int e = 0; e < 8; ++e) {
+            Dm += bgrad_w(W, 8 * bi + e, mu) * W->dw[8 * bi + e];
+            rel = fmax(rel, fabs(W->dw[8 * bi + e]) / (1.0 + fabs(W->w[8 * bi + e])));
+        }
+        for (int r = 0; r < 4; ++r) {
+            Dm += bgrad_s(W, bi, r, mu) * W->ds[4 * bi + r];
+            rel = fmax(rel, fabs(W->ds[4 * bi + r]) / (1.0 + fabs(W->s[4 * bi + r])));
+        }
+    }
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            Dm += bgrad_sf(W, i, mu) * W->dsf[i];
+            rel = fmax(rel, fabs(W->dsf[i]) / (1.0 + fabs(W->sf[i])));
+        }
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            Dm += (W->rho - mu / W->pr[i]) * W->dpr[i] + (W->rho - mu / W->nr[i]) * W->dnr[i];
+            rel = fmax(rel, fmax(fabs(W->dpr[i]) / (1.0 + fabs(W->pr[i])), fabs(W->dnr[i]) / (1.0 + fabs(W->nr[i]))));
+        }
+    *rel_out = rel;
+    return Dm;
+}
+
+
+/* TTO_CHECK diagnostic: relative residuals of the un-condensed primal-dual Newton rows (x, u, w, s, p/n
+ * stationarity and the linearised constraint rows) for the step in dx du dw ds (dp dn) ycp ydp ydpf dsf */
+static void check_newton(ws_t* W, double mu, double dw) {
+    const tto_obca_problem* P = W->P;
+    const int N = W->N, rs = W->R == M_RESTO;
+    double wx = 0, wu = 0, ww = 0, wsl = 0, wpn = 0, wrow = 0;
+#define ACC(t_, sc_) do { t += (t_); sc += fabs(t_); } while (0)
+    for (int k = 0; k <= N; ++k) {
+        const double tf = (k == N && W->mode == TTO_OBCA_PLAN) ? P->tfac : 1.0;
+        for (int i = 0; i < 6; ++i) {
+            double t = 0, sc = 0;
+            ACC(bgrad_x(W, k, i, mu), 0);
+            for (int j = 0; j < 6; ++j) {
+                double h = (k < N ? W->Wd[36 * k + i * 6 + j] : 0.0);
+                if (!rs) h += 2.0 * tf * W->Qc[i * 6 + j];
+                ACC(h * W->dx[6 * k + j], 0);
+            }
+            ACC((sig_x(W, k, i) + dw + (rs ? W->zeta * W->dRx[6 * k + i] : 0.0)) * W->dx[6 * k + i], 0);
+            ACC(W->ycp[6 * k + i], 0);
+            if (k < N) for (int l = 0; l < 6; ++l) ACC(-W->A[36 * k + l * 6 + i] * W->ycp[6 * (k + 1) + l], 0);
+            if (k == N && W->mode == TTO_OBCA_PLAN) ACC(W->ydpf[i], 0);
+            if (i < 4)
+                for (int j = 0; j < W->nbk; ++j) {
+                    const int bi = k * W->nbk + j;
+                    for (int q = 0; q < 4; ++q) ACC(W->Hxx[16 * bi + i * 4 + q] * W->dx[6 * k + q], 0);
+                    for (int a = 0; a < 8; ++a) ACC(W->Hxw[32 * bi + i * 8 + a] * W->dw[8 * bi + a], 0);
+                    for (int r = 0; r < 4; ++r) ACC(W->Jx[16 * bi + r * 4 + i] * W->ydp[4 * bi + r], 0);
+                }
+            wx = fmax(wx, fabs(t) / (sc + 1e-300));
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) {
+                double t = 0, sc = 0;
+                ACC(bgrad_u(W, k, i, mu), 0);
+                if (!rs) for (int j = 0; j < 2; ++j) ACC(2.0 * W->Rc[i * 2 + j] * W->du[2 * k + j], 0);
+                ACC((sig_u(W, k, i) + dw + (rs ? W->zeta * W->dRu[2 * k + i] : 0.0)) * W->du[2 * k + i], 0);
+                ACC(-P->dt * W->ycp[6 * (k + 1) + (i == 0 ? 5 : 4)], 0);
+                wu = fmax(wu, fabs(t) / (sc + 1e-300));
+            }
+        for (int j = 0; j < W->nbk; ++j) {
+            const int bi = k * W->nbk + j;
+            for (int a = 0; a < 8; ++a) {
+                double t = 0, sc = 0;
+                ACC(bgrad_w(W, 8 * bi + a, mu), 0);
+                ACC((W->zw[8 * bi + a] / (W->w[8 * bi + a] + RELAX) + dw + (rs ? W->zeta * W->dRw[8 * bi + a] : 0.0)) * W->dw[8 * bi + a], 0);
+                for (int q = 0; q < 4; ++q) ACC(W->Hxw[32 * bi + q * 8 + a] * W->dx[6 * k + q], 0);
+                if (a >= 4) for (int b = 0; b < 4; ++b) ACC(W->Hww[16 * bi + (a - 4) * 4 + b] * W->dw[8 * bi + 4 + b], 0);
+                for (int r = 0; r < 4; ++r) ACC(W->Jw[32 * bi + r * 8 + a] * W->ydp[4 * bi + r], 0);
+                ww = fmax(ww, fabs(t) / (sc + 1e-300));
+            }
+            for (int r = 0; r < 4; ++r) {
+                const int v = 4 * bi + r, ro = W->nrc + v;
+                double t = 0, sc = 0;
+                ACC((sig_s(W, bi, r) + dw) * W->ds[v], 0);
+                ACC(-W->ydp[v], 0);
+                ACC(bgrad_s(W, bi, r, mu), 0);
+                wsl = fmax(wsl, fabs(t) / (sc + 1e-300));
+                t = 0; sc = 0;
+                ACC(W->rd0[v], 0);
+                for (int q = 0; q < 4; ++q) ACC(W->Jx[16 * bi + r * 4 + q] * W->dx[6 * k + q], 0);
+                for (int a = 0; a < 8; ++a) ACC(W->Jw[32 * bi + r * 8 + a] * W->dw[8 * bi + a], 0);
+                ACC(-W->ds[v], 0);
+                if (rs) { ACC(-W->dpr[ro], 0); ACC(W->dnr[ro], 0); }
+                wrow = fmax(wrow, fabs(t) / (sc + 1e-300));
+            }
+        }
+        for (int i = 0; i < 6; ++i) { /* dynamics rows */
+            double t = 0, sc = 0;
+            const int v = 6 * k + i;
+            ACC(W->rc0[v], 0);
+            ACC(W->dx[v], 0);
+            if (k > 0) {
+                for (int j = 0; j < 6; ++j) ACC(-W->A[36 * (k - 1) + i * 6 + j] * W->dx[6 * (k - 1) + j], 0);
+                if (i == 5) ACC(-P->dt * W->du[2 * (k - 1)], 0);
+                if (i == 4) ACC(-P->dt * W->du[2 * (k - 1) + 1], 0);
+            }
+            if (rs) { ACC(-W->dpr[v], 0); ACC(W->dnr[v], 0); }
+            wrow = fmax(wrow, fabs(t) / (sc + 1e-300));
+        }
+    }
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            const int ro = W->nrc + W->nrd + i;
+            double t = 0, sc = 0;
+            ACC(W->rf0[i], 0); ACC(W->dx[6 * N + i], 0); ACC(-W->dsf[i], 0);
+            if (rs) { ACC(-W->dpr[ro], 0); ACC(W->dnr[ro], 0); }
+            wrow = fmax(wrow, fabs(t) / (sc + 1e-300));
+            t = 0; sc = 0;
+            ACC((W->vLf[i] / (W->sf[i] - W->fL) + W->vUf[i] / (W->fU - W->sf[i]) + dw) * W->dsf[i], 0);
+            ACC(-W->ydpf[i], 0); ACC(bgrad_sf(W, i, mu), 0);
+            wsl = fmax(wsl, fabs(t) / (sc + 1e-300));
+        }
+    if (rs)
+        for (int i = 0; i < W->nrow; ++i) {
+            const double yp = i < W->nrc ? W->ycp[i] : i < W->nrc + W->nrd ? W->ydp[i - W->nrc] : W->ydpf[i - W->nrc - W->nrd];
+            double t = 0, sc = 0;
+            ACC((W->zp[i] / W->pr[i] + dw) * W->dpr[i], 0); ACC(-yp, 0); ACC(W->rho - mu / W->pr[i], 0);
+            wpn = fmax(wpn, fabs(t) / (sc + 1e-300));
+            t = 0; sc = 0;
+            ACC((W->zn[i] / W->nr[i] + dw) * W->dnr[i], 0); ACC(yp, 0); ACC(W->rho - mu / W->nr[i], 0);
+            wpn = fmax(wpn, fabs(t) / (sc + 1e-300));
+        }
+#undef ACC
+    fprintf(stderr, "   check(R=%d): x %.1e u %.1e w %.1e s %.1e pn %.1e rows %.1e\n", W->R, wx, wu, ww, wsl, wpn, wrow);
+}
+
+/* Newton step with inertia correction into dx..; 0 on success */
+static int newton(ws_t* W, ipm_state_t* S, double* dw_out) {
+    double dw = 0.0;
+    int ok = 0;
+    for (int attempt = 0; attempt < 40; ++attempt) {
+        if (factor(W, dw) == 0) { ok = 1; break; }
+        dw = (dw == 0.0) ? (S->dw_last == 0.0 ? 1e-4 : fmax(1e-20, S->dw_last / 3.0)) : (S->dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
+        if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
+    }
+    if (!ok) return 1;
+    if (dw > 0) S->dw_last = dw;
+    *dw_out = dw;
+    memcpy(W->cr, W->rc0, (size_t)W->nrc * 8);
+    memcpy(W->dr, W->rd0, (size_t)W->nrd * 8);
+    solve_rhs(W, S->mu, W->cr, W->dr, W->rf0);
+    if (getenv("TTO_CHECK")) check_newton(W, S->mu, dw);
+    mult_steps(W, S->mu);
+    return 0;
+}
+
+/* filter line search with second-order corrections on the current system.  Returns 1 (accepted, h-type
+ * adds a filter entry), 0 (line search failed); *alpha_out / *az_out the step sizes. */
+static int line_search(ws_t* W, ipm_state_t* S, int iter0, double th0, double phi0, double* alpha_out, double* az_out) {
+    const double mu = S->mu, tau = S->tau;
+    double ap = ftb_primal(W, tau), az = ftb_dual(W, tau), rel = 0.0;
+    const double Dm = dir_deriv(W, mu, &rel);
+    if (iter0 || !(S->th_max > 0)) { S->th_max = 1e4 * fmax(1.0, th0); S->th_min = 1e-4 * fmax(1.0, th0); }
+    const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
+    double amin;
+    if (Dm < 0.0) {
+        amin = fmin(g_th, g_ph * th0 / (-Dm));
+        if (th0 <= S->th_min) amin = fmin(amin, delta * pow(th0, s_th) / pow(-Dm, s_ph));
+    } else {
+        amin = g_th;
+    }
+    amin *= g_al;
+    const double tolc = 10.0 * DBL_EPSILON;
+    double alpha = ap;
+    int accepted = rel < 1e-15, ftype = 0;
+    const int rs = W->R == M_RESTO;
+    const size_t nx_ = 6 * (size_t)(W->N + 1), nu_ = 2 * (size_t)W->N, nw_ = 8 * (size_t)W->nb, ns_ = 4 * (size_t)W->nb;
+    const size_t nr_ = (size_t)W->nrow;
+    double tht = 0.0, pht = 0.0;
+    for (int ls = 0; !accepted; ++ls) {
+        set_trial(W, alpha);
+        trial_eval(W, mu, &tht, &pht);
+        const int sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
+        int ok = 0;
+        if (isfinite(pht) && tht <= S->th_max && !in_filter(&S->F, tht, pht)) {
+            if (th0 <= S->th_min && sw) { ftype = 1; ok = pht - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+            else { ftype = 0; ok = tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+        }
+        if (ok) { accepted = 1; break; }
+        if (ls == 0 && isfinite(pht) && tht >= th0) {
+            /* second-order corrections (IPOPT max_soc 4, kappa_soc 0.99) */
+            double* o = W->sv;
+            memcpy(o, W->dx, nx_ * 8); o += nx_; memcpy(o, W->du, nu_ * 8); o += nu_;
+            memcpy(o, W->dw, nw_ * 8); o += nw_; memcpy(o, W->ds, ns_ * 8); o += ns_;
+            memcpy(o, W->ycp, nx_ * 8); o += nx_; memcpy(o, W->ydp, ns_ * 8); o += ns_;
+            memcpy(o, W->dsf, 48); o += 6; memcpy(o, W->ydpf, 48); o += 6;
+            if (rs) { memcpy(o, W->dpr, nr_ * 8); o += nr_; memcpy(o, W->dnr, nr_ * 8); o += nr_; }
+            /* c_soc(0) = alpha r(x) + r(x + alpha d), c_soc(p+1) = a_soc(p) c_soc(p) + r(x + a_soc(p) d_soc(p)) */
+            double frs[6], a_soc = alpha, th_old = th0;
+            memcpy(W->cr, W->rc0, nx_ * 8);
+            memcpy(W->dr, W->rd0, ns_ * 8);
+            memcpy(frs, W->rf0, 48);
+            int soc_ok = 0;
+            for (int p = 0; p < 4; ++p) {
+                if (p > 0 && tht > 0.99 * th_old) break;
+                th_old = tht;
+                for (size_t i = 0; i < nx_; ++i) W->cr[i] = a_soc * W->cr[i] + W->ct[i];
+                for (size_t i = 0; i < ns_; ++i) W->dr[i] = a_soc * W->dr[i] + W->dtr[i];
+                if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = a_soc * frs[i] + W->dft[i];
+                solve_rhs(W, mu, W->cr, W->dr, frs);
+                a_soc = ftb_primal(W, tau);
+                set_trial(W, a_soc);
+                trial_eval(W, mu, &tht, &pht);
+                int ok2 = 0;
+                if (isfinite(pht) && tht <= S->th_max && !in_filter(&S->F, tht, pht)) {
+                    if (th0 <= S->th_min && sw) { ftype = 1; ok2 = pht - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+                    else { ftype = 0; ok2 = tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+                }
+                if (ok2) { soc_ok = 1; break; }
+                if (!isfinite(pht)) break;
+            }
+            if (soc_ok) {
+                accepted = 2;
+                alpha = a_soc;
+                mult_steps(W, mu);
+                az = ftb_dual(W, tau);
+                break;
+            }
+            o = W->sv;
+            memcpy(W->dx, o, nx_ * 8); o += nx_; memcpy(W->du, o, nu_ * 8); o += nu_;
+            memcpy(W->dw, o, nw_ * 8); o += nw_; memcpy(W->ds, o, ns_ * 8); o += ns_;
+            memcpy(W->ycp, o, nx_ * 8); o += nx_; memcpy(W->ydp, o, ns_ * 8); o += ns_;
+            memcpy(W->dsf, o, 48); o += 6; memcpy(W->ydpf, o, 48); o += 6;
+            if (rs) { memcpy(W->dpr, o, nr_ * 8); o += nr_; memcpy(W->dnr, o, nr_ * 8); o += nr_; }
+        }
+        if (alpha * 0.5 < amin) break;
+        alpha *= 0.5;
+    }
+    if (accepted && !ftype) add_filter(&S->F, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+    *alpha_out = alpha;
+    *az_out = az;
+    return accepted != 0;
+}
+
+/* original-problem theta / phi at the current iterate (also valid at a restoration iterate: the shared
+ * variables x, u, w, s, sf) */
+static void orig_th_phi(ws_t* W, double mu, double* th, double* ph) {
+    double rfo[6] = {0};
+    residuals(W, W->c, W->d, W->s, W->df, W->sf, NULL, NULL, W->cr, W->dr, rfo);
+    *th = infeas1(W, W->cr, W->dr, rfo);
+    int bad = 0;
+    const double b = barrier(W, W->x, W->u, W->w, W->s, W->sf, NULL, NULL, mu, &bad);
+    *ph = bad ? INFINITY : cost_eval(W, W->x, W->u) + b;
+}
+
 static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const double* xref, const double* uref,
                      const double* zg, double* zout, int* iters_out, double* kkt_out) {
     const tto_obca_problem* P = W->P;
     const int N = W->N;
     W->xinit = xinit; W->xgoal = xgoal; W->xref = xref; W->uref = uref;
-    const int dbg = getenv("TTO_DEBUG") != NULL, chk = getenv("TTO_CHECK") != NULL;
+    W->R = M_ORIG;
+    W->lsq = 0;
+    W->have_acc = 0;
+    const int dbg = getenv("TTO_DEBUG") != NULL;
+    const int use_resto = !(P->opts & TTO_OPT_NO_RESTO), use_soft = !(P->opts & TTO_OPT_NO_SOFT_RESTO);
     /* weights, bounds (bound_relax_factor 1e-8 on every finite bound) */
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) W->Qc[i * 6 + j] = 0.5 * (P->Q[i * 6 + j] + P->Q[j * 6 + i]);
@@ -1185,7 +1905,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         if (kkt_out) *kkt_out = INFINITY;
         return 3;
     }
-    /* bound push of the primal guess, slacks = d(x0) pushed, multipliers 1 / 0 */
+    /* bound push of the primal guess, slacks = d(x0) pushed, bound multipliers 1, constraint multipliers by
+     * least squares */
     for (int k = 0; k <= N; ++k) {
         for (int i = 0; i < 6; ++i) push_into(&W->x[6 * k + i], W->xl[i], W->xu[i], W->hxl[i], W->hxu[i]);
         if (k < N)
@@ -1221,229 +1942,167 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
                 W->zUu[2 * k + i] = W->huu[i] ? 1.0 : 0.0;
             }
     }
-    double mu = 0.1, tau = fmax(0.99, 1.0 - mu), dw_last = 0.0, th_max = 0.0, th_min = 0.0;
-    int acc_count = 0, n_fallback = 0;
-    W->nf = 0;
-    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+    if (!(P->opts & TTO_OPT_NO_LSQ_MULT)) ls_multipliers(W);
 
+    ipm_state_t SO, SR;
+    ipm_reset(&SO, 0.1);
+    ipm_reset(&SR, 0.1);
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+    int in_soft = 0, soft_cnt = 0, first_resto = 0, n_resto = 0, n_soft = 0, fallback = 0, resto_iter0 = 0;
+    double th_resto0 = 0.0;
     for (iter = 0;; ++iter) {
+        ipm_state_t* S = W->R == M_RESTO ? &SR : &SO;
         linearise(W);
-        double Emu, dinf, pinf;
-        int finite;
-        opt_error(W, mu, &E0, &Emu, &dinf, &pinf, &finite);
-        if (!finite) { status = 4; break; }
-        if (dbg) fprintf(stderr, "it %4d E0 %.3e dinf %.3e pinf %.3e mu %.2e f %.6e\n", iter, E0, dinf, pinf, mu,
-                         cost_eval(W, W->x, W->u));
-        if (E0 <= P->tol) { status = 0; break; }
-        if (E0 <= P->acc_tol) {
-            if (++acc_count >= P->acc_iter) { status = 1; break; }
-        } else {
-            acc_count = 0;
-        }
-        if (iter >= P->max_iter) { status = E0 <= P->acc_tol ? 1 : 2; break; }
-        while (Emu <= kappa_eps * mu && mu > P->tol / 10.0 * 1.0000001) {
-            mu = fmax(P->tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
-            tau = fmax(0.99, 1.0 - mu);
-            W->nf = 0; /* IPOPT resets the filter on every barrier update */
-            opt_error(W, mu, &E0, &Emu, &dinf, &pinf, &finite);
-        }
-        /* Newton step with inertia correction */
-        double dw = 0.0;
-        int ok = 0;
-        for (int attempt = 0; attempt < 40; ++attempt) {
-            if (factor(W, dw) == 0) { ok = 1; break; }
-            dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-            if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
-        }
-        if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
-        if (dw > 0) dw_last = dw;
-        for (int i = 0; i < 4 * W->nb; ++i) W->dr[i] = W->d[i] - W->s[i];
-        double fr[6] = {0};
-        if (W->mode == TTO_OBCA_PLAN)
-            for (int i = 0; i < 6; ++i) fr[i] = W->df[i] - W->sf[i];
-        solve_rhs(W, mu, W->c, W->dr, fr);
-        if (chk) fprintf(stderr, "   newton residual %.3e (dw %.2e)\n", check_newton(W, mu, dw), dw);
-        mult_steps(W, mu);
-        double ap = ftb_primal(W, W->dx, W->du, W->dw, W->ds, W->dsf, tau);
-        if (getenv("TTO_FTBDBG")) {
-            double aw = 1, as_[4] = {1, 1, 1, 1}, ax = 1, au = 1, af = 1; int kw = -1, kx = -1, ix = -1;
-            for (int bi = 0; bi < W->nb; ++bi) {
-                for (int e = 0; e < 8; ++e) { double t = aw; FTB_P(W->w[8 * bi + e], -RELAX, W->dw[8 * bi + e], tau, aw); if (aw < t) kw = bi / W->nbk; }
-                for (int r = 0; r < 4; ++r) { const int v = 4 * bi + r; if (W->hrL[r]) FTB_P(W->s[v], W->rL[r], W->ds[v], tau, as_[r]); if (W->hrU[r]) FTB_PU(W->s[v], W->rU[r], W->ds[v], tau, as_[r]); }
+        opterr_t oe = opt_error(W, S->mu);
+        E0 = oe.E0;
+        if (!oe.finite) { status = 4; break; }
+        if (W->R == M_ORIG) {
+            if (dbg) fprintf(stderr, "it %4d E0 %.3e dinf %.3e pinf %.3e mu %.2e f %.6e\n", iter, E0, oe.dinf, oe.pinf,
+                             S->mu, cost_eval(W, W->x, W->u));
+            if (E0 <= P->tol) { status = 0; break; }
+            if (E0 <= P->acc_tol) {
+                memcpy(W->xacc, W->x, 6 * ((size_t)N + 1) * 8);
+                memcpy(W->uacc, W->u, 2 * (size_t)N * 8);
+                memcpy(W->wacc, W->w, 8 * (size_t)W->nb * 8);
+                W->have_acc = 1;
+                if (++S->acc_count >= P->acc_iter) { status = 1; break; }
+            } else {
+                S->acc_count = 0;
             }
-            for (int k = 0; k <= N; ++k) for (int i = 0; i < 6; ++i) { double t = ax; if (W->hxl[i]) FTB_P(W->x[6 * k + i], W->xl[i], W->dx[6 * k + i], tau, ax); if (W->hxu[i]) FTB_PU(W->x[6 * k + i], W->xu[i], W->dx[6 * k + i], tau, ax); if (ax < t) { kx = k; ix = i; } }
-            for (int k = 0; k < N; ++k) for (int i = 0; i < 2; ++i) { if (W->hul[i]) FTB_P(W->u[2 * k + i], W->ul[i], W->du[2 * k + i], tau, au); if (W->huu[i]) FTB_PU(W->u[2 * k + i], W->uu[i], W->du[2 * k + i], tau, au); }
-            if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) { FTB_P(W->sf[i], W->fL, W->dsf[i], tau, af); FTB_PU(W->sf[i], W->fU, W->dsf[i], tau, af); }
-            fprintf(stderr, "     ftb w %.1e(k%d) s %.1e %.1e %.1e %.1e x %.1e(k%d,i%d) u %.1e f %.1e\n", aw, kw, as_[0], as_[1], as_[2], as_[3], ax, kx, ix, au, af);
+            if (iter >= P->max_iter) { status = E0 <= P->acc_tol ? 1 : 2; break; }
+        } else {
+            /* restoration convergence (RestoConvergenceCheck): original infeasibility reduced to kappa_resto of
+             * its value at entry and the point acceptable to the augmented original filter */
+            double thO, phO;
+            orig_th_phi(W, SO.mu, &thO, &phO);
+            if (dbg) fprintf(stderr, "rit %3d E0 %.3e dinf %.3e pinf %.3e muR %.2e thO %.3e (%.3e)\n", iter, E0, oe.dinf,
+                             oe.pinf, S->mu, thO, th_resto0);
+            if (!first_resto && thO <= KAPPA_RESTO * th_resto0 && thO <= SO.th_max && !in_filter(&SO.F, thO, phO)) {
+                leave_resto(W, SO.mu, SO.tau);
+                SO.acc_count = 0;
+                --iter; /* the return itself is not an iteration */
+                continue;
+            }
+            first_resto = 0;
+            if (E0 <= P->acc_tol) ++S->acc_count; else S->acc_count = 0;
+            if (E0 <= P->tol || S->acc_count >= P->acc_iter) {
+                /* the restoration NLP converged (or converged to an acceptable point) without reaching a point
+                 * acceptable to the original problem */
+                if (oe.pinf <= 1e2 * P->tol || thO <= 1e2 * P->tol) {
+                    leave_resto(W, SO.mu, SO.tau); /* feasible but filter-unacceptable: continue with a fresh filter */
+                    SO.F.n = 0;
+                    --iter;
+                    continue;
+                }
+                status = 3; /* IPOPT: converged to a point of local infeasibility */
+                break;
+            }
+            if (iter >= P->max_iter) { status = 2; break; }
         }
-        double az = ftb_dual(W, tau);
-        /* filter line search (Waechter & Biegler 2006, IPOPT defaults) */
-        double ymax = 0.0;
-        for (int i = 0; i < 6 * (N + 1); ++i) ymax = fmax(ymax, fabs(W->ycp[i]));
-        for (int i = 0; i < 4 * W->nb; ++i) ymax = fmax(ymax, fabs(W->ydp[i]));
-        if (W->mode == TTO_OBCA_PLAN)
-            for (int i = 0; i < 6; ++i) ymax = fmax(ymax, fabs(W->ydpf[i]));
+        /* barrier update (monotone, Fiacco-McCormick); the filter is reset on every change */
+        while (oe.Emu <= kappa_eps * S->mu && S->mu > P->tol / 10.0 * 1.0000001) {
+            S->mu = fmax(P->tol / 10.0, fmin(kappa_mu * S->mu, pow(S->mu, theta_mu)));
+            S->tau = fmax(0.99, 1.0 - S->mu);
+            S->F.n = 0;
+            if (W->R == M_RESTO) { W->zeta = sqrt(S->mu); obj_grad(W); }
+            oe = opt_error(W, S->mu);
+        }
+        const double mu = S->mu;
         int bad = 0;
-        const double th0 = infeas1(W, W->c, W->d, W->s, W->df, W->sf);
-        const double phi0 = cost_eval(W, W->x, W->u) + barrier(W, W->x, W->u, W->w, W->s, W->sf, mu, &bad);
-        double Dm = 0.0, rel = 0.0;
-        for (int k = 0; k <= N; ++k) {
-            for (int i = 0; i < 6; ++i) {
-                Dm += bgrad_x(W, k, i, mu) * W->dx[6 * k + i];
-                rel = fmax(rel, fabs(W->dx[6 * k + i]) / (1.0 + fabs(W->x[6 * k + i])));
-            }
-            if (k < N)
-                for (int i = 0; i < 2; ++i) {
-                    Dm += bgrad_u(W, k, i, mu) * W->du[2 * k + i];
-                    rel = fmax(rel, fabs(W->du[2 * k + i]) / (1.0 + fabs(W->u[2 * k + i])));
-                }
+        const double th0 = infeas1(W, W->rc0, W->rd0, W->rf0);
+        const double phi0 = (W->R == M_RESTO ? resto_obj(W, W->x, W->u, W->w, W->pr, W->nr) : cost_eval(W, W->x, W->u)) +
+                            barrier(W, W->x, W->u, W->w, W->s, W->sf, W->R == M_RESTO ? W->pr : NULL,
+                                    W->R == M_RESTO ? W->nr : NULL, mu, &bad);
+        double dw = 0.0, alpha = 0.0, az = 0.0;
+        int accepted = 0;
+        if (fallback || newton(W, S, &dw) != 0) {
+            fallback = 0;
+            if (W->R == M_RESTO || !use_resto) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
+            goto restoration;                                         /* IPOPT's fallback: restoration phase */
         }
-        for (int bi = 0; bi < W->nb; ++bi) {
-            for (int e = 0; e < 8; ++e) {
-                Dm += -mu / (W->w[8 * bi + e] + RELAX) * W->dw[8 * bi + e];
-                rel = fmax(rel, fabs(W->dw[8 * bi + e]) / (1.0 + fabs(W->w[8 * bi + e])));
-            }
-            for (int r = 0; r < 4; ++r) {
-                Dm += bgrad_s(W, r, W->s[4 * bi + r], mu) * W->ds[4 * bi + r];
-                rel = fmax(rel, fabs(W->ds[4 * bi + r]) / (1.0 + fabs(W->s[4 * bi + r])));
-            }
-        }
-        if (W->mode == TTO_OBCA_PLAN)
-            for (int i = 0; i < 6; ++i) {
-                Dm += (-mu / (W->sf[i] - W->fL) + mu / (W->fU - W->sf[i])) * W->dsf[i];
-                rel = fmax(rel, fabs(W->dsf[i]) / (1.0 + fabs(W->sf[i])));
-            }
-        if (iter == 0 || !(th_max > 0)) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
-        const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
-        double amin;
-        if (Dm < 0.0) {
-            amin = fmin(g_th, g_ph * th0 / (-Dm));
-            if (th0 <= th_min) amin = fmin(amin, delta * pow(th0, s_th) / pow(-Dm, s_ph));
+        if (W->R == M_ORIG && in_soft) {
+            accepted = 0; /* handled below as a soft restoration step */
         } else {
-            amin = g_th;
+            accepted = line_search(W, S, (W->R == M_RESTO ? iter == resto_iter0 : iter == 0), th0, phi0, &alpha, &az);
         }
-        amin *= g_al;
-        const double tolc = 10.0 * DBL_EPSILON;
-        double alpha = ap;
-        int accepted = rel < 1e-15, ftype = 0;
-        const size_t nx_ = 6 * (size_t)(N + 1), nu_ = 2 * (size_t)N, nw_ = 8 * (size_t)W->nb, ns_ = 4 * (size_t)W->nb;
-#define TRIAL(a_) do { \
-            for (size_t i = 0; i < nx_; ++i) W->xt[i] = W->x[i] + (a_) * W->dx[i]; \
-            for (size_t i = 0; i < nu_; ++i) W->ut[i] = W->u[i] + (a_) * W->du[i]; \
-            for (size_t i = 0; i < nw_; ++i) W->wt[i] = W->w[i] + (a_) * W->dw[i]; \
-            for (size_t i = 0; i < ns_; ++i) W->st[i] = W->s[i] + (a_) * W->ds[i]; \
-            for (int i = 0; i < 6; ++i) W->sft[i] = W->sf[i] + (a_) * W->dsf[i]; \
-            trial_eval(W, mu, &tht, &pht); } while (0)
-        double tht = 0.0, pht = 0.0;
-        for (int ls = 0; !accepted; ++ls) {
-            TRIAL(alpha);
-            const int sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
-            int ok = 0;
-            if (isfinite(pht) && tht <= th_max && !in_filter(W, tht, pht)) {
-                if (th0 <= th_min && sw) { ftype = 1; ok = pht - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
-                else { ftype = 0; ok = tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+        if (!accepted && W->R == M_ORIG && use_soft && (in_soft ? ++soft_cnt <= MAX_SOFT_RESTO : 1)) {
+            /* soft restoration step (BacktrackingLineSearch::TrySoftRestoStep): primal and dual step
+             * min(alpha_p, alpha_d); accepted when acceptable to the filter or when the primal-dual error
+             * at mu drops by 0.9999 */
+            const double ap = ftb_primal(W, S->tau), azd = ftb_dual(W, S->tau), as = fmin(ap, azd);
+            set_trial(W, as);
+            double tht, pht;
+            trial_eval(W, mu, &tht, &pht);
+            const double g_th = 1e-5, g_ph = 1e-8, tolc = 10.0 * DBL_EPSILON;
+            const int orig_ok = isfinite(pht) && tht <= S->th_max && !in_filter(&S->F, tht, pht) &&
+                                (tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0));
+            int acc_soft = orig_ok;
+            if (!orig_ok && isfinite(pht)) {
+                snapshot(W, 0);
+                take_step(W, mu, as, as);
+                linearise(W);
+                const opterr_t ot = opt_error(W, mu);
+                snapshot(W, 1);
+                linearise(W);
+                acc_soft = ot.finite && ot.pderr <= SOFT_RESTO_FACTOR * oe.pderr;
             }
-            if (ok) { accepted = 1; break; }
-            if (ls == 0 && isfinite(pht) && tht >= th0) {
-                /* second-order corrections (IPOPT max_soc 4, kappa_soc 0.99) */
-                double* sv = (double*)malloc((nx_ + nu_ + nw_ + ns_ + nx_ + ns_ + 12) * sizeof(double));
-                if (!sv) break;
-                double* o = sv;
-                memcpy(o, W->dx, nx_ * 8); o += nx_; memcpy(o, W->du, nu_ * 8); o += nu_;
-                memcpy(o, W->dw, nw_ * 8); o += nw_; memcpy(o, W->ds, ns_ * 8); o += ns_;
-                memcpy(o, W->ycp, nx_ * 8); o += nx_; memcpy(o, W->ydp, ns_ * 8); o += ns_;
-                memcpy(o, W->dsf, 48); o += 6; memcpy(o, W->ydpf, 48);
-                /* c_soc(0) = alpha r(x) + r(x + alpha d), c_soc(p+1) = a_soc(p) c_soc(p) + r(x + a_soc(p) d_soc(p)) */
-                double frs[6] = {0}, a_soc = alpha, th_old = th0;
-                for (size_t i = 0; i < nx_; ++i) W->cr[i] = W->c[i];
-                for (size_t i = 0; i < ns_; ++i) W->dr[i] = W->d[i] - W->s[i];
-                if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = W->df[i] - W->sf[i];
-                int soc_ok = 0;
-                for (int p = 0; p < 4; ++p) {
-                    if (p > 0 && tht > 0.99 * th_old) break;
-                    th_old = tht;
-                    for (size_t i = 0; i < nx_; ++i) W->cr[i] = a_soc * W->cr[i] + W->ct[i];
-                    for (size_t i = 0; i < ns_; ++i) W->dr[i] = a_soc * W->dr[i] + (W->dtr[i] - W->st[i]);
-                    if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = a_soc * frs[i] + (W->dft[i] - W->sft[i]);
-                    solve_rhs(W, mu, W->cr, W->dr, frs);
-                    a_soc = ftb_primal(W, W->dx, W->du, W->dw, W->ds, W->dsf, tau);
-                    TRIAL(a_soc);
-                    int ok2 = 0;
-                    if (isfinite(pht) && tht <= th_max && !in_filter(W, tht, pht)) {
-                        if (th0 <= th_min && sw) { ftype = 1; ok2 = pht - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
-                        else { ftype = 0; ok2 = tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
-                    }
-                    if (ok2) { soc_ok = 1; break; }
-                    if (!isfinite(pht)) break;
+            if (acc_soft) {
+                ++n_soft;
+                add_filter(&S->F, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+                in_soft = !orig_ok;
+                if (orig_ok) soft_cnt = 0;
+                if (dbg) fprintf(stderr, "     soft-resto step a %.3e (orig %d)\n", as, orig_ok);
+                take_step(W, mu, as, as);
+                continue;
+            }
+        }
+        if (!accepted) {
+            if (W->R == M_RESTO) {
+                /* restoration of the restoration phase: elastic variables back to their closed form */
+                set_pn(W, mu);
+                S->F.n = 0;
+                if (dbg) fprintf(stderr, "     resto line search failed: p/n reset\n");
+                continue;
+            }
+            if (!use_resto) { S->F.n = 0; take_step(W, mu, alpha, az); continue; } /* round-1 fallback (opt-out) */
+        restoration:
+            in_soft = 0;
+            soft_cnt = 0;
+            if (th0 <= 1e-2 * P->tol) {
+                /* restoration called at an almost feasible point: IPOPT restores the last acceptable iterate
+                 * (Solved_To_Acceptable_Level) or stops with Restoration_Failed */
+                if (W->have_acc) {
+                    memcpy(W->x, W->xacc, 6 * ((size_t)N + 1) * 8);
+                    memcpy(W->u, W->uacc, 2 * (size_t)N * 8);
+                    memcpy(W->w, W->wacc, 8 * (size_t)W->nb * 8);
+                    status = 1;
+                } else {
+                    status = 3;
                 }
-                if (soc_ok) {
-                    accepted = 2;
-                    alpha = a_soc;
-                    mult_steps(W, mu);
-                    az = ftb_dual(W, tau);
-                    free(sv);
-                    break;
-                }
-                o = sv;
-                memcpy(W->dx, o, nx_ * 8); o += nx_; memcpy(W->du, o, nu_ * 8); o += nu_;
-                memcpy(W->dw, o, nw_ * 8); o += nw_; memcpy(W->ds, o, ns_ * 8); o += ns_;
-                memcpy(W->ycp, o, nx_ * 8); o += nx_; memcpy(W->ydp, o, ns_ * 8); o += ns_;
-                memcpy(W->dsf, o, 48); o += 6; memcpy(W->ydpf, o, 48);
-                free(sv);
+                break;
             }
-            if (alpha * 0.5 < amin) break;
-            alpha *= 0.5;
+            {
+                /* PrepareRestoPhaseStart: the current iterate enters the original filter */
+                const double g_th = 1e-5, g_ph = 1e-8;
+                if (isfinite(phi0)) add_filter(&SO.F, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+                if (!(SO.th_max > 0)) { SO.th_max = 1e4 * fmax(1.0, th0); SO.th_min = 1e-4 * fmax(1.0, th0); }
+                th_resto0 = th0;
+                const double muR = enter_resto(W, SO.mu);
+                if (!(P->opts & TTO_OPT_NO_LSQ_MULT)) ls_multipliers(W);
+                ipm_reset(&SR, muR);
+                first_resto = 1;
+                resto_iter0 = iter;
+                ++n_resto;
+                if (dbg) fprintf(stderr, "     -> restoration #%d (theta %.3e, muR %.3e)\n", n_resto, th0, muR);
+            }
+            --iter; /* entering is not an iteration */
+            continue;
         }
-        if (!accepted) { /* IPOPT would enter restoration here; we take a fallback step and reset the filter */
-            W->nf = 0;
-            ++n_fallback;
-        } else if (!ftype) {
-            add_filter(W, (1.0 - g_th) * th0, phi0 - g_ph * th0);
-        }
-#undef TRIAL
-        if (dbg) fprintf(stderr, "     ap %.3e az %.3e alpha %.3e acc %d f %d dw %.2e D %.3e th %.3e nf %d fb %d\n", ap, az, alpha, accepted, ftype, dw, Dm, th0, W->nf, n_fallback);
-        /* update */
-        for (size_t i = 0; i < nx_; ++i) W->x[i] += alpha * W->dx[i];
-        for (size_t i = 0; i < nu_; ++i) W->u[i] += alpha * W->du[i];
-        for (size_t i = 0; i < nw_; ++i) W->w[i] += alpha * W->dw[i];
-        for (size_t i = 0; i < ns_; ++i) W->s[i] += alpha * W->ds[i];
-        for (size_t i = 0; i < nx_; ++i) W->yc[i] += alpha * (W->ycp[i] - W->yc[i]);
-        for (size_t i = 0; i < ns_; ++i) W->yd[i] += alpha * (W->ydp[i] - W->yd[i]);
-        if (W->mode == TTO_OBCA_PLAN)
-            for (int i = 0; i < 6; ++i) {
-                W->sf[i] += alpha * W->dsf[i];
-                W->ydf[i] += alpha * (W->ydpf[i] - W->ydf[i]);
-                W->vLf[i] += az * W->dvLf[i];
-                W->vUf[i] += az * W->dvUf[i];
-                clamp_mult(&W->vLf[i], W->sf[i] - W->fL, mu);
-                clamp_mult(&W->vUf[i], W->fU - W->sf[i], mu);
-            }
-        for (int k = 0; k <= N; ++k) {
-            for (int i = 0; i < 6; ++i) {
-                const int v = 6 * k + i;
-                if (W->hxl[i]) { W->zLx[v] += az * W->dzLx[v]; clamp_mult(&W->zLx[v], W->x[v] - W->xl[i], mu); }
-                if (W->hxu[i]) { W->zUx[v] += az * W->dzUx[v]; clamp_mult(&W->zUx[v], W->xu[i] - W->x[v], mu); }
-            }
-            if (k < N)
-                for (int i = 0; i < 2; ++i) {
-                    const int v = 2 * k + i;
-                    if (W->hul[i]) { W->zLu[v] += az * W->dzLu[v]; clamp_mult(&W->zLu[v], W->u[v] - W->ul[i], mu); }
-                    if (W->huu[i]) { W->zUu[v] += az * W->dzUu[v]; clamp_mult(&W->zUu[v], W->uu[i] - W->u[v], mu); }
-                }
-        }
-        for (int bi = 0; bi < W->nb; ++bi) {
-            for (int e = 0; e < 8; ++e) {
-                const int v = 8 * bi + e;
-                W->zw[v] += az * W->dzw[v];
-                clamp_mult(&W->zw[v], W->w[v] + RELAX, mu);
-            }
-            for (int r = 0; r < 4; ++r) {
-                const int v = 4 * bi + r;
-                if (W->hrL[r]) { W->vL[v] += az * W->dvL[v]; clamp_mult(&W->vL[v], W->s[v] - W->rL[r], mu); }
-                if (W->hrU[r]) { W->vU[v] += az * W->dvU[v]; clamp_mult(&W->vU[v], W->rU[r] - W->s[v], mu); }
-            }
-        }
+        if (dbg) fprintf(stderr, "     alpha %.3e az %.3e dw %.2e th %.3e nf %d\n", alpha, az, dw, th0, S->F.n);
+        take_step(W, mu, alpha, az);
     }
+    if (W->R == M_RESTO) W->R = M_ORIG;
+    if (dbg) fprintf(stderr, "status %d iters %d resto %d soft %d\n", status, iter, n_resto, n_soft);
     pack(W, zout);
     if (iters_out) *iters_out = iter;
     if (kkt_out) *kkt_out = E0;

@@ -38,12 +38,18 @@ typedef struct {
     int dual_init;                   /* 0: start from the guess's mu/lam (reference behaviour);
                                         1: replace them by the separating-axis certificate of each
                                         body/obstacle pair at the guess pose (see tt_obca.c) */
+    int opts;                        /* TTO_OPT_* bits switching IPOPT features off (diagnostics; 0 = IPOPT) */
 } tto_obca_problem;
+
+#define TTO_OPT_NO_RESTO 1       /* no restoration phase: a failed line search takes its last trial step */
+#define TTO_OPT_NO_SOFT_RESTO 2  /* no soft restoration phase */
+#define TTO_OPT_NO_LSQ_MULT 4    /* constraint multipliers start at 0 instead of the least-squares estimate */
 
 /* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).
  * z_guess (n) or NULL (plan: _generate_initial_trajectory_guess 209-225; track: reference copy +
  * dual pattern, mpc_control_obs.py:216-239).  z_out (n).  Returns per-instance status
- * (0 converged, 1 acceptable, 2 max_iter, 3 infeasible x_init, 4 non-finite / regularisation failed). */
+ * (0 converged, 1 acceptable, 2 max_iter, 3 infeasible x_init or restoration converged to a point of local
+ * infeasibility, 4 non-finite, 5 step computation failed). */
 int tto_obca_solve(const tto_obca_problem* P, const double* x_init, const double* x_goal, const double* xref,
                    const double* uref, const double* z_guess, double* z_out, int* iters, double* kkt);
 

@@ -116,11 +116,11 @@ class TTOObcaProblem(C.Structure):
                 ("ulb", C.c_double * 2), ("uub", C.c_double * 2), ("obs", C.c_double * (4 * MAXM)),
                 ("dmin", C.c_double), ("eq_tol", C.c_double), ("fin_tol", C.c_double), ("tfac", C.c_double),
                 ("tol", C.c_double), ("acc_tol", C.c_double), ("max_iter", C.c_int), ("acc_iter", C.c_int),
-                ("dual_init", C.c_int)]
+                ("dual_init", C.c_int), ("opts", C.c_int)]
 
 
 def make_obca_problem(N, params, Q, R, xlb, xub, ulb, uub, obstacles, mode=OBCA_PLAN, tol=1e-8, acc_tol=1e-6,
-                      max_iter=5000, acc_iter=15, dual_init=1):
+                      max_iter=5000, acc_iter=15, dual_init=0, opts=0):
     """obstacles: (M,4) array of (cx, cy, w, h) (get_obstacles.py format)."""
     ob = np.asarray(obstacles, dtype=np.float64).reshape(-1, 4)
     if not 1 <= ob.shape[0] <= MAXM:
@@ -138,6 +138,7 @@ def make_obca_problem(N, params, Q, R, xlb, xub, ulb, uub, obstacles, mode=OBCA_
     P.tfac = 100.0 if mode == OBCA_PLAN else 1.0
     P.tol, P.acc_tol, P.max_iter, P.acc_iter = tol, acc_tol, max_iter, acc_iter
     P.dual_init = int(dual_init)
+    P.opts = int(opts)
     return P
 
 
