@@ -49,8 +49,11 @@ constexpr int kObcaThreads = 256;  // one workgroup (4 waves) per instance
 constexpr int kObcaMaxFilter = 64;
 enum { OBCA_PLAN = 0, OBCA_TRACK = 1 };
 
+// ObcaArgs::opts bits (diagnostics; 0 = IPOPT's algorithm): the same switches as the oracle's TTO_OPT_*
+enum { OBCA_OPT_NO_RESTO = 1, OBCA_OPT_NO_SOFT_RESTO = 2, OBCA_OPT_NO_LSQ_MULT = 4 };
+
 struct ObcaArgs {
-    int N, M, B, mode, max_iter, acc_iter, dual_init;
+    int N, M, B, mode, max_iter, acc_iter, dual_init, opts;
     double dt, L1, L2, Mh, W1, W2, tol, acc_tol, dmin, eq_tol, fin_tol, tfac;
     double Q[36], R[4];
     double xlb[6], xub[6], ulb[2], uub[2];
@@ -72,8 +75,8 @@ struct ObcaArgs {
 enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_TOTAL, kObcaPhases };
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
-constexpr int kObcaStageFields = 188;
-constexpr int kObcaBlockFields = 76;
+constexpr int kObcaStageFields = 339;
+constexpr int kObcaBlockFields = 184;
 __host__ __device__ inline size_t obca_ws_doubles(int N, int M) {
     return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
 }

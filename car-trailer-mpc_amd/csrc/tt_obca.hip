@@ -9,17 +9,21 @@
 //   plan  : goal cost, terminal 100 Q, |x_N - g| <= 1e-2               trajectory_optimization.py:168-183
 //   track : reference tracking cost, Q_f = Q                           mpc_control_obs.py:31-41
 //
-// Solver: the slack-form IPOPT restatement of the oracle (tol 1e-8, acceptable 1e-6 x 15, monotone mu,
-// bound_relax 1e-8, bound_push 1e-2, kappa_sigma 1e10, exact Hessian), IPOPT's filter line search with
-// up to 4 second-order corrections, Hessian regularisation with IPOPT's delta_w schedule.
+// Solver: the IPOPT restatement of the oracle (IPOPT defaults, trajectory_optimization.py:195-205):
+// slack-form barrier method (tol 1e-8, acceptable 1e-6 x 15, monotone mu, bound_relax 1e-8, bound_push
+// 1e-2, kappa_sigma 1e10, exact Hessian), least-squares constraint multipliers at the start
+// (constr_mult_init_max 1000), delta_w inertia correction, filter line search with up to 4 second-order
+// corrections, the soft restoration phase and the MinC_1Nrm feasibility restoration phase (elastic
+// p/n per constraint row, rho 1000, proximity sqrt(mu_R) ||D_R (xbar - xbar_R)||^2; the dynamics rows
+// become soft, so its Riccati sweep eliminates P~ = P - P Y P with Y = S (I + S P S)^-1 S).
 //
 // One workgroup (4 waves) per instance.  Work split:
 //   * stage-parallel phases (linearisation, optimality error, block elimination + stage Hessians,
-//     block step recovery, fraction-to-boundary, trial evaluation, updates): thread k owns stage k and
-//     its 2M OBCA blocks (obstacle x body).  Each block (8 duals, 4 rows) couples only to
-//     (X, Y, theta, psi) of its stage; its mu part is diagonal and its lam part a 4x4 SPD block, so
-//     the elimination is a 4x4 Cholesky + a 4x4 Schur complement T = D^-1 + Y'Y (never C'DC: D reaches
-//     1e10 on the +-1e-5 range rows and that product cancels catastrophically).
+//     block step recovery, fraction-to-boundary, trial evaluation, updates, restoration entry/exit):
+//     thread k owns stage k, its 6 dynamics rows and its 2M OBCA blocks (obstacle x body).  Each block
+//     (8 duals, 4 rows) couples only to (X, Y, theta, psi) of its stage; its mu part is diagonal and its
+//     lam part a 4x4 SPD block, so the elimination is a 4x4 Cholesky + a 4x4 Schur complement
+//     T = E + Y'Y (never C'DC: D reaches 1e10 on the +-1e-5 range rows and that product cancels).
 //   * serial phases (Riccati backward sweep over the 6x6 stage blocks, forward sweep): wave 0, lane
 //     (i,j) owns entry (i,j) of the 6x6 products; P and PA tiles in LDS.
 // Workspace: per instance in HBM, stage fields [f][k] and block fields [f][j][k] so that the lanes of a
@@ -34,17 +38,34 @@ namespace {
 constexpr int T = kObcaThreads;
 constexpr double RELAX = 1e-8;
 constexpr double EPS = 2.220446049250313e-16;
+constexpr double RHO = 1000.0;                 // resto_penalty_parameter
+constexpr double KAPPA_RESTO = 0.9;            // required_infeasibility_reduction
+constexpr double BOUND_MULT_RESET = 1000.0;    // bound_mult_reset_threshold
+constexpr double CONSTR_MULT_INIT_MAX = 1000.0;
+constexpr double SOFT_RESTO_FACTOR = 0.9999;   // soft_resto_pderror_reduction_factor
+constexpr int MAX_SOFT_RESTO = 10;             // max_soft_resto_iters
 
 enum : int {
     S_X = 0, S_U = 6, S_ZLX = 8, S_ZUX = 14, S_ZLU = 20, S_ZUU = 22, S_YC = 24,
     S_GX = 30, S_GU = 36, S_C = 38, S_AJ = 44, S_WD = 53, S_QT = 60, S_QV = 81, S_RT = 87, S_RV = 90,
     S_P = 92, S_PV = 113, S_K = 119, S_KF = 131, S_GI = 133, S_H = 136, S_DX = 148, S_DU = 160, S_YCP = 164,
-    S_CT = 176, S_CR = 182, S_END = 188
+    S_CT = 176, S_CR = 182,
+    // restoration phase: elastic pairs of the 6 dynamics rows of the stage (and their steps, 2 buffers),
+    // S = sqrt(E) of those rows, Y = S M^-1 S of the soft Riccati, the effective row residual, the
+    // reference point and D_R^2, the saved original bound multipliers, the stored acceptable point and the
+    // soft-restoration snapshot (x u zLx zUx zLu zUu yc)
+    S_PR = 188, S_NR = 194, S_ZP = 200, S_ZN = 206, S_DP = 212, S_DN = 224, S_SD = 236, S_Y = 242,
+    S_CE = 263, S_XR = 269, S_UR = 275, S_DRX = 277, S_DRU = 283, S_SZ = 285, S_XACC = 301, S_UACC = 307,
+    S_SNAP = 309, S_END = 339
 };
 static_assert(S_END == kObcaStageFields, "stage field count");
 enum : int {
     B_W = 0, B_ZW = 8, B_S = 16, B_VL = 20, B_VU = 24, B_YD = 28, B_D = 32, B_DW = 36, B_DS = 52, B_YP = 60,
-    B_DT = 68, B_DR = 72, B_END = 76
+    B_DT = 68, B_DR = 72,
+    // restoration phase: elastic pairs of the 4 rows (+ steps, 2 buffers), reference duals / slacks and
+    // D_R^2, saved multipliers, acceptable point, soft-restoration snapshot (w zw s vL vU yd)
+    B_PR = 76, B_NR = 80, B_ZP = 84, B_ZN = 88, B_DP = 92, B_DN = 100, B_WR = 108, B_DRW = 116, B_SR = 124,
+    B_SZW = 128, B_SVL = 136, B_SVU = 140, B_WACC = 144, B_SNAP = 152, B_END = 184
 };
 static_assert(B_END == kObcaBlockFields, "block field count");
 
@@ -91,11 +112,17 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 struct Shared {
-    double red[4][12];
+    double red[4][16];
     // final-row (plan mode) state, owned by the thread of stage N
-    double sf[6], vLf[6], vUf[6], ydf[6], df[6], dsf[2][6], ydpf[2][6], dft[6], dfr[6], Df[6], rf[6];
-    double fth[kObcaMaxFilter], fph[kObcaMaxFilter];
-    int nf;
+    double sf[6], vLf[6], vUf[6], ydf[6], df[6], dsf[2][6], ydpf[2][6], dft[6], dfr[6], Dsf[6], Dfe[6], rf[6];
+    // their restoration-phase elastic pairs, saved multipliers and the soft-restoration snapshot
+    double pf[6], nf[6], zpf[6], znf[6], dpf[2][6], dnf[2][6], sfR[6], svLf[6], svUf[6], snapf[24];
+    // filters: [0] original problem, [1] restoration problem
+    double fth[2][kObcaMaxFilter], fph[2][kObcaMaxFilter];
+    int nfl[2];
+    int R;       // 1 while in the restoration phase
+    int lsq;     // 1 while assembling the least-squares multiplier system
+    double zeta; // restoration proximity weight sqrt(mu_R)
     int flag;
     unsigned long long stamp[kObcaPhases];
     unsigned long long t0;
@@ -290,7 +317,8 @@ struct Blk {
     double Zl[4][4];                 // L^-1 W_lam x  [a][q]
     double LT[10];                   // chol of T
     double G[4][4];                  // Y_lam' Z - Jx  [r][q]
-    double D[4];
+    double D[4];                     // Sigma_s + dw of the 4 slacks
+    double E[4];                     // E of the 4 rows: 1/D (+ 1/D_p + 1/D_n in the restoration phase)
 };
 
 __device__ __forceinline__ bool chol4(double* L) {
@@ -401,7 +429,8 @@ __device__ __forceinline__ double jwm(const Blk& k, int r, int a) {
 }
 
 // elimination of a linearised block: returns false when the lam block is not positive definite.
-// sig_w: Sigma of the 8 duals; D: Sigma_s + dw of the 4 rows.  Adds the Schur complement into the
+// sig_w: diagonal Hessian of the 8 duals (Sigma_w, plus zeta D_R^2 in the restoration phase); E: the rows'
+// dual regularisation (1/D, plus 1/D_p + 1/D_n in the restoration phase).  Adds the Schur complement into the
 // stage Hessian contribution C (10 packed lower entries over X,Y,theta,psi).
 __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double dw, double* C) {
 #pragma unroll
@@ -435,7 +464,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int s = 0; s <= r; ++s) {
-            double t = (r == s) ? frcp(k.D[r]) : 0.0;
+            double t = (r == s) ? k.E[r] : 0.0;
 #pragma unroll
             for (int a = 0; a < 4; ++a) t += jwm(k, r, a) * jwm(k, s, a) * idm[a] + k.Yl[a][r] * k.Yl[a][s];
             k.LT[lo4(r, s)] = t;
@@ -588,6 +617,28 @@ __device__ __forceinline__ void ftb_hi(double v, double hi, double d, double tau
     if (d > 0.0) a = fmin(a, tau * (hi - v) / d);
 }
 
+// ---------------- restoration-phase elastic pairs (IPOPT MinC_1NrmRestorationPhase) ----------------
+// closed-form start: argmin rho (p + n) - mu (ln p + ln n) subject to p - n = r
+__device__ __forceinline__ void pn_closed_form(double r, double mu, double& p, double& n) {
+    const double S = sqrt(mu * mu + RHO * RHO * r * r);
+    const double am = mu - RHO * r, bp = mu + RHO * r;
+    n = am >= 0.0 ? (am + S) / (2.0 * RHO) : mu * r / (S - am);
+    p = bp >= 0.0 ? (bp + S) / (2.0 * RHO) : -mu * r / (S - bp);
+}
+// Newton terms of a pair: D_p dp - y+ = -g_p, D_n dn + y+ = -g_n (least-squares system: unit Hessian,
+// gradient rho - z)
+struct PN {
+    double Dp, Dn, gp, gn;
+};
+__device__ __forceinline__ PN pn_terms(bool lsq, double p, double n, double zp, double zn, double mu, double dw) {
+    PN t;
+    t.Dp = lsq ? 1.0 : zp / p + dw;
+    t.Dn = lsq ? 1.0 : zn / n + dw;
+    t.gp = RHO - (lsq ? zp : mu / p);
+    t.gn = RHO - (lsq ? zn : mu / n);
+    return t;
+}
+
 // ---------------- stage pieces ----------------
 __device__ __forceinline__ void load_x(const Ctx& c, int k, double* x) {
 #pragma unroll
@@ -615,7 +666,6 @@ __device__ __forceinline__ double stage_cost(const Ctx& c, int k, const double* 
     return F;
 }
 
-
 // barrier gradients of the block rows
 __device__ __forceinline__ double sig_row(const Ctx& c, int r, double s, double vl, double vu) {
     double sg = vu / (c.rU(r) - s);
@@ -628,25 +678,42 @@ __device__ __forceinline__ double grad_row(const Ctx& c, int r, double s, double
     return g;
 }
 
-// linearise + factor + rhs of one block at the current iterate; returns false if not positive definite
-__device__ __forceinline__ bool block_setup(const Ctx& c, int j, int k, const double* x, double mu, double dw, Blk& bk,
-                                            double* fw, double* zf, double* t4, double* C4, double* q4) {
+// linearise + factor + rhs of one block at the current iterate; returns false if not positive definite.
+// Outputs D (Sigma_s + dw), E (row regularisation), the elimination and the block's Hessian / gradient
+// contribution to its stage.
+__device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, int j, int k, const double* x, double mu,
+                                            double dw, Blk& bk, double* fw, double* zf, double* t4, double* C4,
+                                            double* q4) {
+    const bool rs = sh.R != 0, lsq = sh.lsq != 0;
     double w[8], y[4], sw[8], rd[4];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         w[e] = c.B(B_W + e, j, k);
-        const double sl = w[e] + RELAX;
-        sw[e] = c.B(B_ZW + e, j, k) / sl;
-        fw[e] = -mu / sl;
+        const double sl = w[e] + RELAX, zw = c.B(B_ZW + e, j, k);
+        double gw = 0.0, hw = 0.0;
+        if (rs) {
+            hw = sh.zeta * c.B(B_DRW + e, j, k);
+            gw = hw * (w[e] - c.B(B_WR + e, j, k));
+        }
+        sw[e] = lsq ? 1.0 : zw / sl + hw;
+        fw[e] = lsq ? gw - zw : gw - mu / sl;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
     blk_lin(*c.a, x, j, w, y, bk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const double s = c.B(B_S + r, j, k);
-        bk.D[r] = sig_row(c, r, s, c.B(B_VL + r, j, k), c.B(B_VU + r, j, k)) + dw;
-        rd[r] = c.B(B_DR + r, j, k) + grad_row(c, r, s, mu) / bk.D[r];
+        const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+        bk.D[r] = lsq ? 1.0 : sig_row(c, r, s, vl, vu) + dw;
+        bk.E[r] = 1.0 / bk.D[r];
+        const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
+        rd[r] = c.B(B_DR + r, j, k) + gs / bk.D[r];
+        if (rs) {
+            const PN t = pn_terms(lsq, c.B(B_PR + r, j, k), c.B(B_NR + r, j, k), c.B(B_ZP + r, j, k),
+                                  c.B(B_ZN + r, j, k), mu, dw);
+            bk.E[r] += 1.0 / t.Dp + 1.0 / t.Dn;
+            rd[r] += t.gp / t.Dp - t.gn / t.Dn;
+        }
     }
     if (!blk_factor(bk, sw, dw, C4)) return false;
     blk_rhs(bk, fw, rd, zf, t4, q4);
@@ -654,27 +721,30 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, int j, int k, const do
 }
 
 // ======== phase: stage Hessians + gradients (all threads) -> fail flag (uniform) ========
+// Also the effective dynamics-row residuals S_CE (= S_CR outside the restoration phase) and the soft-row
+// scales S_SD = sqrt(1/D_p + 1/D_n) of the restoration phase.
 __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, double dw) {
     LArgs& a = *c.a;
     const int N = c.N;
-    const bool plan = c.plan();
+    const bool plan = c.plan(), rs = sh.R != 0, lsq = sh.lsq != 0;
     double fail[1] = {0.0};
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6];
         load_x(c, k, x);
-        // the 12 OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
+        // the OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
         double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             double fw[8], zf[8], t4[4];
-            if (!block_setup(c, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+            if (!block_setup(c, sh, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
         }
         double Qs[21], qv[6];
         const double sc = (k == N && plan) ? a.tfac : 1.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i)
-            for (int j2 = i; j2 < 6; ++j2) Qs[sy6(i, j2)] = sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
-        if (k < N) {
+            for (int j2 = i; j2 < 6; ++j2)
+                Qs[sy6(i, j2)] = lsq ? (i == j2 ? 1.0 : 0.0) : rs ? 0.0 : sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
+        if (k < N && !lsq) {
             Qs[sy6(2, 2)] += c.S(S_WD + 0, k);
             Qs[sy6(2, 5)] += c.S(S_WD + 1, k);
             Qs[sy6(3, 3)] += c.S(S_WD + 2, k);
@@ -686,10 +756,18 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double xv = x[i];
-            double sg = dw, g = c.S(S_GX + i, k);
-            if (c.hlx(i)) { sg += c.S(S_ZLX + i, k) / (xv - c.xl[i]); g -= mu / (xv - c.xl[i]); }
-            if (c.hux(i)) { sg += c.S(S_ZUX + i, k) / (c.xu[i] - xv); g += mu / (c.xu[i] - xv); }
-            Qs[sy6(i, i)] += sg;
+            double sg = dw + (rs && !lsq ? sh.zeta * c.S(S_DRX + i, k) : 0.0), g = c.S(S_GX + i, k);
+            if (c.hlx(i)) {
+                const double zl = c.S(S_ZLX + i, k);
+                sg += zl / (xv - c.xl[i]);
+                g -= lsq ? zl : mu / (xv - c.xl[i]);
+            }
+            if (c.hux(i)) {
+                const double zu = c.S(S_ZUX + i, k);
+                sg += zu / (c.xu[i] - xv);
+                g += lsq ? zu : mu / (c.xu[i] - xv);
+            }
+            if (!lsq) Qs[sy6(i, i)] += sg;
             qv[i] = g;
         }
 #pragma unroll
@@ -701,24 +779,54 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
-                const double Df = sh.vLf[i] / sl + sh.vUf[i] / su + dw;
-                sh.Df[i] = Df;
-                sh.rf[i] = sh.dfr[i] + (-mu / sl + mu / su) / Df;
-                Qs[sy6(i, i)] += Df;
-                qv[i] += Df * sh.rf[i];
+                const double Ds = lsq ? 1.0 : sh.vLf[i] / sl + sh.vUf[i] / su + dw;
+                const double gs = lsq ? -sh.vLf[i] + sh.vUf[i] : -mu / sl + mu / su;
+                double E = 1.0 / Ds, rf = sh.dfr[i] + gs / Ds;
+                if (rs) {
+                    const PN t = pn_terms(lsq, sh.pf[i], sh.nf[i], sh.zpf[i], sh.znf[i], mu, dw);
+                    E += 1.0 / t.Dp + 1.0 / t.Dn;
+                    rf += t.gp / t.Dp - t.gn / t.Dn;
+                }
+                const double Dfe = 1.0 / E;
+                sh.Dsf[i] = Ds;
+                sh.Dfe[i] = Dfe;
+                sh.rf[i] = rf;
+                Qs[sy6(i, i)] += Dfe;
+                qv[i] += Dfe * rf;
             }
 #pragma unroll
         for (int i = 0; i < 21; ++i) c.S(S_QT + i, k) = Qs[i];
 #pragma unroll
         for (int i = 0; i < 6; ++i) c.S(S_QV + i, k) = qv[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double ce = c.S(S_CR + i, k), sd = 0.0;
+            if (rs) {
+                const PN t = pn_terms(lsq, c.S(S_PR + i, k), c.S(S_NR + i, k), c.S(S_ZP + i, k), c.S(S_ZN + i, k), mu, dw);
+                ce += t.gp / t.Dp - t.gn / t.Dn;
+                sd = sqrt(1.0 / t.Dp + 1.0 / t.Dn);
+            }
+            c.S(S_CE + i, k) = ce;
+            c.S(S_SD + i, k) = sd;
+        }
         if (k < N) {
             const double u0 = c.S(S_U, k), u1 = c.S(S_U + 1, k);
-            double R0 = 2.0 * a.R[0] + dw, R1 = a.R[1] + a.R[2], R3 = 2.0 * a.R[3] + dw;
-            double g0 = c.S(S_GU, k), g1 = c.S(S_GU + 1, k);
-            if (c.hlu(0)) { R0 += c.S(S_ZLU, k) / (u0 - c.ul[0]); g0 -= mu / (u0 - c.ul[0]); }
-            if (c.huu(0)) { R0 += c.S(S_ZUU, k) / (c.uu[0] - u0); g0 += mu / (c.uu[0] - u0); }
-            if (c.hlu(1)) { R3 += c.S(S_ZLU + 1, k) / (u1 - c.ul[1]); g1 -= mu / (u1 - c.ul[1]); }
-            if (c.huu(1)) { R3 += c.S(S_ZUU + 1, k) / (c.uu[1] - u1); g1 += mu / (c.uu[1] - u1); }
+            double R0, R1, R3, g0 = c.S(S_GU, k), g1 = c.S(S_GU + 1, k);
+            if (lsq) {
+                R0 = 1.0; R1 = 0.0; R3 = 1.0;
+                if (c.hlu(0)) g0 -= c.S(S_ZLU, k);
+                if (c.huu(0)) g0 += c.S(S_ZUU, k);
+                if (c.hlu(1)) g1 -= c.S(S_ZLU + 1, k);
+                if (c.huu(1)) g1 += c.S(S_ZUU + 1, k);
+            } else {
+                R0 = (rs ? sh.zeta * c.S(S_DRU, k) : 2.0 * a.R[0]) + dw;
+                R1 = rs ? 0.0 : a.R[1] + a.R[2];
+                R3 = (rs ? sh.zeta * c.S(S_DRU + 1, k) : 2.0 * a.R[3]) + dw;
+                if (c.hlu(0)) { R0 += c.S(S_ZLU, k) / (u0 - c.ul[0]); g0 -= mu / (u0 - c.ul[0]); }
+                if (c.huu(0)) { R0 += c.S(S_ZUU, k) / (c.uu[0] - u0); g0 += mu / (c.uu[0] - u0); }
+                if (c.hlu(1)) { R3 += c.S(S_ZLU + 1, k) / (u1 - c.ul[1]); g1 -= mu / (u1 - c.ul[1]); }
+                if (c.huu(1)) { R3 += c.S(S_ZUU + 1, k) / (c.uu[1] - u1); g1 += mu / (c.uu[1] - u1); }
+            }
             c.S(S_RT, k) = R0;
             c.S(S_RT + 1, k) = R1;
             c.S(S_RT + 2, k) = R3;
@@ -733,6 +841,7 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
 
 // Stage data of the serial sweeps, either straight from the HBM workspace (GSrc) or from LDS copies
 // staged by all four waves before the sweep (LSrc: region A = sweep inputs, region B = its outputs).
+// CR is the effective dynamics-row residual S_CE.
 struct GSrc {
     const Ctx& c;
     __device__ double QT(int i, int k) const { return c.S(S_QT + i, k); }
@@ -740,7 +849,7 @@ struct GSrc {
     __device__ double RT(int i, int k) const { return c.S(S_RT + i, k); }
     __device__ double RV(int i, int k) const { return c.S(S_RV + i, k); }
     __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
-    __device__ double CR(int i, int k) const { return c.S(S_CR + i, k); }
+    __device__ double CR(int i, int k) const { return c.S(S_CE + i, k); }
     __device__ double P(int i, int k) const { return c.S(S_P + i, k); }
     __device__ double PV(int i, int k) const { return c.S(S_PV + i, k); }
     __device__ double K(int i, int k) const { return c.S(S_K + i, k); }
@@ -785,7 +894,7 @@ __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
         else if (f < 30) g = S_RT + f - 27;
         else if (f < 32) g = S_RV + f - 30;
         else if (f < 41) g = S_AJ + f - 32;
-        else g = S_CR + f - 41;
+        else g = S_CE + f - 41;
         A[k * LA + f] = (k < c.N || (f < 27 || f >= 41)) ? c.S(g, k) : 0.0;
     }
 }
@@ -987,12 +1096,235 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
     }
 }
 
+// ======== restoration phase: Riccati sweep with soft dynamics rows (wave 0, HBM operands) ========
+// Row k reads x_k - F(x_{k-1}) - p + n = c: eliminating the elastic pair leaves J dx - E y+ = -r~ with
+// E = 1/D_p + 1/D_n, so x_k = yhat_k + E y+_k.  Before stage k-1 the cost-to-go of stage k is softened:
+// M = I + S P_k S (S = E^1/2; positive definite or the inertia is wrong), Y_k = S M^-1 S,
+// P~_k = P_k - P_k Y_k P_k, p~_k = p_k - P_k Y_k p_k; stage k-1 then runs the hard recursion on P~, p~.
+// M^-1 by in-place Gauss-Jordan (lane (i, j) owns entry (i, j); the pivots are M's LDL' pivots).  Y_k
+// is kept (S_Y) for the forward sweep.  Not latency-tuned: it runs only in restoration iterations.
+__device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh) {
+    const GSrc src{c};
+    const int lane = threadIdx.x, N = c.N;
+    const double dt = c.dt, dt2 = dt * dt;
+    const bool act = lane < 36, vec = lane >= 48 && lane < 54;
+    const int i = act ? lane / 6 : 0, j = act ? lane % 6 : 0, r = vec ? lane - 48 : 0;
+    const int ii = min(i, j), jj = max(i, j);
+    __shared__ double Pt[48], Mt[48], Yt[48], Tt[48];
+    if (act) {
+        const double q = src.QT(sy6(ii, jj), N);
+        Pt[8 * i + j] = q;
+        if (i <= j) src.setP(sy6(i, j), N, q);
+    }
+    double pv = vec ? src.QV(r, N) : 0.0;
+    if (vec) src.setPV(r, N, pv);
+    bool fail = false;
+    wave_sync();
+    for (int k = N;; --k) {
+        // ---- soften stage k
+        const double Si = c.S(S_SD + i, k), Sj = c.S(S_SD + j, k);
+        if (act) Mt[8 * i + j] = (i == j ? 1.0 : 0.0) + Si * Pt[8 * ii + jj] * Sj;
+        wave_sync();
+        for (int p = 0; p < 6; ++p) {
+            const double piv = Mt[8 * p + p];
+            double nv = 0.0;
+            if (act) {
+                const double aip = Mt[8 * i + p], apj = Mt[8 * p + j], aij = Mt[8 * i + j], ip = 1.0 / piv;
+                nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : aij - aip * apj * ip;
+            }
+            fail = fail || !(piv > 0.0);
+            wave_sync();
+            if (act) Mt[8 * i + j] = nv;
+            wave_sync();
+        }
+        if (act) {
+            const double y = c.S(S_SD + ii, k) * Mt[8 * ii + jj] * c.S(S_SD + jj, k);
+            Yt[8 * i + j] = y;
+            if (i <= j) c.S(S_Y + sy6(i, j), k) = y;
+        }
+        wave_sync();
+        if (act) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(Pt[8 * i + l], Yt[8 * l + j], t);
+            Tt[8 * i + j] = t;  // P Y
+        }
+        double pl[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) pl[q] = readlane_d(pv, 48 + q);
+        wave_sync();
+        double nP = 0.0, npv = pv;
+        if (act) {
+            double t = Pt[8 * ii + jj];
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(-Tt[8 * ii + l], Pt[8 * l + jj], t);
+            nP = t;
+        }
+        if (vec) {
+#pragma unroll
+            for (int l = 0; l < 6; ++l) npv = fma(-Tt[8 * r + l], pl[l], npv);
+        }
+        wave_sync();
+        if (act) Pt[8 * i + j] = nP;
+        pv = npv;
+        wave_sync();
+        if (k == 0) break;
+        // ---- stage kk = k-1 on P~_k, p~_k
+        const int kk = k - 1;
+        double dj[9], e[6];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) dj[q] = src.AJ(q, kk);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k);
+        const ColMask mj(j), mi(ii), mr(r), mjj(jj);
+        if (act) {  // PA[i][j] = P[i][j] + sum_{l<4} P[i][l] D[l][j]
+            double c0, c1, c2, c3;
+            dcol(dj, mj, c0, c1, c2, c3);
+            Tt[8 * i + j] = fma(Pt[8 * i + 0], c0, fma(Pt[8 * i + 1], c1, fma(Pt[8 * i + 2], c2, fma(Pt[8 * i + 3], c3, Pt[8 * i + j]))));
+        }
+        double pp = 0.0;
+        if (vec) {
+            pp = pv;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) pp = fma(-Pt[8 * r + q], e[q], pp);
+        }
+        wave_sync();
+        const double G00 = src.RT(0, kk) + dt2 * Pt[8 * 5 + 5], G01 = src.RT(1, kk) + dt2 * Pt[8 * 5 + 4];
+        const double G11 = src.RT(2, kk) + dt2 * Pt[8 * 4 + 4];
+        const double det = G00 * G11 - G01 * G01;
+        fail = fail || !(G00 > 0.0) || !(det > 0.0);
+        const double idet = 1.0 / det;
+        const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
+        double Pk = 0.0;
+        if (act) {  // P_kk[ii][jj] = Q~ + (A'PA)[ii][jj] + H'K
+            double c0, c1, c2, c3;
+            dcol(dj, mi, c0, c1, c2, c3);
+            const double atpa = fma(c0, Tt[8 * 0 + jj], fma(c1, Tt[8 * 1 + jj], fma(c2, Tt[8 * 2 + jj], fma(c3, Tt[8 * 3 + jj], Tt[8 * ii + jj]))));
+            const double H0i = dt * Tt[8 * 5 + ii], H1i = dt * Tt[8 * 4 + ii], H0j = dt * Tt[8 * 5 + jj], H1j = dt * Tt[8 * 4 + jj];
+            const double K0j = -fma(Gi00, H0j, Gi01 * H1j), K1j = -fma(Gi01, H0j, Gi11 * H1j);
+            Pk = src.QT(sy6(ii, jj), kk) + atpa + fma(H0i, K0j, H1i * K1j);
+        }
+        double ppl[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, 48 + q);
+        const double g0 = fma(dt, ppl[5], src.RV(0, kk)), g1 = fma(dt, ppl[4], src.RV(1, kk));
+        const double kf0 = -fma(Gi00, g0, Gi01 * g1), kf1 = -fma(Gi01, g0, Gi11 * g1);
+        double pnew = 0.0;
+        if (vec) {
+            double c0, c1, c2, c3;
+            dcol(dj, mr, c0, c1, c2, c3);
+            double ppr = ppl[0];
+#pragma unroll
+            for (int q = 1; q < 6; ++q) ppr = r == q ? ppl[q] : ppr;
+            const double H0 = dt * Tt[8 * 5 + r], H1 = dt * Tt[8 * 4 + r];
+            pnew = src.QV(r, kk) + fma(c0, ppl[0], fma(c1, ppl[1], fma(c2, ppl[2], fma(c3, ppl[3], ppr)))) +
+                   fma(H0, kf0, H1 * kf1);
+            src.setK(r, kk, -fma(Gi00, H0, Gi01 * H1));
+            src.setK(6 + r, kk, -fma(Gi01, H0, Gi11 * H1));
+            src.setPV(r, kk, pnew);
+        }
+        if (lane == 0) {
+            src.setKF(0, kk, kf0);
+            src.setKF(1, kk, kf1);
+        }
+        if (act && i <= j) src.setP(sy6(i, j), kk, Pk);
+        wave_sync();
+        if (act) Pt[8 * i + j] = Pk;
+        pv = pnew;
+        wave_sync();
+        (void)mjj;
+    }
+    if (lane == 0) sh.flag = fail ? 1 : 0;
+    wave_sync();
+}
+
+// forward sweep with soft rows: yhat = A dx + B du - r~; dx = yhat - Y (P yhat + p)
+__device__ __noinline__ void forward_soft(const Ctx& c, int buf) {
+    const GSrc src{c};
+    const int lane = threadIdx.x, N = c.N;
+    const double dt = c.dt;
+    const int r = lane < 6 ? lane : 0;
+    double dx[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) dx[q] = -src.CR(q, 0);
+    for (int k = 0;; ++k) {
+        double b[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            double t = src.PV(q, k);
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(src.P(sy6(q, l), k), dx[l], t);
+            b[q] = t;
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(c.S(S_Y + sy6(q, l), k), b[l], t);
+            dx[q] -= t;
+        }
+        if (lane < 6) {
+            double t = src.PV(r, k), dxr = dx[0];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) t = fma(src.P(sy6(r, q), k), dx[q], t);
+#pragma unroll
+            for (int q = 1; q < 6; ++q) dxr = r == q ? dx[q] : dxr;
+            c.S(S_YCP + 6 * buf + r, k) = -t;
+            c.S(S_DX + 6 * buf + r, k) = dxr;
+        }
+        if (k == N) break;
+        double du0 = src.KF(0, k), du1 = src.KF(1, k);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            du0 = fma(src.K(q, k), dx[q], du0);
+            du1 = fma(src.K(6 + q, k), dx[q], du1);
+        }
+        if (lane == 0) {
+            c.S(S_DU + 2 * buf, k) = du0;
+            c.S(S_DU + 2 * buf + 1, k) = du1;
+        }
+        double aj[9], e[6];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) aj[q] = src.AJ(q, k);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k + 1);
+        double nx[6];
+        nx[0] = (dx[0] - e[0]) + fma(aj[0], dx[2], aj[1] * dx[5]);
+        nx[1] = (dx[1] - e[1]) + fma(aj[2], dx[2], aj[3] * dx[5]);
+        nx[2] = (dx[2] - e[2]) + fma(aj[4], dx[4], aj[5] * dx[5]);
+        nx[3] = (dx[3] - e[3]) + fma(aj[6], dx[3], fma(aj[7], dx[4], aj[8] * dx[5]));
+        nx[4] = (dx[4] - e[4]) + dt * du1;
+        nx[5] = (dx[5] - e[5]) + dt * du0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) dx[q] = nx[q];
+    }
+}
+
+// elastic-pair step of one row from its new multiplier: dp = (y+ - g_p)/D_p, dn = (-y+ - g_n)/D_n, plus
+// fraction to the boundary (p, n >= 0; z_p, z_n >= 0), directional derivative and relative step size
+__device__ __forceinline__ void pn_step(double p, double n, double zp, double zn, double yp, double mu, double dw,
+                                        double tau, double& dp, double& dn, double& ap, double& az, double& Dm,
+                                        double& rel) {
+    const PN t = pn_terms(false, p, n, zp, zn, mu, dw);
+    dp = (yp - t.gp) / t.Dp;
+    dn = (-yp - t.gn) / t.Dn;
+    ftb_lo(p, 0.0, dp, tau, ap);
+    ftb_lo(n, 0.0, dn, tau, ap);
+    const double dzp = mu / p - zp - zp / p * dp, dzn = mu / n - zn - zn / n * dn;
+    if (dzp < 0.0) az = fmin(az, -tau * zp / dzp);
+    if (dzn < 0.0) az = fmin(az, -tau * zn / dzn);
+    Dm += t.gp * dp + t.gn * dn;
+    rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+}
+
 // ======== phase: block step recovery + fraction to boundary + directional derivative ========
-// out: [0] alpha_primal (min), [1] alpha_dual (min), [2] grad phi' d (sum), [3] max relative step
-__device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, double (&out)[4]) {
+// out: [0] alpha_primal (min), [1] alpha_dual (min), [2] grad phi' d (sum), [3] max relative step,
+//      [4] max |y+| (least-squares multiplier test)
+__device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf,
+                                           double (&out)[5]) {
     const int N = c.N;
-    const bool plan = c.plan();
-    double ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
+    const bool plan = c.plan(), rs = sh.R != 0 && !sh.lsq, lsq = sh.lsq != 0;
+    double ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0, ymax = 0.0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], dx[6];
         load_x(c, k, x);
@@ -1018,6 +1350,15 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 if (dz < 0.0) az = fmin(az, -tau * z / dz);
             }
             Dm += g * d;
+            const double yp = c.S(S_YCP + 6 * buf + i, k);
+            ymax = fmax(ymax, fabs(yp));
+            if (rs) {
+                double dp, dn;
+                pn_step(c.S(S_PR + i, k), c.S(S_NR + i, k), c.S(S_ZP + i, k), c.S(S_ZN + i, k), yp, mu, dw, tau, dp, dn,
+                        ap, az, Dm, rel);
+                c.S(S_DP + 6 * buf + i, k) = dp;
+                c.S(S_DN + 6 * buf + i, k) = dn;
+            }
         }
         if (k < N)
 #pragma unroll
@@ -1045,7 +1386,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             double fw[8], zf[8], t4[4], yp[4], dwv[8];
-            (void)block_setup(c, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4);
+            (void)block_setup(c, sh, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4);
             blk_recover(bk, fw, zf, t4, dx, yp, dwv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -1060,21 +1401,30 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double s = c.B(B_S + r, j, k);
-                const double gs = grad_row(c, r, s, mu);
+                const double vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+                const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
                 const double ds = (yp[r] - gs) / bk.D[r];
                 c.B(B_YP + 4 * buf + r, j, k) = yp[r];
                 c.B(B_DS + 4 * buf + r, j, k) = ds;
+                ymax = fmax(ymax, fabs(yp[r]));
                 rel = fmax(rel, fabs(ds) / (1.0 + fabs(s)));
                 Dm += gs * ds;
-                const double vu = c.B(B_VU + r, j, k), slu = c.rU(r) - s;
+                const double slu = c.rU(r) - s;
                 ftb_hi(s, c.rU(r), ds, tau, ap);
                 const double dvu = mu / slu - vu + vu / slu * ds;
                 if (dvu < 0.0) az = fmin(az, -tau * vu / dvu);
                 if (c.hrl(r)) {
-                    const double vl = c.B(B_VL + r, j, k), sll = s - c.rL(r);
+                    const double sll = s - c.rL(r);
                     ftb_lo(s, c.rL(r), ds, tau, ap);
                     const double dvl = mu / sll - vl - vl / sll * ds;
                     if (dvl < 0.0) az = fmin(az, -tau * vl / dvl);
+                }
+                if (rs) {
+                    double dp, dn;
+                    pn_step(c.B(B_PR + r, j, k), c.B(B_NR + r, j, k), c.B(B_ZP + r, j, k), c.B(B_ZN + r, j, k), yp[r],
+                            mu, dw, tau, dp, dn, ap, az, Dm, rel);
+                    c.B(B_DP + 4 * buf + r, j, k) = dp;
+                    c.B(B_DN + 4 * buf + r, j, k) = dn;
                 }
             }
         }
@@ -1082,11 +1432,12 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
-                const double gs = -mu / sl + mu / su;
-                const double yp = sh.Df[i] * (dx[i] + sh.rf[i]);
-                const double ds = (yp - gs) / sh.Df[i];
+                const double gs = lsq ? -sh.vLf[i] + sh.vUf[i] : -mu / sl + mu / su;
+                const double yp = sh.Dfe[i] * (dx[i] + sh.rf[i]);
+                const double ds = (yp - gs) / sh.Dsf[i];
                 sh.ydpf[buf][i] = yp;
                 sh.dsf[buf][i] = ds;
+                ymax = fmax(ymax, fabs(yp));
                 rel = fmax(rel, fabs(ds) / (1.0 + fabs(sh.sf[i])));
                 Dm += gs * ds;
                 ftb_lo(sh.sf[i], c.fL, ds, tau, ap);
@@ -1095,19 +1446,26 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 const double dvu = mu / su - sh.vUf[i] + sh.vUf[i] / su * ds;
                 if (dvl < 0.0) az = fmin(az, -tau * sh.vLf[i] / dvl);
                 if (dvu < 0.0) az = fmin(az, -tau * sh.vUf[i] / dvu);
+                if (rs) {
+                    double dp, dn;
+                    pn_step(sh.pf[i], sh.nf[i], sh.zpf[i], sh.znf[i], yp, mu, dw, tau, dp, dn, ap, az, Dm, rel);
+                    sh.dpf[buf][i] = dp;
+                    sh.dnf[buf][i] = dn;
+                }
             }
     }
-    out[0] = ap; out[1] = az; out[2] = Dm; out[3] = rel;
-    const int ops[4] = {R_MIN, R_MIN, R_SUM, R_MAX};
+    if (!isfinite(ymax)) ymax = INFINITY;
+    out[0] = ap; out[1] = az; out[2] = Dm; out[3] = rel; out[4] = ymax;
+    const int ops[5] = {R_MIN, R_MIN, R_SUM, R_MAX, R_MAX};
     wg_reduce(sh, out, ops);
 }
 
 // ======== phase: trial point x + alpha d (step buffer buf) -> theta, phi (barrier objective), bad ========
-// also stores the trial residuals (for second-order corrections)
+// of the current NLP; also stores the trial residual rows (for second-order corrections)
 __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, double alpha, int buf, double (&out)[3]) {
     LArgs& a = *c.a;
     const int N = c.N;
-    const bool plan = c.plan();
+    const bool plan = c.plan(), rs = sh.R != 0;
     double th = 0.0, F = 0.0, logs = 0.0, bad = 0.0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0};
@@ -1118,36 +1476,59 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
             for (int i = 0; i < 2; ++i) u[i] = c.S(S_U + i, k) + alpha * c.S(S_DU + 2 * buf + i, k);
         LogSum ls;
         bool ok = true;
+        double Fr = 0.0, prox = 0.0;  // restoration objective of this stage: rho sum(p + n), D_R-weighted distances
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; ok &= sl > 0.0; ls.add(sl); }
             if (c.hux(i)) { const double sl = c.xu[i] - x[i]; ok &= sl > 0.0; ls.add(sl); }
+            if (rs) { const double e = x[i] - c.S(S_XR + i, k); prox += c.S(S_DRX + i, k) * e * e; }
         }
         if (k < N)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; ok &= sl > 0.0; ls.add(sl); }
                 if (c.huu(i)) { const double sl = c.uu[i] - u[i]; ok &= sl > 0.0; ls.add(sl); }
+                if (rs) { const double e = u[i] - c.S(S_UR + i, k); prox += c.S(S_DRU + i, k) * e * e; }
             }
         // dynamics residual c_{k+1} = x_{k+1} - F(x_k, u_k) (thread k), c_0 = x_0 - x_init
-        if (k == 0)
+        double ck[6] = {0, 0, 0, 0, 0, 0};
+        if (k == 0) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const double cv = x[i] - a.x0[6 * (size_t)c.b + i];
-                c.S(S_CT + i, 0) = cv;
-                th += fabs(cv);
-            }
+            for (int i = 0; i < 6; ++i) ck[i] = x[i] - a.x0[6 * (size_t)c.b + i];
+        }
         if (k < N) {
             double fo[6];
             model_f(a, x, u, fo);
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double xn = c.S(S_X + i, k + 1) + alpha * c.S(S_DX + 6 * buf + i, k + 1);
-                const double cv = xn - (x[i] + a.dt * fo[i]);
+                double cv = xn - (x[i] + a.dt * fo[i]);
+                if (rs) {  // row of stage k+1 (owned there: read its elastic pair)
+                    const double p = c.S(S_PR + i, k + 1) + alpha * c.S(S_DP + 6 * buf + i, k + 1);
+                    const double n = c.S(S_NR + i, k + 1) + alpha * c.S(S_DN + 6 * buf + i, k + 1);
+                    cv -= p - n;
+                }
                 c.S(S_CT + i, k + 1) = cv;
                 th += fabs(cv);
             }
         }
+        if (rs)  // elastic pairs of this stage's own dynamics rows: barrier + objective (+ row 0's residual)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double p = c.S(S_PR + i, k) + alpha * c.S(S_DP + 6 * buf + i, k);
+                const double n = c.S(S_NR + i, k) + alpha * c.S(S_DN + 6 * buf + i, k);
+                ok &= p > 0.0 && n > 0.0;
+                ls.add(p);
+                ls.add(n);
+                Fr += p + n;
+                if (k == 0) ck[i] -= p - n;
+            }
+        if (k == 0)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                c.S(S_CT + i, 0) = ck[i];
+                th += fabs(ck[i]);
+            }
         for (int j = 0; j < c.nbk; ++j) {
             double w[8], d[4];
 #pragma unroll
@@ -1156,12 +1537,22 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
                 const double sl = w[e] + RELAX;
                 ok &= sl > 0.0;
                 ls.add(sl);
+                if (rs) { const double ew = w[e] - c.B(B_WR + e, j, k); prox += c.B(B_DRW + e, j, k) * ew * ew; }
             }
             blk_vals(a, x, j, w, d);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double s = c.B(B_S + r, j, k) + alpha * c.B(B_DS + 4 * buf + r, j, k);
-                const double res = d[r] - s;
+                double res = d[r] - s;
+                if (rs) {
+                    const double p = c.B(B_PR + r, j, k) + alpha * c.B(B_DP + 4 * buf + r, j, k);
+                    const double n = c.B(B_NR + r, j, k) + alpha * c.B(B_DN + 4 * buf + r, j, k);
+                    ok &= p > 0.0 && n > 0.0;
+                    ls.add(p);
+                    ls.add(n);
+                    Fr += p + n;
+                    res -= p - n;
+                }
                 c.B(B_DT + r, j, k) = res;
                 th += fabs(res);
                 const double su = c.rU(r) - s;
@@ -1174,7 +1565,15 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double s = sh.sf[i] + alpha * sh.dsf[buf][i];
-                const double res = (x[i] - c.tgt_x[i]) - s;
+                double res = (x[i] - c.tgt_x[i]) - s;
+                if (rs) {
+                    const double p = sh.pf[i] + alpha * sh.dpf[buf][i], n = sh.nf[i] + alpha * sh.dnf[buf][i];
+                    ok &= p > 0.0 && n > 0.0;
+                    ls.add(p);
+                    ls.add(n);
+                    Fr += p + n;
+                    res -= p - n;
+                }
                 sh.dft[i] = res;
                 th += fabs(res);
                 const double sl = s - c.fL, su = c.fU - s;
@@ -1182,7 +1581,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
                 ls.add(sl);
                 ls.add(su);
             }
-        F += stage_cost(c, k, x, u);
+        F += rs ? RHO * Fr + 0.5 * sh.zeta * prox : stage_cost(c, k, x, u);
         if (!ok) bad = 1.0;
         else logs += ls.value();
     }
@@ -1208,9 +1607,28 @@ __device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a
     }
 }
 
+// ======== phase: residual rows of the Newton right-hand side at the iterate (zero: least squares) ========
+__device__ __noinline__ void phase_resid(const Ctx& c, LShared& sh, bool zero) {
+    const bool rs = sh.R != 0;
+    for (int k = (int)threadIdx.x; k <= c.N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+            c.S(S_CR + i, k) = zero ? 0.0 : c.S(S_C + i, k) - (rs ? c.S(S_PR + i, k) - c.S(S_NR + i, k) : 0.0);
+        for (int j = 0; j < c.nbk; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                c.B(B_DR + r, j, k) = zero ? 0.0 : c.B(B_D + r, j, k) - c.B(B_S + r, j, k) -
+                                                       (rs ? c.B(B_PR + r, j, k) - c.B(B_NR + r, j, k) : 0.0);
+        if (k == c.N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) sh.dfr[i] = zero ? 0.0 : sh.df[i] - sh.sf[i] - (rs ? sh.pf[i] - sh.nf[i] : 0.0);
+    }
+}
+
 // ======== phase: accept the step ========
 __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
     const int N = c.N;
+    const bool rs = sh.R != 0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -1231,6 +1649,18 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
             c.S(S_X + i, k) = xn;
             const double y = c.S(S_YC + i, k);
             c.S(S_YC + i, k) = y + alpha * (c.S(S_YCP + 6 * buf + i, k) - y);
+            if (rs) {
+                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
+                const double dp = c.S(S_DP + 6 * buf + i, k), dn = c.S(S_DN + 6 * buf + i, k);
+                const double pn = p + alpha * dp, nn = n + alpha * dn;
+                double zpn = zp + az * (mu / p - zp - zp / p * dp), znn = zn + az * (mu / n - zn - zn / n * dn);
+                clamp_mult(zpn, pn, mu);
+                clamp_mult(znn, nn, mu);
+                c.S(S_PR + i, k) = pn;
+                c.S(S_NR + i, k) = nn;
+                c.S(S_ZP + i, k) = zpn;
+                c.S(S_ZN + i, k) = znn;
+            }
         }
         if (k < N)
 #pragma unroll
@@ -1277,6 +1707,19 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                 c.B(B_S + r, j, k) = sn;
                 const double y = c.B(B_YD + r, j, k);
                 c.B(B_YD + r, j, k) = y + alpha * (c.B(B_YP + 4 * buf + r, j, k) - y);
+                if (rs) {
+                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k), zp = c.B(B_ZP + r, j, k),
+                                 zn = c.B(B_ZN + r, j, k);
+                    const double dp = c.B(B_DP + 4 * buf + r, j, k), dn = c.B(B_DN + 4 * buf + r, j, k);
+                    const double pn = p + alpha * dp, nn = n + alpha * dn;
+                    double zpn = zp + az * (mu / p - zp - zp / p * dp), znn = zn + az * (mu / n - zn - zn / n * dn);
+                    clamp_mult(zpn, pn, mu);
+                    clamp_mult(znn, nn, mu);
+                    c.B(B_PR + r, j, k) = pn;
+                    c.B(B_NR + r, j, k) = nn;
+                    c.B(B_ZP + r, j, k) = zpn;
+                    c.B(B_ZN + r, j, k) = znn;
+                }
             }
         }
         if (k == N && c.plan())
@@ -1292,43 +1735,76 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                 sh.vUf[i] = vu;
                 sh.sf[i] = sn;
                 sh.ydf[i] += alpha * (sh.ydpf[buf][i] - sh.ydf[i]);
+                if (rs) {
+                    const double p = sh.pf[i], n = sh.nf[i], zp = sh.zpf[i], zn = sh.znf[i];
+                    const double dp = sh.dpf[buf][i], dn = sh.dnf[buf][i];
+                    const double pn = p + alpha * dp, nn = n + alpha * dn;
+                    double zpn = zp + az * (mu / p - zp - zp / p * dp), znn = zn + az * (mu / n - zn - zn / n * dn);
+                    clamp_mult(zpn, pn, mu);
+                    clamp_mult(znn, nn, mu);
+                    sh.pf[i] = pn;
+                    sh.nf[i] = nn;
+                    sh.zpf[i] = zpn;
+                    sh.znf[i] = znn;
+                }
             }
     }
 }
 
-__device__ __forceinline__ bool in_filter(const LShared& sh, double th, double ph) {
-    for (int i = 0; i < sh.nf; ++i)
-        if (th >= sh.fth[i] && ph >= sh.fph[i]) return true;
+// filters: [0] original problem, [1] restoration problem
+__device__ __forceinline__ bool in_filter(const LShared& sh, int f, double th, double ph) {
+    for (int i = 0; i < sh.nfl[f]; ++i)
+        if (th >= sh.fth[f][i] && ph >= sh.fph[f][i]) return true;
     return false;
 }
-__device__ __forceinline__ void add_filter(LShared& sh, double th, double ph) {  // thread 0 only
+__device__ __forceinline__ void add_filter(LShared& sh, int f, double th, double ph) {  // thread 0 only
     int j = 0;
-    for (int i = 0; i < sh.nf; ++i)
-        if (!(sh.fth[i] >= th && sh.fph[i] >= ph)) { sh.fth[j] = sh.fth[i]; sh.fph[j] = sh.fph[i]; ++j; }
+    for (int i = 0; i < sh.nfl[f]; ++i)
+        if (!(sh.fth[f][i] >= th && sh.fph[f][i] >= ph)) { sh.fth[f][j] = sh.fth[f][i]; sh.fph[f][j] = sh.fph[f][i]; ++j; }
     if (j == kObcaMaxFilter) {
-        for (int i = 0; i + 1 < kObcaMaxFilter; ++i) { sh.fth[i] = sh.fth[i + 1]; sh.fph[i] = sh.fph[i + 1]; }
+        for (int i = 0; i + 1 < kObcaMaxFilter; ++i) { sh.fth[f][i] = sh.fth[f][i + 1]; sh.fph[f][i] = sh.fph[f][i + 1]; }
         --j;
     }
-    sh.fth[j] = th;
-    sh.fph[j] = ph;
-    sh.nf = j + 1;
+    sh.fth[f][j] = th;
+    sh.fph[f][j] = ph;
+    sh.nfl[f] = j + 1;
 }
 
-// ======== phase: linearisation at the iterate + optimality-error ingredients ========
-// out: [0] dual inf (max) [1] primal inf (max) [2] complementarity (max) [3] sum |y| + sum z
-//      [4] sum z [5] theta = l1 infeasibility [6] cost [7] sum log slacks
-__device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[8]) {
+// ======== phase: linearisation at the iterate + optimality-error ingredients of the current NLP ========
+// out: [0] dual inf (max) [1] primal inf (max) [2] complementarity (max) [3] sum |y| + sum z [4] sum z
+//      [5] theta (l1 of the residual rows) [6] objective [7] sum log slacks [8] sum |dual residuals|
+//      [9] original theta [10] original cost [11] original sum log slacks (restoration: no p, n)
+__device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[12]) {
     LArgs& a = *c.a;
     const int N = c.N;
-    const bool plan = c.plan();
+    const bool plan = c.plan(), rs = sh.R != 0;
+    const double zeta = sh.zeta;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[i] = 0.0;
+    for (int i = 0; i < 12; ++i) red[i] = 0.0;
     const double* xinit = a.x0 + 6 * (size_t)c.b;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0}, gl[6];
+        double objR = 0.0;  // restoration objective of this stage
         load_x(c, k, x);
         if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
-        {
+        if (rs) {
+            double prox = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double dr = c.S(S_DRX + i, k), e = x[i] - c.S(S_XR + i, k);
+                gl[i] = zeta * dr * e;
+                c.S(S_GX + i, k) = gl[i];
+                prox += dr * e * e;
+            }
+            if (k < N)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const double dr = c.S(S_DRU + i, k), e = u[i] - c.S(S_UR + i, k);
+                    c.S(S_GU + i, k) = zeta * dr * e;
+                    prox += dr * e * e;
+                }
+            objR += 0.5 * zeta * prox;
+        } else {
             const double* tg = plan ? c.tgt_x : c.tgt_x + 6 * k;
             const double sc = (k == N && plan) ? a.tfac : 1.0;
 #pragma unroll
@@ -1357,11 +1833,28 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
             for (int i = 0; i < 6; ++i) ck[i] = x[i] - (xp[i] + a.dt * fo[i]);
         }
+        LogSum lsum, lorig;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             c.S(S_C + i, k) = ck[i];
-            red[1] = fmax(red[1], fabs(ck[i]));
-            red[5] += fabs(ck[i]);
+            double res = ck[i];
+            if (rs) {
+                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
+                const double y = c.S(S_YC + i, k);
+                res -= p - n;
+                const double t1 = RHO - y - zp, t2 = RHO + y - zn;
+                red[0] = fmax(red[0], fmax(fabs(t1), fabs(t2)));
+                red[8] += fabs(t1) + fabs(t2);
+                red[2] = fmax(red[2], fmax(fabs(p * zp), fabs(n * zn)));
+                red[3] += zp + zn;
+                red[4] += zp + zn;
+                lsum.add(p);
+                lsum.add(n);
+                objR += RHO * (p + n);
+            }
+            red[1] = fmax(red[1], fabs(res));
+            red[5] += fabs(res);
+            red[9] += fabs(ck[i]);
         }
         double yk[6], yn[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -1387,7 +1880,6 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
-        LogSum lsum;
         for (int j = 0; j < c.nbk; ++j) {
             double w[8], y[4], zw[8];
 #pragma unroll
@@ -1408,30 +1900,57 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 double t = -zw[e];
+                if (rs) {
+                    const double dr = c.B(B_DRW + e, j, k), ew = w[e] - c.B(B_WR + e, j, k);
+                    t += zeta * dr * ew;
+                    objR += 0.5 * zeta * dr * ew * ew;
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * y[r];
                 red[0] = fmax(red[0], fabs(t));
+                red[8] += fabs(t);
                 const double sl = w[e] + RELAX;
                 red[2] = fmax(red[2], fabs(zw[e] * sl));
                 red[3] += zw[e];
                 red[4] += zw[e];
                 lsum.add(sl);
+                lorig.add(sl);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
-                red[0] = fmax(red[0], fabs(-y[r] - vl + vu));
-                red[1] = fmax(red[1], fabs(bk.d[r] - s));
-                red[5] += fabs(bk.d[r] - s);
+                const double td = -y[r] - vl + vu;
+                red[0] = fmax(red[0], fabs(td));
+                red[8] += fabs(td);
+                double res = bk.d[r] - s;
+                red[9] += fabs(res);
+                if (rs) {
+                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k), zp = c.B(B_ZP + r, j, k),
+                                 zn = c.B(B_ZN + r, j, k);
+                    res -= p - n;
+                    const double t1 = RHO - y[r] - zp, t2 = RHO + y[r] - zn;
+                    red[0] = fmax(red[0], fmax(fabs(t1), fabs(t2)));
+                    red[8] += fabs(t1) + fabs(t2);
+                    red[2] = fmax(red[2], fmax(fabs(p * zp), fabs(n * zn)));
+                    red[3] += zp + zn;
+                    red[4] += zp + zn;
+                    lsum.add(p);
+                    lsum.add(n);
+                    objR += RHO * (p + n);
+                }
+                red[1] = fmax(red[1], fabs(res));
+                red[5] += fabs(res);
                 red[3] += fabs(y[r]) + vu;
                 red[4] += vu;
                 red[2] = fmax(red[2], fabs(vu * (c.rU(r) - s)));
                 lsum.add(c.rU(r) - s);
+                lorig.add(c.rU(r) - s);
                 if (c.hrl(r)) {
                     red[2] = fmax(red[2], fabs(vl * (s - c.rL(r))));
                     red[3] += vl;
                     red[4] += vl;
                     lsum.add(s - c.rL(r));
+                    lorig.add(s - c.rL(r));
                 }
             }
         }
@@ -1441,23 +1960,43 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
                 gl[i] += sh.ydf[i];
                 const double dfi = x[i] - c.tgt_x[i];
                 sh.df[i] = dfi;
-                red[0] = fmax(red[0], fabs(-sh.ydf[i] - sh.vLf[i] + sh.vUf[i]));
-                red[1] = fmax(red[1], fabs(dfi - sh.sf[i]));
-                red[5] += fabs(dfi - sh.sf[i]);
+                const double td = -sh.ydf[i] - sh.vLf[i] + sh.vUf[i];
+                red[0] = fmax(red[0], fabs(td));
+                red[8] += fabs(td);
+                double res = dfi - sh.sf[i];
+                red[9] += fabs(res);
+                if (rs) {
+                    const double p = sh.pf[i], n = sh.nf[i], zp = sh.zpf[i], zn = sh.znf[i];
+                    res -= p - n;
+                    const double t1 = RHO - sh.ydf[i] - zp, t2 = RHO + sh.ydf[i] - zn;
+                    red[0] = fmax(red[0], fmax(fabs(t1), fabs(t2)));
+                    red[8] += fabs(t1) + fabs(t2);
+                    red[2] = fmax(red[2], fmax(fabs(p * zp), fabs(n * zn)));
+                    red[3] += zp + zn;
+                    red[4] += zp + zn;
+                    lsum.add(p);
+                    lsum.add(n);
+                    objR += RHO * (p + n);
+                }
+                red[1] = fmax(red[1], fabs(res));
+                red[5] += fabs(res);
                 const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
                 red[2] = fmax(red[2], fmax(fabs(sh.vLf[i] * sl), fabs(sh.vUf[i] * su)));
                 red[3] += fabs(sh.ydf[i]) + sh.vLf[i] + sh.vUf[i];
                 red[4] += sh.vLf[i] + sh.vUf[i];
                 lsum.add(sl);
                 lsum.add(su);
+                lorig.add(sl);
+                lorig.add(su);
             }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
             gl[i] += -zl + zu;
             red[0] = fmax(red[0], fabs(gl[i]));
-            if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
-            if (c.hux(i)) { const double sl = c.xu[i] - x[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
+            red[8] += fabs(gl[i]);
+            if (c.hlx(i)) { const double sl = x[i] - c.xl[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); lorig.add(sl); }
+            if (c.hux(i)) { const double sl = c.xu[i] - x[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); lorig.add(sl); }
         }
         if (k < N)
 #pragma unroll
@@ -1465,55 +2004,73 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
                 const double zl = c.S(S_ZLU + i, k), zu = c.S(S_ZUU + i, k);
                 const double t = c.S(S_GU + i, k) - a.dt * yn[i == 0 ? 5 : 4] - zl + zu;
                 red[0] = fmax(red[0], fabs(t));
-                if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); }
-                if (c.huu(i)) { const double sl = c.uu[i] - u[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); }
+                red[8] += fabs(t);
+                if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); lorig.add(sl); }
+                if (c.huu(i)) { const double sl = c.uu[i] - u[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); lorig.add(sl); }
             }
-        red[6] += stage_cost(c, k, x, u);
+        const double cost = stage_cost(c, k, x, u);
+        red[6] += rs ? objR : cost;
         red[7] += lsum.value();
+        red[10] += cost;
+        red[11] += lorig.value();
         if (!isfinite(red[0]) || !isfinite(red[1])) red[0] = INFINITY;
     }
-    const int ops[8] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM};
+    const int ops[12] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM};
     wg_reduce(sh, red, ops);
 }
 
-// ======== phase: complementarity vs mu (max |z s - mu|) ========
-__device__ __noinline__ double phase_compl(const Ctx& c, LShared& sh, double mu) {
+// ======== phase: complementarity vs mu: max and sum of |z s - mu| (elastic pairs included) ========
+__device__ __noinline__ double2 phase_compl(const Ctx& c, LShared& sh, double mu) {
     const int N = c.N;
-    double cm[1] = {0.0};
+    const bool rs = sh.R != 0;
+    double cm[2] = {0.0, 0.0};
+    auto acc = [&](double v) { cm[0] = fmax(cm[0], v); cm[1] += v; };
     for (int k = (int)threadIdx.x; k <= N; k += T) {
-        double m = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double xv = c.S(S_X + i, k);
-            if (c.hlx(i)) m = fmax(m, fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
-            if (c.hux(i)) m = fmax(m, fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
+            if (c.hlx(i)) acc(fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
+            if (c.hux(i)) acc(fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
+            if (rs) {
+                acc(fabs(c.S(S_ZP + i, k) * c.S(S_PR + i, k) - mu));
+                acc(fabs(c.S(S_ZN + i, k) * c.S(S_NR + i, k) - mu));
+            }
         }
         if (k < N)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const double uv = c.S(S_U + i, k);
-                if (c.hlu(i)) m = fmax(m, fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
-                if (c.huu(i)) m = fmax(m, fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
+                if (c.hlu(i)) acc(fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
+                if (c.huu(i)) acc(fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
             }
         for (int j = 0; j < c.nbk; ++j) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) m = fmax(m, fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
+            for (int e = 0; e < 8; ++e) acc(fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double s = c.B(B_S + r, j, k);
-                m = fmax(m, fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
-                if (c.hrl(r)) m = fmax(m, fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
+                acc(fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
+                if (c.hrl(r)) acc(fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
+                if (rs) {
+                    acc(fabs(c.B(B_ZP + r, j, k) * c.B(B_PR + r, j, k) - mu));
+                    acc(fabs(c.B(B_ZN + r, j, k) * c.B(B_NR + r, j, k) - mu));
+                }
             }
         }
         if (k == N && c.plan())
 #pragma unroll
-            for (int i = 0; i < 6; ++i)
-                m = fmax(m, fmax(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu), fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu)));
-        cm[0] = fmax(cm[0], m);
+            for (int i = 0; i < 6; ++i) {
+                acc(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu));
+                acc(fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu));
+                if (rs) {
+                    acc(fabs(sh.zpf[i] * sh.pf[i] - mu));
+                    acc(fabs(sh.znf[i] * sh.nf[i] - mu));
+                }
+            }
     }
-    const int ops[1] = {R_MAX};
+    const int ops[2] = {R_MAX, R_SUM};
     wg_reduce(sh, cm, ops);
-    return cm[0];
+    return make_double2(cm[0], cm[1]);
 }
 
 // Newton solve for the current residual arrays (S_CR / B_DR / sh.dfr) with the given dw into buffer buf.
@@ -1524,7 +2081,13 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
     const bool f = phase_factor(c, sh, mu, dw);
     stamp(sh, on, OPH_FACTOR);
     if (!f) return false;
-    if (c.lds) {
+    if (sh.R) {  // soft dynamics rows (restoration phase): HBM operands
+        if (threadIdx.x < 64) riccati_soft(c, sh);
+        __syncthreads();
+        stamp(sh, on, OPH_RIC);
+        if (sh.flag) return false;
+        if (threadIdx.x < 64) forward_soft(c, buf);
+    } else if (c.lds) {
         stage_inputs(c, c.lds);
         __syncthreads();
         stamp(sh, on, OPH_COMPL);  // (diagnostic: staging cost booked under 'compl')
@@ -1546,6 +2109,305 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
     stamp(sh, on, OPH_FWD);
     return true;
 }
+
+// ======== restoration / soft-restoration / acceptable-point bookkeeping (all stage-parallel) ========
+// snapshot of the iterate (save = true) or its restore (soft restoration trial)
+__device__ __noinline__ void phase_snapshot(const Ctx& c, LShared& sh, bool save) {
+    const int N = c.N;
+    auto mv = [&](gdouble& live, gdouble& snap) { if (save) snap = live; else live = snap; };
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+        int o = S_SNAP;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { mv(c.S(S_X + i, k), c.S(o + i, k)); mv(c.S(S_ZLX + i, k), c.S(o + 6 + i, k)); mv(c.S(S_ZUX + i, k), c.S(o + 12 + i, k)); mv(c.S(S_YC + i, k), c.S(o + 18 + i, k)); }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { mv(c.S(S_U + i, k), c.S(o + 24 + i, k)); mv(c.S(S_ZLU + i, k), c.S(o + 26 + i, k)); mv(c.S(S_ZUU + i, k), c.S(o + 28 + i, k)); }
+        for (int j = 0; j < c.nbk; ++j) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { mv(c.B(B_W + e, j, k), c.B(B_SNAP + e, j, k)); mv(c.B(B_ZW + e, j, k), c.B(B_SNAP + 8 + e, j, k)); }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                mv(c.B(B_S + r, j, k), c.B(B_SNAP + 16 + r, j, k));
+                mv(c.B(B_VL + r, j, k), c.B(B_SNAP + 20 + r, j, k));
+                mv(c.B(B_VU + r, j, k), c.B(B_SNAP + 24 + r, j, k));
+                mv(c.B(B_YD + r, j, k), c.B(B_SNAP + 28 + r, j, k));
+            }
+        }
+        if (k == N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                if (save) { sh.snapf[i] = sh.sf[i]; sh.snapf[6 + i] = sh.vLf[i]; sh.snapf[12 + i] = sh.vUf[i]; sh.snapf[18 + i] = sh.ydf[i]; }
+                else { sh.sf[i] = sh.snapf[i]; sh.vLf[i] = sh.snapf[6 + i]; sh.vUf[i] = sh.snapf[12 + i]; sh.ydf[i] = sh.snapf[18 + i]; }
+            }
+    }
+}
+
+// last acceptable iterate (IPOPT's stored acceptable point): store (x, u, w) or restore it
+__device__ __noinline__ void phase_acc(const Ctx& c, bool restore) {
+    for (int k = (int)threadIdx.x; k <= c.N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (restore) c.S(S_X + i, k) = c.S(S_XACC + i, k); else c.S(S_XACC + i, k) = c.S(S_X + i, k);
+        }
+        if (k < c.N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (restore) c.S(S_U + i, k) = c.S(S_UACC + i, k); else c.S(S_UACC + i, k) = c.S(S_U + i, k);
+            }
+        for (int j = 0; j < c.nbk; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (restore) c.B(B_W + e, j, k) = c.B(B_WACC + e, j, k); else c.B(B_WACC + e, j, k) = c.B(B_W + e, j, k);
+            }
+    }
+}
+
+__device__ __forceinline__ double dr2(double v) { const double d = fmin(1.0, 1.0 / fabs(v)); return d * d; }
+
+// elastic pairs at their closed form for the raw rows at the iterate (entry; restoration of the restoration)
+__device__ __noinline__ void phase_setpn(const Ctx& c, LShared& sh, double mu) {
+    const int N = c.N;
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double p, n;
+            pn_closed_form(c.S(S_C + i, k), mu, p, n);
+            c.S(S_PR + i, k) = p;
+            c.S(S_NR + i, k) = n;
+            c.S(S_ZP + i, k) = mu / p;
+            c.S(S_ZN + i, k) = mu / n;
+        }
+        for (int j = 0; j < c.nbk; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double p, n;
+                pn_closed_form(c.B(B_D + r, j, k) - c.B(B_S + r, j, k), mu, p, n);
+                c.B(B_PR + r, j, k) = p;
+                c.B(B_NR + r, j, k) = n;
+                c.B(B_ZP + r, j, k) = mu / p;
+                c.B(B_ZN + r, j, k) = mu / n;
+            }
+        if (k == N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double p, n;
+                pn_closed_form(sh.df[i] - sh.sf[i], mu, p, n);
+                sh.pf[i] = p;
+                sh.nf[i] = n;
+                sh.zpf[i] = mu / p;
+                sh.znf[i] = mu / n;
+            }
+    }
+}
+
+// enter the restoration phase at the (linearised, original) iterate: reference point and D_R^2, saved
+// bound multipliers, elastic pairs, bound multipliers clipped to rho, constraint multipliers 0
+__device__ __noinline__ void phase_enter_resto(const Ctx& c, LShared& sh, double muR) {
+    const int N = c.N;
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double x = c.S(S_X + i, k);
+            c.S(S_XR + i, k) = x;
+            c.S(S_DRX + i, k) = dr2(x);
+            const double zl = c.S(S_ZLX + i, k), zu = c.S(S_ZUX + i, k);
+            c.S(S_SZ + i, k) = zl;
+            c.S(S_SZ + 6 + i, k) = zu;
+            c.S(S_ZLX + i, k) = fmin(zl, RHO);
+            c.S(S_ZUX + i, k) = fmin(zu, RHO);
+            c.S(S_YC + i, k) = 0.0;
+        }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double u = c.S(S_U + i, k);
+                c.S(S_UR + i, k) = u;
+                c.S(S_DRU + i, k) = dr2(u);
+                const double zl = c.S(S_ZLU + i, k), zu = c.S(S_ZUU + i, k);
+                c.S(S_SZ + 12 + i, k) = zl;
+                c.S(S_SZ + 14 + i, k) = zu;
+                c.S(S_ZLU + i, k) = fmin(zl, RHO);
+                c.S(S_ZUU + i, k) = fmin(zu, RHO);
+            }
+        for (int j = 0; j < c.nbk; ++j) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const double w = c.B(B_W + e, j, k), z = c.B(B_ZW + e, j, k);
+                c.B(B_WR + e, j, k) = w;
+                c.B(B_DRW + e, j, k) = dr2(w);
+                c.B(B_SZW + e, j, k) = z;
+                c.B(B_ZW + e, j, k) = fmin(z, RHO);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                c.B(B_SR + r, j, k) = c.B(B_S + r, j, k);
+                const double vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+                c.B(B_SVL + r, j, k) = vl;
+                c.B(B_SVU + r, j, k) = vu;
+                c.B(B_VL + r, j, k) = fmin(vl, RHO);
+                c.B(B_VU + r, j, k) = fmin(vu, RHO);
+                c.B(B_YD + r, j, k) = 0.0;
+            }
+        }
+        if (k == N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                sh.sfR[i] = sh.sf[i];
+                sh.svLf[i] = sh.vLf[i];
+                sh.svUf[i] = sh.vUf[i];
+                sh.vLf[i] = fmin(sh.vLf[i], RHO);
+                sh.vUf[i] = fmin(sh.vUf[i], RHO);
+                sh.ydf[i] = 0.0;
+            }
+    }
+    phase_setpn(c, sh, muR);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sh.R = 1;
+        sh.zeta = sqrt(muR);
+    }
+    __syncthreads();
+}
+
+// leave the restoration phase: original bound multipliers advanced by the complementarity Newton step of
+// the whole restoration change (fraction to the boundary tau), kappa_sigma safeguard, all reset to 1 when
+// one exceeds 1000; constraint multipliers 0
+__device__ __noinline__ void phase_leave_resto(const Ctx& c, LShared& sh, double mu, double tau) {
+    const int N = c.N;
+    double red[1] = {1.0};
+    // dz of a lower-bound multiplier z0 whose slack moved from sl0 by d
+    auto dzl = [&](double z0, double sl0, double d) { return mu / sl0 - z0 - z0 / sl0 * d; };
+    for (int pass = 0; pass < 2; ++pass) {
+        double acc = pass == 0 ? 1.0 : 0.0;  // pass 0: fraction to the boundary; pass 1: max multiplier
+        const double al = red[0];
+        auto use = [&](double z0, double dz, gdouble& z, double slnew) {
+            if (pass == 0) { if (dz < 0.0) acc = fmin(acc, -tau * z0 / dz); }
+            else { double zn = z0 + al * dz; clamp_mult(zn, slnew, mu); z = zn; acc = fmax(acc, zn); }
+        };
+        for (int k = (int)threadIdx.x; k <= N; k += T) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double x = c.S(S_X + i, k), xr = c.S(S_XR + i, k), d = x - xr;
+                if (c.hlx(i)) { const double z0 = c.S(S_SZ + i, k); use(z0, dzl(z0, xr - c.xl[i], d), c.S(S_ZLX + i, k), x - c.xl[i]); }
+                if (c.hux(i)) { const double z0 = c.S(S_SZ + 6 + i, k); use(z0, dzl(z0, c.xu[i] - xr, -d), c.S(S_ZUX + i, k), c.xu[i] - x); }
+            }
+            if (k < N)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const double u = c.S(S_U + i, k), ur = c.S(S_UR + i, k), d = u - ur;
+                    if (c.hlu(i)) { const double z0 = c.S(S_SZ + 12 + i, k); use(z0, dzl(z0, ur - c.ul[i], d), c.S(S_ZLU + i, k), u - c.ul[i]); }
+                    if (c.huu(i)) { const double z0 = c.S(S_SZ + 14 + i, k); use(z0, dzl(z0, c.uu[i] - ur, -d), c.S(S_ZUU + i, k), c.uu[i] - u); }
+                }
+            for (int j = 0; j < c.nbk; ++j) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const double w = c.B(B_W + e, j, k), wr = c.B(B_WR + e, j, k), z0 = c.B(B_SZW + e, j, k);
+                    use(z0, dzl(z0, wr + RELAX, w - wr), c.B(B_ZW + e, j, k), w + RELAX);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double s = c.B(B_S + r, j, k), sr = c.B(B_SR + r, j, k), d = s - sr;
+                    if (c.hrl(r)) { const double z0 = c.B(B_SVL + r, j, k); use(z0, dzl(z0, sr - c.rL(r), d), c.B(B_VL + r, j, k), s - c.rL(r)); }
+                    const double z0 = c.B(B_SVU + r, j, k);
+                    use(z0, dzl(z0, c.rU(r) - sr, -d), c.B(B_VU + r, j, k), c.rU(r) - s);
+                }
+            }
+            if (k == N && c.plan())
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const double s = sh.sf[i], sr = sh.sfR[i], d = s - sr;
+                    const double dl = dzl(sh.svLf[i], sr - c.fL, d), du = dzl(sh.svUf[i], c.fU - sr, -d);
+                    if (pass == 0) {
+                        if (dl < 0.0) acc = fmin(acc, -tau * sh.svLf[i] / dl);
+                        if (du < 0.0) acc = fmin(acc, -tau * sh.svUf[i] / du);
+                    } else {
+                        double vl = sh.svLf[i] + al * dl, vu = sh.svUf[i] + al * du;
+                        clamp_mult(vl, s - c.fL, mu);
+                        clamp_mult(vu, c.fU - s, mu);
+                        sh.vLf[i] = vl;
+                        sh.vUf[i] = vu;
+                        acc = fmax(acc, fmax(vl, vu));
+                    }
+                }
+        }
+        red[0] = acc;
+        const int ops[1] = {pass == 0 ? R_MIN : R_MAX};
+        wg_reduce(sh, red, ops);
+    }
+    const bool reset = red[0] > BOUND_MULT_RESET;
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            if (reset) {
+                c.S(S_ZLX + i, k) = c.hlx(i) ? 1.0 : 0.0;
+                c.S(S_ZUX + i, k) = c.hux(i) ? 1.0 : 0.0;
+            }
+            c.S(S_YC + i, k) = 0.0;
+        }
+        if (k < N && reset)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                c.S(S_ZLU + i, k) = c.hlu(i) ? 1.0 : 0.0;
+                c.S(S_ZUU + i, k) = c.huu(i) ? 1.0 : 0.0;
+            }
+        for (int j = 0; j < c.nbk; ++j) {
+            if (reset)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) c.B(B_ZW + e, j, k) = 1.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (reset) {
+                    c.B(B_VL + r, j, k) = c.hrl(r) ? 1.0 : 0.0;
+                    c.B(B_VU + r, j, k) = 1.0;
+                }
+                c.B(B_YD + r, j, k) = 0.0;
+            }
+        }
+        if (k == N && c.plan())
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                if (reset) sh.vLf[i] = sh.vUf[i] = 1.0;
+                sh.ydf[i] = 0.0;
+            }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sh.R = 0;
+    __syncthreads();
+}
+
+// least-squares constraint multipliers of the current NLP (IPOPT constr_mult_init_max = 1000):
+// [[I, J'], [J, 0]] [d; y] = [-(grad f - z); 0] with unit slack / elastic Hessians; kept when max |y| <= 1000
+__device__ __noinline__ void ls_multipliers(const Ctx& c, LShared& sh) {
+    if (threadIdx.x == 0) sh.lsq = 1;
+    __syncthreads();
+    double red[12];
+    phase_lin(c, sh, red);  // Jacobians at the iterate (y = 0: no curvature terms)
+    phase_resid(c, sh, true);
+    __syncthreads();
+    if (newton_solve(c, sh, 0.0, 0.0, 0)) {
+        double rec[5];
+        phase_recover(c, sh, 0.0, 0.0, 0.99, 0, rec);
+        if (isfinite(rec[4]) && rec[4] <= CONSTR_MULT_INIT_MAX) {
+            for (int k = (int)threadIdx.x; k <= c.N; k += T) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) c.S(S_YC + i, k) = c.S(S_YCP + i, k);
+                for (int j = 0; j < c.nbk; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) c.B(B_YD + r, j, k) = c.B(B_YP + r, j, k);
+                if (k == c.N && c.plan())
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) sh.ydf[i] = sh.ydpf[0][i];
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sh.lsq = 0;
+    __syncthreads();
+}
+
+struct IpmState {
+    double mu, tau, th_max, th_min, dw_last;
+    int acc;
+};
 
 // ---------------- the kernel ----------------
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void obca_kernel(ObcaArgs args) {
@@ -1610,6 +2472,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     if (tid == 0) {
         for (int i = 0; i < kObcaPhases; ++i) sh.stamp[i] = 0;
         sh.t0 = clock64();
+        sh.R = 0;
+        sh.lsq = 0;
+        sh.zeta = 0.0;
+        sh.nfl[0] = sh.nfl[1] = 0;
     }
     const unsigned long long tstart = clock64();
     // ---------------- initial point (bound push, slacks = pushed d(x0), multipliers 1 / 0) ----------------
@@ -1617,7 +2483,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
 #pragma unroll
     for (int i = 0; i < 6; ++i)
         if (!isfinite(xinit[i]) || (c.hlx(i) && xinit[i] < c.xl[i]) || (c.hux(i) && xinit[i] > c.xu[i])) infeasible = true;
-    if (tid == 0) sh.nf = 0;
+    __syncthreads();
     for (int k = tid; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0};
 #pragma unroll
@@ -1706,146 +2572,272 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         for (int i = 0; i < 2; ++i) nub += c.hlu(i) + c.huu(i);
         const double n_bounds = (double)(N + 1) * nxb + (double)N * nub + (double)(N + 1) * NBK * 14 + (plan ? 12 : 0);
         const double n_rows = 6.0 * (N + 1) + 4.0 * (N + 1) * NBK + (plan ? 6 : 0);
-        double mu = 0.1, tau = fmax(0.99, 1.0 - mu), dw_last = 0.0, th_max = 0.0, th_min = 0.0;
-        int acc_count = 0;
-        const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+        const bool use_resto = !(a.opts & OBCA_OPT_NO_RESTO), use_soft = !(a.opts & OBCA_OPT_NO_SOFT_RESTO);
+        const bool use_lsq = !(a.opts & OBCA_OPT_NO_LSQ_MULT);
+        if (use_lsq) ls_multipliers(cs, sh);
+        IpmState S0, S1;
+        S0.mu = 0.1; S0.tau = fmax(0.99, 1.0 - 0.1); S0.th_max = S0.th_min = 0.0; S0.dw_last = 0.0; S0.acc = 0;
+        S1 = S0;
+        int in_soft = 0, soft_cnt = 0, first_resto = 0, resto_iter0 = 0, have_acc = 0;
+        double th_resto0 = 0.0;
+        const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, smax = 100.0;
         const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
+        const double tolc = 10.0 * EPS;
         for (iter = 0;; ++iter) {
-            double red[8];
-            stamp(sh, ston, OPH_UPD);
-            phase_lin(cs, sh, red);
-            stamp(sh, ston, OPH_LIN);
-            const double dinf = red[0], pinf = red[1], c0 = red[2];
-            const double th0 = red[5];
-            if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; break; }
-            const double smax = 100.0;
-            const double sd = fmax(smax, red[3] / (n_rows + n_bounds)) / smax;
-            const double sc = fmax(smax, red[4] / n_bounds) / smax;
-            E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
-            if (E0 <= a.tol) { status = 0; break; }
-            if (E0 <= a.acc_tol) {
-                if (++acc_count >= a.acc_iter) { status = 1; break; }
-            } else {
-                acc_count = 0;
-            }
-            if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; break; }
-            // ---- barrier update (monotone, Fiacco-McCormick) ----
-            while (mu > a.tol / 10.0 * 1.0000001) {
-                const double Emu = fmax(fmax(dinf / sd, pinf), phase_compl(cs, sh, mu) / sc);
-                stamp(sh, ston, OPH_COMPL);
-                if (!(Emu <= kappa_eps * mu)) break;
-                mu = fmax(a.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
-                tau = fmax(0.99, 1.0 - mu);
-                __syncthreads();
-                if (tid == 0) sh.nf = 0;  // IPOPT resets the filter on every barrier update
-            }
-            const double phi0 = red[6] - mu * red[7];
-            // ---- residual arrays of the Newton right-hand side: c, d - s, d_f - s_f ----
-            for (int k = tid; k <= N; k += T) {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = c.S(S_C + i, k);
-                for (int j = 0; j < NBK; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = c.B(B_D + r, j, k) - c.B(B_S + r, j, k);
-                if (k == N && plan)
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) sh.dfr[i] = sh.df[i] - sh.sf[i];
-            }
-            __syncthreads();
-            // ---- Newton step with inertia correction (IPOPT delta_w schedule) ----
-            double dw = 0.0;
-            bool ok = false;
-            for (int attempt = 0; attempt < 40; ++attempt) {
-                if (newton_solve(cs, sh, mu, dw, 0)) { ok = true; break; }
-                dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0)) : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-                if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
-            }
-            if (!ok) { status = 5; break; } /* IPOPT Error_In_Step_Computation */
-            if (dw > 0) dw_last = dw;
-            double rec[4];
-            phase_recover(cs, sh, mu, dw, tau, 0, rec);
-            stamp(sh, ston, OPH_REC);
-            const double ap = rec[0], Dm = rec[2], rel = rec[3];
-            double az = rec[1];
-            // ---- filter line search ----
-            if (iter == 0 || !(th_max > 0)) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
-            double amin;
-            if (Dm < 0.0) {
-                amin = fmin(g_th, g_ph * th0 / (-Dm));
-                if (th0 <= th_min) amin = fmin(amin, delta * pow(th0, s_th) / pow(-Dm, s_ph));
-            } else {
-                amin = g_th;
-            }
-            amin *= g_al;
-            const double tolc = 10.0 * EPS;
-            double alpha = ap;
-            int buf = 0;
-            bool accepted = rel < 1e-15;
-            bool ftype = false;
-            for (int ls = 0; !accepted; ++ls) {
-                double tr[3];
-                phase_trial(cs, sh, mu, alpha, 0, tr);
-                stamp(sh, ston, OPH_TRIAL);
-                const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
-                bool okls = false;
-                if (isfinite(tr[1]) && tr[0] <= th_max && !in_filter(sh, tr[0], tr[1])) {
-                    if (th0 <= th_min && sw) { ftype = true; okls = tr[1] - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
-                    else { ftype = false; okls = tr[0] <= (1.0 - g_th) * th0 || tr[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+            const int R = sh.R;
+            IpmState stt = R ? S1 : S0;
+            bool done = false, redo = false, switched = false;
+            do {
+                double red[12];
+                stamp(sh, ston, OPH_UPD);
+                phase_lin(cs, sh, red);
+                stamp(sh, ston, OPH_LIN);
+                double dinf = red[0], pinf = red[1], c0 = red[2];
+                if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; done = true; break; }
+                const double nbd = n_bounds + (R ? 2.0 * n_rows : 0.0);
+                double sd = fmax(smax, red[3] / (n_rows + nbd)) / smax, sc = fmax(smax, red[4] / nbd) / smax;
+                E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
+                if (!R) {
+                    if (E0 <= a.tol) { status = 0; done = true; break; }
+                    if (E0 <= a.acc_tol) {
+                        phase_acc(cs, false);
+                        have_acc = 1;
+                        if (++stt.acc >= a.acc_iter) { status = 1; done = true; break; }
+                    } else {
+                        stt.acc = 0;
+                    }
+                    if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; done = true; break; }
+                } else {
+                    // restoration convergence: original infeasibility down to kappa_resto of its value at entry and
+                    // the point acceptable to the augmented original filter
+                    const double thO = red[9], phO = red[10] - S0.mu * red[11];
+                    if (!first_resto && thO <= KAPPA_RESTO * th_resto0 && thO <= S0.th_max && !in_filter(sh, 0, thO, phO)) {
+                        phase_leave_resto(cs, sh, S0.mu, S0.tau);
+                        S1 = stt;
+                        S0.acc = 0;
+                        switched = true;
+                        redo = true;
+                        break;
+                    }
+                    first_resto = 0;
+                    if (E0 <= a.acc_tol) ++stt.acc; else stt.acc = 0;
+                    if (E0 <= a.tol || stt.acc >= a.acc_iter) {
+                        if (pinf <= 1e2 * a.tol || thO <= 1e2 * a.tol) {  // feasible but filter-unacceptable
+                            phase_leave_resto(cs, sh, S0.mu, S0.tau);
+                            if (tid == 0) sh.nfl[0] = 0;
+                            __syncthreads();
+                            S1 = stt;
+                            S0.acc = 0;
+                            switched = true;
+                            redo = true;
+                            break;
+                        }
+                        status = 3;  // converged to a point of local infeasibility
+                        done = true;
+                        break;
+                    }
+                    if (iter >= a.max_iter) { status = 2; done = true; break; }
                 }
-                if (okls) { accepted = true; break; }
-                if (ls == 0 && isfinite(tr[1]) && tr[0] >= th0) {
-                    // second-order corrections into step buffer 1
-                    for (int k = tid; k <= N; k += T) {
-#pragma unroll
-                        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = c.S(S_C + i, k);
-                        for (int j = 0; j < NBK; ++j)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = c.B(B_D + r, j, k) - c.B(B_S + r, j, k);
-                        if (k == N && plan)
-#pragma unroll
-                            for (int i = 0; i < 6; ++i) sh.dfr[i] = sh.df[i] - sh.sf[i];
+                // ---- barrier update (monotone, Fiacco-McCormick); the filter is reset on every change ----
+                while (stt.mu > a.tol / 10.0 * 1.0000001) {
+                    const double2 cm = phase_compl(cs, sh, stt.mu);
+                    stamp(sh, ston, OPH_COMPL);
+                    if (!(fmax(fmax(dinf / sd, pinf), cm.x / sc) <= kappa_eps * stt.mu)) break;
+                    stt.mu = fmax(a.tol / 10.0, fmin(kappa_mu * stt.mu, pow(stt.mu, theta_mu)));
+                    stt.tau = fmax(0.99, 1.0 - stt.mu);
+                    __syncthreads();
+                    if (tid == 0) {
+                        sh.nfl[R] = 0;
+                        if (R) sh.zeta = sqrt(stt.mu);
                     }
                     __syncthreads();
-                    double a_soc = alpha, th_old = th0, th_t = tr[0];
-                    bool soc_ok = false;
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        if (p > 0 && th_t > 0.99 * th_old) break;
-                        th_old = th_t;
-                        phase_soc_resid(cs, sh, a_soc);
-                        __syncthreads();
-                        if (!newton_solve(cs, sh, mu, dw, 1)) break;
-                        double rs[4];
-                        phase_recover(cs, sh, mu, dw, tau, 1, rs);
-                        stamp(sh, ston, OPH_REC);
-                        a_soc = rs[0];
-                        double t2[3];
-                        phase_trial(cs, sh, mu, a_soc, 1, t2);
-                        stamp(sh, ston, OPH_TRIAL);
-                        th_t = t2[0];
-                        bool ok2 = false;
-                        if (isfinite(t2[1]) && t2[0] <= th_max && !in_filter(sh, t2[0], t2[1])) {
-                            if (th0 <= th_min && sw) { ftype = true; ok2 = t2[1] - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
-                            else { ftype = false; ok2 = t2[0] <= (1.0 - g_th) * th0 || t2[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
-                        }
-                        if (ok2) { soc_ok = true; az = rs[1]; break; }
-                        if (!isfinite(t2[1])) break;
+                    if (R) {  // the proximity weight changed: gradient and optimality error with it
+                        phase_lin(cs, sh, red);
+                        dinf = red[0]; pinf = red[1]; c0 = red[2];
+                        sd = fmax(smax, red[3] / (n_rows + nbd)) / smax;
+                        sc = fmax(smax, red[4] / nbd) / smax;
                     }
-                    if (soc_ok) { accepted = true; alpha = a_soc; buf = 1; break; }
                 }
-                if (alpha * 0.5 < amin) break;
-                alpha *= 0.5;
+                const double mu = stt.mu;
+                const double th0 = red[5], phi0 = red[6] - mu * red[7];
+                phase_resid(cs, sh, false);
+                __syncthreads();
+                // ---- Newton step with inertia correction (IPOPT delta_w schedule) ----
+                double dw = 0.0;
+                bool ok = false;
+                for (int attempt = 0; attempt < 40; ++attempt) {
+                    if (newton_solve(cs, sh, mu, dw, 0)) { ok = true; break; }
+                    dw = (dw == 0.0) ? (stt.dw_last == 0.0 ? 1e-4 : fmax(1e-20, stt.dw_last / 3.0))
+                                     : (stt.dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
+                    if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
+                }
+                bool go_resto = false;
+                if (!ok) {
+                    if (R || !use_resto) { status = 5; done = true; break; } /* Error_In_Step_Computation */
+                    go_resto = true;                                         /* IPOPT's fallback: restoration */
+                } else {
+                    if (dw > 0) stt.dw_last = dw;
+                    double rec[5];
+                    phase_recover(cs, sh, mu, dw, stt.tau, 0, rec);
+                    stamp(sh, ston, OPH_REC);
+                    const double ap = rec[0], Dm = rec[2], rel = rec[3];
+                    double az = rec[1], alpha = ap;
+                    int buf = 0;
+                    bool accepted = false, ftype = false;
+                    if (R || !in_soft) {
+                        // ---- filter line search ----
+                        const bool first = (R ? iter == resto_iter0 : iter == 0) || !(stt.th_max > 0);
+                        if (first) { stt.th_max = 1e4 * fmax(1.0, th0); stt.th_min = 1e-4 * fmax(1.0, th0); }
+                        double amin;
+                        if (Dm < 0.0) {
+                            amin = fmin(g_th, g_ph * th0 / (-Dm));
+                            if (th0 <= stt.th_min) amin = fmin(amin, delta * pow(th0, s_th) / pow(-Dm, s_ph));
+                        } else {
+                            amin = g_th;
+                        }
+                        amin *= g_al;
+                        accepted = rel < 1e-15;
+                        for (int ls = 0; !accepted; ++ls) {
+                            double tr[3];
+                            phase_trial(cs, sh, mu, alpha, 0, tr);
+                            stamp(sh, ston, OPH_TRIAL);
+                            const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
+                            bool okls = false;
+                            if (isfinite(tr[1]) && tr[0] <= stt.th_max && !in_filter(sh, R, tr[0], tr[1])) {
+                                if (th0 <= stt.th_min && sw) { ftype = true; okls = tr[1] - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+                                else { ftype = false; okls = tr[0] <= (1.0 - g_th) * th0 || tr[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+                            }
+                            if (okls) { accepted = true; break; }
+                            if (ls == 0 && isfinite(tr[1]) && tr[0] >= th0) {
+                                // second-order corrections into step buffer 1
+                                phase_resid(cs, sh, false);
+                                __syncthreads();
+                                double a_soc = alpha, th_old = th0, th_t = tr[0];
+                                bool soc_ok = false;
+#pragma unroll 1
+                                for (int p = 0; p < 4; ++p) {
+                                    if (p > 0 && th_t > 0.99 * th_old) break;
+                                    th_old = th_t;
+                                    phase_soc_resid(cs, sh, a_soc);
+                                    __syncthreads();
+                                    if (!newton_solve(cs, sh, mu, dw, 1)) break;
+                                    double rs[5];
+                                    phase_recover(cs, sh, mu, dw, stt.tau, 1, rs);
+                                    stamp(sh, ston, OPH_REC);
+                                    a_soc = rs[0];
+                                    double t2[3];
+                                    phase_trial(cs, sh, mu, a_soc, 1, t2);
+                                    stamp(sh, ston, OPH_TRIAL);
+                                    th_t = t2[0];
+                                    bool ok2 = false;
+                                    if (isfinite(t2[1]) && t2[0] <= stt.th_max && !in_filter(sh, R, t2[0], t2[1])) {
+                                        if (th0 <= stt.th_min && sw) { ftype = true; ok2 = t2[1] - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+                                        else { ftype = false; ok2 = t2[0] <= (1.0 - g_th) * th0 || t2[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+                                    }
+                                    if (ok2) { soc_ok = true; az = rs[1]; break; }
+                                    if (!isfinite(t2[1])) break;
+                                }
+                                if (soc_ok) { accepted = true; alpha = a_soc; buf = 1; break; }
+                            }
+                            if (alpha * 0.5 < amin) break;
+                            alpha *= 0.5;
+                        }
+                        __syncthreads();
+                        if (accepted && !ftype && tid == 0) add_filter(sh, R, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+                        __syncthreads();
+                    }
+                    if (!accepted && !R && use_soft && (in_soft ? ++soft_cnt <= MAX_SOFT_RESTO : true)) {
+                        // ---- soft restoration step: primal and dual step min(alpha_p, alpha_d), accepted when
+                        // acceptable to the filter or when the primal-dual error at mu drops by 0.9999 ----
+                        const double as = fmin(rec[0], rec[1]);
+                        double tr[3];
+                        phase_trial(cs, sh, mu, as, 0, tr);
+                        const bool orig_ok = isfinite(tr[1]) && tr[0] <= stt.th_max && !in_filter(sh, 0, tr[0], tr[1]) &&
+                                             (tr[0] <= (1.0 - g_th) * th0 || tr[1] - (phi0 - g_ph * th0) <= tolc * fabs(phi0));
+                        bool acc_soft = orig_ok;
+                        if (!orig_ok && isfinite(tr[1])) {
+                            const double pd_cur = red[8] + red[5] + phase_compl(cs, sh, mu).y;
+                            phase_snapshot(cs, sh, true);
+                            __syncthreads();
+                            phase_update(cs, sh, mu, as, as, 0);
+                            __syncthreads();
+                            double rt[12];
+                            phase_lin(cs, sh, rt);
+                            const double pd_t = rt[8] + rt[5] + phase_compl(cs, sh, mu).y;
+                            const bool fin = isfinite(rt[0]) && isfinite(rt[1]);
+                            phase_snapshot(cs, sh, false);
+                            __syncthreads();
+                            phase_lin(cs, sh, red);  // the restored iterate's linearisation (restoration needs it)
+                            pinf = red[1];
+                            acc_soft = fin && pd_t <= SOFT_RESTO_FACTOR * pd_cur;
+                        }
+                        if (acc_soft) {
+                            __syncthreads();
+                            if (tid == 0) add_filter(sh, 0, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+                            __syncthreads();
+                            in_soft = orig_ok ? 0 : 1;
+                            if (orig_ok) soft_cnt = 0;
+                            phase_update(cs, sh, mu, as, as, 0);
+                            __syncthreads();
+                            break;
+                        }
+                    }
+                    if (!accepted) {
+                        if (R) {  // restoration of the restoration phase: elastic pairs back to their closed form
+                            phase_setpn(cs, sh, mu);
+                            __syncthreads();
+                            if (tid == 0) sh.nfl[1] = 0;
+                            __syncthreads();
+                            break;
+                        }
+                        if (!use_resto) {  // diagnostics only: the round-1 fallback (last trial step, filter reset)
+                            __syncthreads();
+                            if (tid == 0) sh.nfl[0] = 0;
+                            __syncthreads();
+                            phase_update(cs, sh, mu, alpha, az, buf);
+                            __syncthreads();
+                            break;
+                        }
+                        go_resto = true;
+                    } else {
+                        phase_update(cs, sh, mu, alpha, az, buf);
+                        __syncthreads();
+                        stamp(sh, ston, OPH_UPD);
+                    }
+                }
+                if (go_resto) {
+                    in_soft = 0;
+                    soft_cnt = 0;
+                    if (th0 <= 1e-2 * a.tol) {  // almost feasible: acceptable point or Restoration_Failed
+                        if (have_acc) { phase_acc(cs, true); status = 1; } else { status = 3; }
+                        done = true;
+                        break;
+                    }
+                    __syncthreads();
+                    if (tid == 0 && isfinite(phi0)) add_filter(sh, 0, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+                    __syncthreads();
+                    if (!(stt.th_max > 0)) { stt.th_max = 1e4 * fmax(1.0, th0); stt.th_min = 1e-4 * fmax(1.0, th0); }
+                    th_resto0 = th0;
+                    const double muR = fmax(stt.mu, pinf);
+                    phase_enter_resto(cs, sh, muR);
+                    if (use_lsq) ls_multipliers(cs, sh);
+                    S0 = stt;
+                    S1.mu = muR; S1.tau = fmax(0.99, 1.0 - muR); S1.th_max = S1.th_min = 0.0; S1.dw_last = 0.0; S1.acc = 0;
+                    if (tid == 0) sh.nfl[1] = 0;
+                    __syncthreads();
+                    first_resto = 1;
+                    resto_iter0 = iter;
+                    switched = true;
+                    redo = true;
+                    break;
+                }
+            } while (0);
+            if (!switched) {
+                if (R) S1 = stt;
+                else S0 = stt;
             }
-            __syncthreads();
-            if (!accepted) {
-                if (tid == 0) sh.nf = 0;  // IPOPT would enter restoration here
-            } else if (!ftype) {
-                if (tid == 0) add_filter(sh, (1.0 - g_th) * th0, phi0 - g_ph * th0);
-            }
-            __syncthreads();
-            phase_update(cs, sh, mu, alpha, az, buf);
-            __syncthreads();
-            stamp(sh, ston, OPH_UPD);
+            if (done) break;
+            if (redo) --iter;
         }
     }
     // ---------------- outputs ----------------
@@ -1888,12 +2880,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
 hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream) {
     if (a.B <= 0) return hipSuccess;
     const size_t need = obca_lds_bytes(a.N);
-    const size_t bytes = need <= kObcaLdsMax ? need : 0;
-    static size_t configured = 0;
-    if (bytes > 64 * 1024 && configured < bytes) {
-        hipError_t e = hipFuncSetAttribute((const void*)obca_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    const int bytes = (int)(need <= kObcaLdsMax ? need : 0);
+    // the >64 KB dynamic-LDS opt-in is a per-device function attribute: set it on every such launch
+    if (bytes > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)obca_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
-        configured = bytes;
     }
     hipLaunchKernelGGL(obca_kernel, dim3(a.B), dim3(T), bytes, stream, a);
     return hipGetLastError();

@@ -233,7 +233,7 @@ class ObcaSolver:
     (MPCTrackingControlObs).  obstacles: (M,4) array of (cx, cy, w, h)."""
 
     def __init__(self, N, params, Q, R, xlb, xub, ulb, uub, obstacles, variant=TT_VARIANT_OBCA_PLAN, tol=0.0,
-                 acc_tol=0.0, max_iter=0, acc_iter=0, dual_init=True, device=None):
+                 acc_tol=0.0, max_iter=0, acc_iter=0, dual_init=False, device=None):
         ob = _f64(obstacles).reshape(-1, 4)
         cfg = TTConfig()
         cfg.nx, cfg.nu, cfg.N, cfg.M = 6, 2, int(N), int(ob.shape[0])

@@ -19,7 +19,7 @@ from .trajectory_planning import TrajectoryPlanning
 class MPCTrackingControlObs(TrajectoryPlanning):
     _ipopt = {"max_iter": 5000}
 
-    def __init__(self, dynamics, params, Q, R, state_bound, input_bound, obstacle_list=None, dual_init=True,
+    def __init__(self, dynamics, params, Q, R, state_bound, input_bound, obstacle_list=None, dual_init=False,
                  device=None):
         self.obstacle_list = list(obstacle_list) if obstacle_list is not None else []
         self._obstacles = scenarios.obstacles_array(self.obstacle_list) if self.obstacle_list else None

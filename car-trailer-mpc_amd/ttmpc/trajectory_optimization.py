@@ -6,11 +6,15 @@ plan(initial_state, goal_state) -> (states (6,N+1), inputs (2,N)); plan_batch() 
 one launch.  IPOPT options of the reference (trajectory_optimization.py:196-199): max_iter 5000, the
 rest IPOPT defaults (tol 1e-8, acceptable 1e-6 x 15).
 
-Initial guess: the reference's plan() always builds it from ../initialize.json
-(_hybrid_a_star_initial_trajectory, trajectory_optimization.py:227-274), ignoring plan()'s arguments
-for the guess.  The mirror does the same when ``initialize_path`` is given (or TTMPC_INITIALIZE is
-set); without one it uses the linear start-goal guess of _generate_initial_trajectory_guess (209-225).
+Initial guess: like the reference, plan() always builds it from initialize.json
+(_hybrid_a_star_initial_trajectory, trajectory_optimization.py:227-274, reading ../initialize.json at
+232-234), ignoring plan()'s arguments for the guess.  The file is ``initialize_path`` if given, else
+$TTMPC_INITIALIZE, else ../initialize.json (the reference's location relative to python-files/, the
+directory its scripts run from), else ./initialize.json; a missing file raises FileNotFoundError as the
+reference's open() does.  Duals start at the reference's mu = 100, lam = kron(1_M, [100, 105, 110, 115,
+...]) (222, 260-261); dual_init=True opts into the separating-axis certificate start instead.
 Like the reference (326-331) plan() does not check success; ``last_status`` exposes it.
+``optimize`` is an alias of ``plan`` (the entry point name BASELINE.json's north star uses).
 """
 from __future__ import annotations
 
@@ -28,7 +32,7 @@ class TrajectoryOptimization(TrajectoryPlanning):
     _ipopt = {"max_iter": 5000}
 
     def __init__(self, dynamics, params, Q, R, state_bound, input_bound, obstacle_list, initialize_path=None,
-                 dual_init=True, device=None):
+                 dual_init=False, device=None):
         self.obstacle_list = list(obstacle_list)
         if len(self.obstacle_list) == 0:
             raise ValueError("TrajectoryOptimization needs at least one obstacle (trajectory_optimization.py:25-26)")
@@ -67,9 +71,16 @@ class TrajectoryOptimization(TrajectoryPlanning):
         z[N * st + 6:] = duals
         return z
 
+    def _initialize_file(self, initialize_path=None):
+        for cand in (initialize_path, self._initialize_path, os.path.join(os.pardir, "initialize.json"), "initialize.json"):
+            if cand and os.path.exists(cand):
+                return cand
+        raise FileNotFoundError("initialize.json not found (trajectory_optimization.py:232 reads ../initialize.json); "
+                                "pass initialize_path= or set TTMPC_INITIALIZE")
+
     # trajectory_optimization.py:227-274
     def _hybrid_a_star_initial_trajectory(self, initialize_path=None):
-        pos, hd, hi = scenarios.load_initialize(initialize_path or self._initialize_path)
+        pos, hd, hi = scenarios.load_initialize(self._initialize_file(initialize_path))
         return scenarios.obca_guess(pos, hd, hi, self._horizon, len(self.obstacle_list))
 
     # trajectory_optimization.py:277-309
@@ -86,13 +97,13 @@ class TrajectoryOptimization(TrajectoryPlanning):
         return states, inputs, mus, lams
 
     def plan(self, initial_state, goal_state):
-        """trajectory_optimization.py:311-331 -> (states (6,N+1), inputs (2,N))."""
-        if self._initialize_path:
-            guess = self._hybrid_a_star_initial_trajectory()
-        else:
-            guess = self._generate_initial_trajectory_guess(initial_state, goal_state)
+        """trajectory_optimization.py:311-331 -> (states (6,N+1), inputs (2,N)); the guess comes from
+        initialize.json (312), never from the arguments."""
+        guess = self._hybrid_a_star_initial_trajectory()
         X, U, _ = self.plan_batch(np.asarray(initial_state)[None], np.asarray(goal_state)[None], guess[None])
         return X[0], U[0]
+
+    optimize = plan
 
     def plan_batch(self, initial_states, goal_states, z_guess=None):
         """B scenarios at once: (B,6), (B,6), z_guess (B,n)|None -> (B,6,N+1), (B,2,N), z (B,n)."""
