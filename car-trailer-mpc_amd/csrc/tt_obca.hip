@@ -2084,9 +2084,12 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
     if (sh.R) {  // soft dynamics rows (restoration phase): HBM operands
         if (threadIdx.x < 64) riccati_soft(c, sh);
         __syncthreads();
-        stamp(sh, on, OPH_RIC);
+        stamp(sh, on, OPH_RIC_SOFT);
         if (sh.flag) return false;
         if (threadIdx.x < 64) forward_soft(c, buf);
+        __syncthreads();
+        stamp(sh, on, OPH_FWD_SOFT);
+        return true;
     } else if (c.lds) {
         stage_inputs(c, c.lds);
         __syncthreads();

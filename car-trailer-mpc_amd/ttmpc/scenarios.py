@@ -26,6 +26,8 @@ XLB = np.array([-np.inf, -np.inf, -np.pi, -np.pi / 3.0, -np.pi / 4.0, -10.0])
 XUB = np.array([np.inf, np.inf, np.pi, np.pi / 3.0, np.pi / 4.0, 10.0])
 ULB = np.array([-5.0, -np.pi / 2])
 UUB = np.array([5.0, np.pi / 2])
+MPC_Q = np.eye(NX)           # simulation.py:400-405
+MPC_R = 10.0 * np.eye(NU)    # simulation.py:406-409
 
 
 def _f(q, u, p):
@@ -317,25 +319,43 @@ def reference_window(ref_states, ref_inputs, k, horizon):
 
 
 def mpc_obs_batch(state_traj, input_traj, B: int, horizon: int, seed: int = 0, dt_plan=0.1, dt=0.05,
-                  pos_sigma=0.2, ang_sigma=0.02):
+                  pos_sigma=0.2, ang_sigma=0.02, obstacles=None, min_gap=0.2):
     """MPC+OBCA batch (mpc_control_obs.py, driven as simulation.py:417-424, 484-522): the OBCA plan is
     interpolated to the MPC step (do_interpolation), instance b tracks the window starting at an evenly
     spread step index, x0 = window start + Gaussian perturbation.  Returns x0 (B,6), xref (B,H+1,6),
-    uref (B,H,2) in the stage-major parameter layout (mpc_control_obs.py:290-301)."""
+    uref (B,H,2) in the stage-major parameter layout (mpc_control_obs.py:290-301).
+
+    With ``obstacles`` ((M,4) cx, cy, w, h) a perturbed start whose truck or trailer lies closer than
+    ``min_gap`` (d_min, trajectory_optimization.py:95) to an obstacle under the reference's SAT test is
+    redrawn: x_0 = x_init is a constraint of the NLP, so such a start makes it infeasible by construction
+    (a closed loop never measures a pose inside an obstacle)."""
+    from .collision import sat_gap
     rng = np.random.default_rng(seed)
     S, U = interpolate_plan(np.asarray(state_traj, float), np.asarray(input_traj, float), dt_plan, dt)
     ks = np.linspace(0, U.shape[1] - 1, B).round().astype(int)
     x0 = np.empty((B, NX))
     xref = np.empty((B, horizon + 1, NX))
     uref = np.empty((B, horizon, NU))
+    lo = np.where(np.isfinite(XLB), XLB + 1e-6, -np.inf)
+    hi = np.where(np.isfinite(XUB), XUB - 1e-6, np.inf)
     for b, k in enumerate(ks):
         Xr, Ur = reference_window(S, U, int(k), horizon)
         xref[b] = Xr.T
         uref[b] = Ur.T
-        pert = np.concatenate([rng.normal(0, pos_sigma, 2), rng.normal(0, ang_sigma, 2), [0.0, 0.0]])
-        x0[b] = np.clip(Xr[:, 0] + pert, np.where(np.isfinite(XLB), XLB + 1e-6, -np.inf),
-                        np.where(np.isfinite(XUB), XUB - 1e-6, np.inf))
+        for _ in range(1000):
+            pert = np.concatenate([rng.normal(0, pos_sigma, 2), rng.normal(0, ang_sigma, 2), [0.0, 0.0]])
+            x0[b] = np.clip(Xr[:, 0] + pert, lo, hi)
+            if obstacles is None or sat_gap(x0[b, :4], PARAMS, obstacles).min() >= min_gap:
+                break
     return x0, xref, uref
+
+
+def blocked_poses(poses, obstacles, params=None):
+    """True where a pose (..., >=4) puts the truck or the trailer inside an obstacle (SAT gap < 0, the
+    reference's check_state_collision, simulation.py:337-361): an OBCA NLP pinned to such a start or goal is
+    infeasible."""
+    from .collision import sat_gap
+    return sat_gap(np.asarray(poses)[..., :4], params or PARAMS, obstacles).min(axis=(-1, -2)) < 0.0
 
 
 # ----------------------------------------------------------------------------------------------

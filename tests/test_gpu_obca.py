@@ -1,11 +1,13 @@
 """GPU parity for the OBCA path (TrajectoryOptimization / MPCTrackingControlObs) through the C ABI.
 
 The GPU (car-trailer-mpc_amd/csrc/tt_obca.hip) and the CPU oracle (oracle/c/tt_obca.c) run the same
-restated algorithm, but not bit-identical arithmetic (device sin/cos/tan/log, reciprocal refinement,
-FMA contraction, structured vs dense block algebra).  On easy instances the iterates coincide (the
-MPC+OBCA windows agree to 1e-8); on harder ones the filter line search can branch differently on
-rounding-level differences and the iteration counts differ, so those tests compare the primal solution
-(same local optimum to <= 1e-6; the OBCA duals mu/lam are not unique) and check properties:
+restated IPOPT (reference duals, least-squares multipliers, soft restoration, restoration phase), but not
+bit-identical arithmetic (device sin/cos/tan/log, reciprocal refinement, FMA contraction, structured vs
+dense block algebra).  On easy instances the iterates coincide (the MPC+OBCA windows agree to 1e-14); on
+harder ones -- hundreds to thousands of iterations through several restoration phases -- the filter line
+search can branch differently on rounding-level differences, so those tests compare statuses on most
+instances, the primal solution where both converge (same local optimum to <= 1e-6 on most; the OBCA
+duals mu/lam are not unique) and check properties:
 feasibility, collision-free plans, bitwise-deterministic reruns.  Independent optimality: the finite-difference KKT certificate of
 oracle/obca_nlp.py (numpy restatement of the reference NLP) on the GPU's output.
 """
@@ -56,30 +58,69 @@ def test_toy_plan_matches_oracle_and_is_kkt():
 
 
 def test_mpc_obca_windows_match_oracle():
-    """MPC+OBCA (mpc_control_obs.py, simulation.py:417-424 setup: N=50, dt=0.05, all 11 obstacles) on
-    windows of the reference's interpolated plan."""
+    """MPC+OBCA (mpc_control_obs.py, simulation.py:417-424 setup: N=50, dt=0.05, all 11 obstacles) on all 16
+    windows of the reference's interpolated plan, from the reference's own start (x = Xref, u = Uref,
+    mu = 100, lam pattern; mpc_control_obs.py:216-239) with max_iter 5000 and IPOPT's restoration phase.
+    Windows whose perturbed start overlaps an obstacle (SAT gap < 0) are infeasible NLPs (x_0 = x_init is a
+    constraint) and cannot converge on either side."""
     from oracle import c_oracle as co
+    from ttmpc import collision
     from ttmpc import scenarios as sc
     import ttmpc
     g = np.load(GOLDEN / "reference_numpy.npz")
     obs = g["obstacles"]
     x0, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 16, 50, seed=0)
-    sel = np.array([0, 1, 2, 3, 5, 6, 7, 8, 9])  # converging windows (4 and the bay windows 10-15 do not, on
-    # either side: breakdown without IPOPT's restoration phase, see DESIGN.md)
     p = dict(P6, dt=0.05)
     bnd = (sc.XLB, sc.XUB, sc.ULB, sc.UUB)
-    X, U, Z, st, it, kk = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0[sel], xref=xr[sel], uref=ur[sel])
-    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0[sel], xref=xr[sel], uref=ur[sel])
-    assert np.all(st == 0) and np.array_equal(st, stc)
-    assert np.max(np.abs(Z - zc)) <= 1e-8
-    # the failing window fails on both
-    X4, U4, Z4, st4, _, _ = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0[4:5], xref=xr[4:5], uref=ur[4:5])
-    z4, st4c, _, _ = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0[4:5], xref=xr[4:5], uref=ur[4:5])
-    # both break down (non-finite / step-computation failure; which one trips first depends on round-off)
-    assert st4[0] in (4, 5) and st4c[0] in (4, 5)
+    X, U, Z, st, it, kk = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0, xref=xr, uref=ur)
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0, xref=xr, uref=ur, nthreads=16)
+    assert (st == stc).sum() >= 14, (st, stc)          # long restoration runs may branch on round-off
+    both = (st <= 1) & (stc <= 1)
+    assert both.sum() >= 9, (st, stc)
+    Xc = co.obca_split(zc, 50, 11)[0]
+    assert np.max(np.abs(X[both] - Xc[both])) <= 1e-8
+    gap = collision.sat_gap(x0[:, :4], p, obs).min(axis=(-1, -2))
+    assert np.all(st[gap < 0.0] > 1) and np.all(stc[gap < 0.0] > 1)
+    assert np.all(st[:4] == 0)                          # the open-road windows
+
+
+def _c4_cases(B, seed=0):
+    import json
+    from ttmpc import scenarios as sc
+    cases = json.loads((GOLDEN / "test_cases.json").read_text())["cases"]
+    obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
+    x0, xg, zg = sc.obca_case_batch(cases, B, 200, 6, seed=seed)
+    return obs, x0, xg, zg
+
+
+def test_c4_test_cases_vs_oracle():
+    """BASELINE C4 workload: the reference's test_cases.json cases with their 2-waypoint
+    initialize.json guess (apply_case.py:16-34, trajectory_optimization.py:227-274), reference duals,
+    N=200, M=6 (obstacles.json[0:6]), max_iter 5000.  Cases 0, 5, 6 put the start or the goal pose inside an
+    obstacle of that set (SAT, the reference's own collision test): those NLPs are infeasible."""
+    from oracle import c_oracle as co
+    from ttmpc import collision
+    from ttmpc import scenarios as sc
+    obs, x0, xg, zg = _c4_cases(14)
+    X, U, Z, st, it, kk = _solver(200, obs).solve(x0, xg, z_guess=zg)
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs), x0, xg, z_guess=zg, nthreads=16)
+    assert (st == stc).sum() >= 12, (st, stc)
+    gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
+    gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
+    blocked = (gs < 0.0) | (gg < 0.0)
+    assert blocked.sum() == 6 and np.all(st[blocked] > 1) and np.all(stc[blocked] > 1)
+    assert (st[~blocked] <= 1).sum() >= 6, st
+    both = (st <= 1) & (stc <= 1)
+    Xc = co.obca_split(zc, 200, 6)[0]
+    same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6       # same local optimum (most; OBCA is nonconvex)
+    assert same[both].sum() >= both.sum() - 1
+    ok = st <= 1
+    assert np.abs(X[ok, -1] - xg[ok]).max() <= 1e-2 + 1e-7
+    assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
 
 
 def test_c4_replan_subset_vs_oracle():
+    """Re-plans around the reference's committed plan (8 Hybrid-A*-style waypoints), reference duals."""
     from oracle import c_oracle as co
     from oracle.obca_nlp import ObcaNLP
     from ttmpc import collision
@@ -87,13 +128,14 @@ def test_c4_replan_subset_vs_oracle():
     g = np.load(GOLDEN / "reference_numpy.npz")
     obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
     x0, xg, zg = sc.obca_replan_batch(g["state_traj"], 16, 200, 6, seed=0)
-    X, U, Z, st, it, kk = _solver(200, obs, max_iter=1000).solve(x0, xg, z_guess=zg)
-    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs, max_iter=1000), x0, xg, z_guess=zg, nthreads=16)
+    X, U, Z, st, it, kk = _solver(200, obs).solve(x0, xg, z_guess=zg)
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs), x0, xg, z_guess=zg, nthreads=16)
     ok = st <= 1
-    assert ok.sum() >= 11, (st, it)
+    assert ok.sum() >= 13 and (stc <= 1).sum() >= 13, (st, stc)
     both = ok & (stc <= 1)
     Xc = co.obca_split(zc, 200, 6)[0]
-    assert np.max(np.abs(X[both] - Xc[both])) <= 1e-6      # same local optimum
+    same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6
+    assert same[both].sum() >= both.sum() - 3          # same local optimum on most instances
     nlp = ObcaNLP(200, 6, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
     for b in np.flatnonzero(ok):
         gv, lbg, ubg = nlp.g(Z[b], x0[b], xg[b])
@@ -102,18 +144,19 @@ def test_c4_replan_subset_vs_oracle():
 
 
 def test_c4_full_batch_properties_and_determinism():
-    """BASELINE config C4 at full size: B=256 scenarios, N=200, M=6."""
+    """BASELINE config C4 at full size: B=256 test_cases.json scenarios, N=200, M=6, max_iter 5000."""
     from ttmpc import collision
-    from ttmpc import scenarios as sc
-    g = np.load(GOLDEN / "reference_numpy.npz")
-    obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
-    x0, xg, zg = sc.obca_replan_batch(g["state_traj"], 256, 200, 6, seed=1)
-    s = _solver(200, obs, max_iter=1000)
+    obs, x0, xg, zg = _c4_cases(256, seed=1)
+    s = _solver(200, obs)
     X, U, Z, st, it, kk = s.solve(x0, xg, z_guess=zg)
     X2, U2, Z2, st2, it2, kk2 = s.solve(x0, xg, z_guess=zg)
     assert np.array_equal(Z, Z2) and np.array_equal(st, st2)   # bitwise-deterministic
     ok = st <= 1
-    assert ok.mean() >= 0.75, np.bincount(st)
+    gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
+    gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
+    blocked = (gs < 0.0) | (gg < 0.0)
+    assert not np.any(ok & blocked)
+    assert ok[~blocked].mean() >= 0.6, np.bincount(st[~blocked])
     dyn = X[:, 1:] - (X[:, :-1] + 0.1 * _f(X[:, :-1], U))
     assert np.abs(dyn[ok]).max() <= 1e-8
     assert np.abs(X[ok, 0] - x0[ok]).max() <= 1e-8
@@ -129,18 +172,31 @@ def _f(X, U):
                      U[..., 1], U[..., 0]], axis=-1)
 
 
-def test_reference_call_surface_obca(capsys):
-    """TrajectoryOptimization.plan / MPCTrackingControlObs.solve mirror the reference signatures."""
+def test_reference_call_surface_obca(capsys, tmp_path, monkeypatch):
+    """TrajectoryOptimization.plan / .optimize and MPCTrackingControlObs.solve mirror the reference
+    signatures; plan() builds its guess from initialize.json as trajectory_optimization.py:232,312 does."""
+    import json
     import ttmpc
     from ttmpc import scenarios as sc
     model = ttmpc.TruckTrailerModel(dict(P6, horizon=60))
     obstacle_list = [{"center": (10.5, 2.6), "width": 3.0, "height": 2.0}]
-    planner = ttmpc.TrajectoryOptimization(model, dict(P6, horizon=60), sc.OBCA_Q, sc.OBCA_R,
-                                           {"lb": sc.OBCA_XLB, "ub": sc.OBCA_XUB}, {"lb": sc.OBCA_ULB, "ub": sc.OBCA_UUB},
-                                           obstacle_list)
+    ini = tmp_path / "initialize.json"   # start / goal headings in the initialize.json convention (-pi/2)
+    ini.write_text(json.dumps({"Positions": [[0.0, 0.0], [26.0, -0.2]], "Headings": [0.02 - np.pi / 2, -np.pi / 2],
+                               "HitchAngles": [0.0, 0.0]}))
+    args = (model, dict(P6, horizon=60), sc.OBCA_Q, sc.OBCA_R, {"lb": sc.OBCA_XLB, "ub": sc.OBCA_XUB},
+            {"lb": sc.OBCA_ULB, "ub": sc.OBCA_UUB}, obstacle_list)
+    planner = ttmpc.TrajectoryOptimization(*args, initialize_path=str(ini))
     states, inputs = planner.plan(np.array([0.0, 0.0, 0.02, 0.0, 0.0, 0.0]), np.array([26.0, -0.2, 0, 0, 0, 0]))
     assert states.shape == (6, 61) and inputs.shape == (2, 60)
-    assert planner.last_status is not None
+    assert planner.last_status[0] == 0
+    states2, inputs2 = planner.optimize(np.array([0.0, 0.0, 0.02, 0.0, 0.0, 0.0]), np.array([26.0, -0.2, 0, 0, 0, 0]))
+    assert np.array_equal(states, states2) and np.array_equal(inputs, inputs2)
+    # without initialize.json the reference's open() fails; so does the mirror
+    monkeypatch.chdir(tmp_path / "..")
+    monkeypatch.delenv("TTMPC_INITIALIZE", raising=False)
+    if not (tmp_path / ".." / "initialize.json").exists() and not (tmp_path / ".." / ".." / "initialize.json").exists():
+        with pytest.raises(FileNotFoundError):
+            ttmpc.TrajectoryOptimization(*args).plan(np.zeros(6), np.zeros(6))
     g = np.load(GOLDEN / "reference_numpy.npz")
     p = dict(P6, dt=0.05, horizon=50)
     ctrl = ttmpc.MPCTrackingControlObs(model, p, sc.OBCA_Q, sc.OBCA_R, {"lb": sc.XLB, "ub": sc.XUB},

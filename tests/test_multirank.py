@@ -141,3 +141,20 @@ def test_single_rank_sharded_is_plain_solve():
     X, U, st, it, kk = sb.results()
     assert stats["instances"] == B and stats["converged"] == int(np.sum(st <= 1)) == B
     assert np.allclose(X[:, 0], x0)
+
+
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts its own two ranks (RANK / LOCAL_RANK / WORLD_SIZE,
+    127.0.0.1 rendezvous) and only rank 0 prints; the selftest config runs the gloo reduction path of the
+    real configs without touching a GPU."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--config", "selftest"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["wall_max"] == 1.5 and rec["ok_total"] == 3 and rec["instances"] == 2
