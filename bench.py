@@ -1,6 +1,6 @@
 """Benchmark: batched truck-trailer NMPC solves on MI355X (BASELINE.json metric).
 
-    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5|c4|c4replan|cobs|sim] [--batch B] [--horizon H]
+    python bench.py --gpus N --steps K --warmup W [--config c2|c3|c5|c4|c4all|c4replan|cobs|sim] [--batch B] [--horizon H]
 
 c5 is the sharded path: one global batch on rank 0, RCCL scatter -> solve -> gather (ttmpc/sharded.py).
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches the N ranks itself (one process
@@ -165,8 +165,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "c4", "c4replan", "cobs", "sim", "selftest"],
-                    help="c2/c3/c5: tracking NMPC; c4: OBCA plans of test_cases.json (trajectory_optimization.py); "
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c5", "c4", "c4all", "c4replan", "cobs", "sim", "selftest"],
+                    help="c2/c3/c5: tracking NMPC; c4: OBCA plans of the collision-free test_cases.json cases "
+                         "(trajectory_optimization.py); c4all: all 7 cases (3 are infeasible NLPs); "
                          "c4replan: OBCA re-plans around the committed plan; cobs: MPC+OBCA (mpc_control_obs.py)")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default by config)")
     ap.add_argument("--horizon", type=int, default=0)
@@ -182,7 +183,7 @@ def main():
         sys.exit(spawn_ranks(args))
     if args.config == "selftest":
         return main_selftest(args)
-    if args.config in ("c4", "c4replan", "cobs"):
+    if args.config in ("c4", "c4all", "c4replan", "cobs"):
         return main_obca(args)
     if args.config == "c5":
         return main_c5(args)
@@ -585,10 +586,12 @@ def main_obca(args):
     """OBCA configs: one step = one launch solving B independent OBCA NLPs with the restated IPOPT
     (reference duals mu = 100 / lam pattern, tol 1e-8, max_iter 5000, restoration phase).
     c4      : BASELINE configs[3] as SURVEY §8(d) defines it -- TrajectoryOptimization, 6 obstacle rectangles
-              (obstacles.json[0:6]), N=200, dt=0.1, B=256 = the 7 test_cases.json cases x Monte-Carlo start
+              (obstacles.json[0:6]), N=200, dt=0.1, B=256 = test_cases.json cases x Monte-Carlo start
               perturbations, each with the reference's 2-waypoint initialize.json guess (apply_case.py:16-34,
-              trajectory_optimization.py:227-274).  Three cases put the start or the goal pose inside an
-              obstacle of that set; their NLPs are infeasible (reported separately).
+              trajectory_optimization.py:227-274).  Three of the 7 cases (baseline_hybrid_path,
+              diagonal_reverse_cross_aisle, angle_test) put the start or the goal pose inside an obstacle of
+              that set: their NLPs are infeasible, so c4 draws from the 4 others (perturbed starts that land in
+              an obstacle are redrawn) and c4all keeps all 7 (infeasible ones reported separately).
     c4replan: the same planner on re-plans around the reference's committed IPOPT plan (data/state_traj.txt
               subsampled to 8 Hybrid-A*-style waypoints, start perturbed).
     cobs    : MPCTrackingControlObs as simulation.py drives it (N=50, dt=0.05, all 11 obstacles), windows of
@@ -610,12 +613,13 @@ def main_obca(args):
     g = np.load(REPO / "tests" / "golden" / "reference_numpy.npz")
     obs_all = sc.obstacles_array(sc.load_obstacles(REPO / "tests" / "golden" / "obstacles.json"))
     blocked = None
-    if args.config in ("c4", "c4replan"):
+    if args.config in ("c4", "c4all", "c4replan"):
         B, N, M = args.batch or 256, args.horizon or 200, 6
         obs = obs_all[:M]
-        if args.config == "c4":
+        if args.config in ("c4", "c4all"):
             cases = json.loads((REPO / "tests" / "golden" / "test_cases.json").read_text())["cases"]
-            x0, xg, zg = sc.obca_case_batch(cases, B, N, M, seed=rank_seed(rank))
+            x0, xg, zg = sc.obca_case_batch(cases, B, N, M, seed=rank_seed(rank),
+                                            obstacles=obs if args.config == "c4" else None, params=sc.OBCA_PARAMS)
             blocked = sc.blocked_poses(x0, obs, sc.OBCA_PARAMS) | sc.blocked_poses(xg, obs, sc.OBCA_PARAMS)
         else:
             x0, xg, zg = sc.obca_replan_batch(g["state_traj"], B, N, M, seed=rank_seed(rank))
@@ -671,8 +675,10 @@ def main_obca(args):
         return
     F = float(np.sum(obca_flops(N, M, iters.astype(np.float64))))
     achieved = F / (kernel_ms * 1e-3) / 1e12
-    name = {"c4": "c4: TrajectoryOptimization OBCA plans of the 7 test_cases.json cases x start perturbations "
-                  "(2-waypoint initialize.json guess)",
+    name = {"c4": "c4: TrajectoryOptimization OBCA plans of the 4 collision-free test_cases.json cases x start "
+                  "perturbations (2-waypoint initialize.json guess)",
+            "c4all": "c4all: TrajectoryOptimization OBCA plans of all 7 test_cases.json cases x start perturbations "
+                     "(2-waypoint initialize.json guess; 3 cases infeasible)",
             "c4replan": "c4replan: TrajectoryOptimization re-plans around the committed plan (8-waypoint guess)",
             "cobs": "cobs: MPC+OBCA (MPCTrackingControlObs) windows"}[args.config]
     solver_rec = {"converged_or_acceptable": ok_total, "instances": B_total,

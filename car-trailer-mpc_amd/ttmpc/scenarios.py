@@ -224,26 +224,47 @@ def obca_guess(positions, headings, hitch, N, M, complete=False, dt=0.1, L1=7.05
     return z
 
 
-def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5, ang_sigma=0.05, complete=False):
+def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5, ang_sigma=0.05, complete=False,
+                    obstacles=None, params=None):
     """C4 generator: test_cases.json cases x Monte-Carlo start perturbations.  Each instance is the
     2-waypoint initialize.json of its case (apply_case.py:16-34) with a perturbed start; the guess is
     built from those waypoints (obca_guess) and (x_init, x_goal) as get_initial_goal_states.py:5-26 +
     trajectory_animation.py:83-92 (speed and steering appended as 0).
+
+    ``obstacles`` given: only cases whose exact start and goal poses are collision-free against them are
+    used, and a perturbed start that lands inside an obstacle is redrawn (an OBCA NLP pinned to a pose in
+    collision is infeasible, blocked_poses).
     Returns x0 (B,6), x_goal (B,6), z_guess (B,n)."""
     rng = np.random.default_rng(seed)
     x0 = np.empty((B, NX))
     xg = np.empty((B, NX))
     st = 8 + 16 * M
     zg = np.empty((B, N * st + 6 + 16 * M))
-    for b in range(B):
-        c = cases[b % len(cases)]
+
+    def waypoints(c):
         pos = np.array([[c["start"]["x"], c["start"]["y"]], [c["goal"]["x"], c["goal"]["y"]]], dtype=np.float64)
         hd = np.array([c["start"]["heading_rad"], c["goal"]["heading_rad"]], dtype=np.float64) + np.pi / 2
         hi = np.array([c["start"]["hitch_angle_rad"], c["goal"]["hitch_angle_rad"]], dtype=np.float64)
+        return pos, hd, hi
+
+    def blocked(pos, hd, hi):
+        poses = np.array([[pos[i, 0], pos[i, 1], hd[i], hi[i]] for i in range(2)])
+        return obstacles is not None and bool(blocked_poses(poses, obstacles, params).any())
+
+    cases = [c for c in cases if not blocked(*waypoints(c))]
+    if not cases:
+        raise ValueError("no test case has a collision-free start and goal")
+    for b in range(B):
+        pos, hd, hi = waypoints(cases[b % len(cases)])
         if b >= len(cases):  # instance 0..len-1 are the exact cases, the rest Monte-Carlo perturbed
-            pos[0] += rng.normal(0.0, pos_sigma, 2)
-            hd[0] += rng.normal(0.0, ang_sigma)
-            hi[0] = float(np.clip(hi[0] + rng.normal(0.0, ang_sigma), -0.5, 0.5))
+            base = (pos.copy(), hd.copy(), hi.copy())
+            for _ in range(100):
+                pos, hd, hi = base[0].copy(), base[1].copy(), base[2].copy()
+                pos[0] += rng.normal(0.0, pos_sigma, 2)
+                hd[0] += rng.normal(0.0, ang_sigma)
+                hi[0] = float(np.clip(hi[0] + rng.normal(0.0, ang_sigma), -0.5, 0.5))
+                if not blocked(pos, hd, hi):
+                    break
         x0[b] = [pos[0, 0], pos[0, 1], hd[0], hi[0], 0.0, 0.0]
         xg[b] = [pos[1, 0], pos[1, 1], hd[1], hi[1], 0.0, 0.0]
         zg[b] = obca_guess(pos, hd, hi, N, M, complete=complete)

@@ -34,7 +34,7 @@ if wl == "cobs":
 else:
     if wl == "c4":
         cases = json.loads((G / "test_cases.json").read_text())["cases"]
-        x0, xg, zg = sc.obca_case_batch(cases, B, 200, 6, seed=0)
+        x0, xg, zg = sc.obca_case_batch(cases, B, 200, 6, seed=0, obstacles=obs_all[:6], params=sc.OBCA_PARAMS)
     else:
         x0, xg, zg = sc.obca_replan_batch(g["state_traj"], B, 200, 6, seed=7)
     s = ttmpc.ObcaSolver(200, sc.OBCA_PARAMS, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB,
