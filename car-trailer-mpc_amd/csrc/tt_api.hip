@@ -35,9 +35,24 @@ struct Handle {
     size_t stage_in = 0, stage_out = 0;
     char *d_sin = nullptr, *d_sout = nullptr, *h_sin = nullptr, *h_sout = nullptr;
     std::string err;
+    unsigned long long* obca_stamps = nullptr;  // diagnostics: per-phase clocks (ttx_obca_set_stamps)
 };
 
 thread_local std::string g_err;
+
+// Makes the handle's device current for one entry point and restores the caller's device on every
+// return path (the C ABI must not leave a different current device behind).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        err = hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 int fail(Handle* h, int code, const char* fmt, const char* detail = "") {
     char buf[512];
@@ -233,7 +248,8 @@ int tt_create(const tt_config* cfg, const double* Q, const double* R, const doub
     memcpy(h->uub, uub, sizeof h->uub);
     if (obca) memcpy(h->obs, obstacles, sizeof(double) * 4 * cfg->M);
     h->device = device;
-    hipError_t e = hipSetDevice(device);
+    DeviceGuard dg(device);
+    hipError_t e = dg.err;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         int rc = hip_fail(nullptr, e, "tt_create");
@@ -261,7 +277,8 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
                                           nullptr, d_status, d_iters, d_kkt_res, stream);
     if (h->cfg.variant == TT_VARIANT_FUZZY && !d_wq_wr)
         return fail(h, -EINVAL, "fuzzy variant needs per-instance weights (mpc_control_fuzzy.py:54-58)%s");
-    hipError_t e = hipSetDevice(h->device);
+    DeviceGuard dg(h->device);
+    hipError_t e = dg.err;
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     ttmpc::TrackArgs a = make_args(h, B);
     a.x0 = d_x0;
@@ -293,7 +310,12 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
     if (is_obca(h->cfg))  // MPC+OBCA handle: its own host path (workspace, z_guess layout)
         return tt_obca_solve_batch(handle, B, x0, nullptr, xref, uref, z_guess, x_out, u_out, nullptr, status, iters,
                                    kkt_res);
-    hipError_t e = hipSetDevice(h->device);
+    // validate everything tt_solve_batch_device would refuse before the staging buffer is touched
+    if (h->cfg.variant == TT_VARIANT_FUZZY && !wq_wr)
+        return fail(h, -EINVAL, "fuzzy variant needs per-instance weights (mpc_control_fuzzy.py:54-58)%s");
+    if (B > (1 << 30)) return fail(h, -EINVAL, "B too large%s");
+    DeviceGuard dg(h->device);
+    hipError_t e = dg.err;
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     // packed layout, instance-major within each array: in  = x0 | xref | uref | [wq_wr] | [z_guess]
     //                                                   out = X | U | kkt | status, iters (int32)
@@ -323,7 +345,10 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
     int* dit = dst + b;
     rc = tt_solve_batch_device(h, B, dptr[0], dptr[1], dptr[2], wq_wr ? dptr[3] : nullptr,
                                z_guess ? dptr[4] : nullptr, dxo, duo, dst, dit, dkk, s);
-    if (rc) return rc;
+    if (rc) {
+        (void)hipStreamSynchronize(s);  // the H2D from the pinned staging buffer may still be in flight
+        return rc;
+    }
     e = hipMemcpyAsync(h->h_sout, h->d_sout, out_d * 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(h, e, "solve");
@@ -358,8 +383,6 @@ int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_x
 }
 #endif
 
-static unsigned long long* g_obca_stamps = nullptr;  // diagnostics: set by ttx_obca_set_stamps
-
 int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
                                const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
                                double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream) {
@@ -373,7 +396,8 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
     if (!d_x0 || !d_x_out || !d_u_out || !d_status) return fail(h, -EINVAL, "NULL device buffer%s");
     if (plan && !d_xgoal) return fail(h, -EINVAL, "plan variant needs the goal states%s");
     if (!plan && (!d_xref || !d_uref)) return fail(h, -EINVAL, "MPC+OBCA variant needs reference states/inputs%s");
-    hipError_t e = hipSetDevice(h->device);
+    DeviceGuard dg(h->device);
+    hipError_t e = dg.err;
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     int rc = ensure_ows(h, B);
     if (rc) return rc;
@@ -417,7 +441,7 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
     a.iters = d_iters;
     a.kkt = d_kkt_res;
     a.ws = h->d_ows;
-    a.stamps = g_obca_stamps;
+    a.stamps = h->obca_stamps;
     hipStream_t s = static_cast<hipStream_t>(stream);
     e = ttmpc::launch_obca(a, s);
     if (e != hipSuccess) return hip_fail(h, e, "OBCA kernel launch");
@@ -435,7 +459,8 @@ int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgo
     const bool plan = h->cfg.variant == TT_VARIANT_OBCA_PLAN;
     if (!x0 || !status || (plan && !xgoal) || (!plan && (!xref || !uref)))
         return fail(h, -EINVAL, "NULL host buffer%s");
-    hipError_t e = hipSetDevice(h->device);
+    DeviceGuard dg(h->device);
+    hipError_t e = dg.err;
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     int rc = ensure_ws(h, B);
     if (rc == 0) rc = ensure_ows(h, B);
@@ -457,7 +482,10 @@ int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgo
     rc = tt_obca_solve_batch_device(h, B, h->d_x0, plan ? h->d_oxg : nullptr, plan ? nullptr : h->d_xref,
                                     plan ? nullptr : h->d_uref, z_guess ? h->d_ozg : nullptr, h->d_xo, h->d_uo,
                                     z_out ? h->d_ozo : nullptr, h->d_st, h->d_it, h->d_kkt, s);
-    if (rc) return rc;
+    if (rc) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     if (x_out) D2H(x_out, h->d_xo, b * (N + 1) * 6 * 8);
     if (u_out) D2H(u_out, h->d_uo, b * N * 2 * 8);
     if (z_out) D2H(z_out, h->d_ozo, b * nz * 8);
@@ -471,10 +499,11 @@ int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgo
     return 0;
 }
 
-/* diagnostics only (not part of include/ttmpc.h): per-instance phase cycle sums of the next OBCA launches
- * into d_stamps[B][kObcaPhases] (device pointer; NULL switches it off) */
-int ttx_obca_set_stamps(unsigned long long* d_stamps) {
-    g_obca_stamps = d_stamps;
+/* diagnostics only (not part of include/ttmpc.h): per-instance phase cycle sums of the handle's next OBCA
+ * launches into d_stamps[B][kObcaPhases] (device pointer; NULL switches it off).  Returns the phase count. */
+int ttx_obca_set_stamps(void* handle, unsigned long long* d_stamps) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (h) h->obca_stamps = d_stamps;
     return ttmpc::kObcaPhases;
 }
 
@@ -491,7 +520,8 @@ int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, co
 void tt_destroy(void* handle) {
     Handle* h = static_cast<Handle*>(handle);
     if (!h) return;
-    (void)hipSetDevice(h->device);
+    DeviceGuard dg(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_ws(h);
     free_ows(h);
     free_stage(h);

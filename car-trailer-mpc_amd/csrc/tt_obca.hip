@@ -65,8 +65,14 @@ enum : int {
     // restoration phase: elastic pairs of the 4 rows (+ steps, 2 buffers), reference duals / slacks and
     // D_R^2, saved multipliers, acceptable point, soft-restoration snapshot (w zw s vL vU yd)
     B_PR = 76, B_NR = 80, B_ZP = 84, B_ZN = 88, B_DP = 92, B_DN = 100, B_WR = 108, B_DRW = 116, B_SR = 124,
-    B_SZW = 128, B_SVL = 136, B_SVU = 140, B_WACC = 144, B_SNAP = 152, B_END = 184
+    B_SZW = 128, B_SVL = 136, B_SVU = 140, B_WACC = 144, B_SNAP = 152,
+    // the block's elimination as phase_factor left it (read back by phase_recover instead of refactoring):
+    // G 16 | LT 10 | LL 10 | 1/dm 4 | zf_lam 4 | t 4 | Zl 16 | Yl 16 | fw 8 | D 4
+    B_FR = 184, B_END = 276
 };
+enum : int { FR_G = 0, FR_LT = 16, FR_LL = 26, FR_IDM = 36, FR_ZFL = 40, FR_T = 44, FR_ZL = 48, FR_YL = 64, FR_FW = 80,
+             FR_D = 88, FR_END = 92 };
+static_assert(B_FR + FR_END == B_END, "factor record");
 static_assert(B_END == kObcaBlockFields, "block field count");
 
 // packed symmetric 6x6 (upper) index
@@ -262,9 +268,18 @@ __device__ __forceinline__ void model_lin(LArgs& a, const double* x, const doubl
 struct Geom {
     double p0, p1, dpt0, dpt1, dpp0, dpp1, ppt0, ppt1, ptp0, ptp1, ppp0, ppp1, ca, sa, angp, hl, hw;
 };
-__device__ __forceinline__ void body_geom(LArgs& a, const double* xk, int body, Geom& g) {
-    double st, ct;
-    sincos(xk[2], &st, &ct);
+// the stage's two body angles (theta, theta + psi): computed once per stage, shared by its 2M blocks
+struct Trig {
+    double st, ct, sa, ca;
+};
+__device__ __forceinline__ Trig stage_trig(const double* xk) {
+    Trig t;
+    sincos(xk[2], &t.st, &t.ct);
+    sincos(xk[2] + xk[3], &t.sa, &t.ca);
+    return t;
+}
+__device__ __forceinline__ void body_geom(LArgs& a, const double* xk, int body, const Trig& tr, Geom& g) {
+    const double st = tr.st, ct = tr.ct;
     if (body == 0) {
         const double h1 = 0.5 * a.L1;
         g.ca = ct; g.sa = st; g.angp = 0.0; g.hl = 0.5 * a.L1; g.hw = 0.5 * a.W1;
@@ -275,8 +290,7 @@ __device__ __forceinline__ void body_geom(LArgs& a, const double* xk, int body, 
         g.ptp0 = g.ptp1 = g.ppp0 = g.ppp1 = 0.0;
     } else {
         const double h2 = 0.5 * a.L2, M = a.Mh;
-        double sa, ca;
-        sincos(xk[2] + xk[3], &sa, &ca);
+        const double sa = tr.sa, ca = tr.ca;
         g.ca = ca; g.sa = sa; g.angp = 1.0; g.hl = 0.5 * a.L2; g.hw = 0.5 * a.W2;
         g.p0 = xk[0] - M * ct - h2 * ca; g.p1 = xk[1] - M * st - h2 * sa;
         g.dpt0 = M * st + h2 * sa; g.dpt1 = -M * ct - h2 * ca;
@@ -288,9 +302,9 @@ __device__ __forceinline__ void body_geom(LArgs& a, const double* xk, int body, 
 }
 
 // constraint values of block j (obstacle j>>1, body j&1)
-__device__ __forceinline__ void blk_vals(LArgs& a, const double* xk, int j, const double* w, double* d) {
+__device__ __forceinline__ void blk_vals(LArgs& a, const double* xk, const Trig& tr, int j, const double* w, double* d) {
     Geom g;
-    body_geom(a, xk, j & 1, g);
+    body_geom(a, xk, j & 1, tr, g);
     const auto* ob = a.obs + 4 * (j >> 1);
     const double ex = g.p0 - ob[0], ey = g.p1 - ob[1], hwo = 0.5 * ob[2], hho = 0.5 * ob[3];
     const double aa = w[4] - w[6], cc = w[5] - w[7];
@@ -311,11 +325,11 @@ struct Blk {
     double hxx22, hxx23, hxx33;
     double hxl[4][4];                // W_{x lam}: rows X,Y,theta,psi
     // elimination
-    double dm[4];                    // Sigma_mu + dw (mu block is diagonal)
-    double LL[10];                   // chol of the lam block
+    double idm[4];                   // 1 / (Sigma_mu + dw) (mu block is diagonal)
+    double LL[10];                   // chol of the lam block (1/L_ii on the diagonal)
     double Yl[4][4];                 // L^-1 Jw_lam'  [a][r]
     double Zl[4][4];                 // L^-1 W_lam x  [a][q]
-    double LT[10];                   // chol of T
+    double LT[10];                   // chol of T (1/L_ii on the diagonal)
     double G[4][4];                  // Y_lam' Z - Jx  [r][q]
     double D[4];                     // Sigma_s + dw of the 4 slacks
     double E[4];                     // E of the 4 rows: 1/D (+ 1/D_p + 1/D_n in the restoration phase)
@@ -328,8 +342,8 @@ __device__ __forceinline__ bool chol4(double* L) {
 #pragma unroll
         for (int k = 0; k < j; ++k) s -= L[lo4(j, k)] * L[lo4(j, k)];
         if (!(s > 0.0)) return false;
-        const double r = sqrt(s), ir = frcp(r);
-        L[lo4(j, j)] = r;
+        const double ir = frcp(sqrt(s));
+        L[lo4(j, j)] = ir;  // the factor keeps 1/L_jj on its diagonal: the solves multiply
 #pragma unroll
         for (int i = j + 1; i < 4; ++i) {
             double t = L[lo4(i, j)];
@@ -346,7 +360,7 @@ __device__ __forceinline__ void fsub4(const double* L, double* b) {
         double t = b[i];
 #pragma unroll
         for (int k = 0; k < i; ++k) t -= L[lo4(i, k)] * b[k];
-        b[i] = t / L[lo4(i, i)];
+        b[i] = t * L[lo4(i, i)];
     }
 }
 __device__ __forceinline__ void bsub4(const double* L, double* b) {
@@ -355,13 +369,14 @@ __device__ __forceinline__ void bsub4(const double* L, double* b) {
         double t = b[i];
 #pragma unroll
         for (int k = i + 1; k < 4; ++k) t -= L[lo4(k, i)] * b[k];
-        b[i] = t / L[lo4(i, i)];
+        b[i] = t * L[lo4(i, i)];
     }
 }
 
-__device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, int j, const double* w, const double* y, Blk& k) {
+__device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& tr, int j, const double* w, const double* y,
+                                        Blk& k) {
     Geom g;
-    body_geom(a, xk, j & 1, g);
+    body_geom(a, xk, j & 1, tr, g);
     const auto* ob = a.obs + 4 * (j >> 1);
     const double ex = g.p0 - ob[0], ey = g.p1 - ob[1], hwo = 0.5 * ob[2], hho = 0.5 * ob[3];
     const double aa = w[4] - w[6], cc = w[5] - w[7];
@@ -435,7 +450,7 @@ __device__ __forceinline__ double jwm(const Blk& k, int r, int a) {
 __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double dw, double* C) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        k.dm[i] = sig_w[i] + dw;
+        k.idm[i] = frcp(sig_w[i] + dw);
         k.LL[lo4(i, i)] += sig_w[4 + i] + dw;
     }
     if (!chol4(k.LL)) return false;
@@ -457,9 +472,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
 #pragma unroll
         for (int a = 0; a < 4; ++a) k.Zl[a][q] = col[a];
     }
-    double idm[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) idm[a] = frcp(k.dm[a]);
+    const double* idm = k.idm;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -505,7 +518,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
 // t = T^-1 h, and adds the gradient contribution into q4.
 __device__ __forceinline__ void blk_rhs(const Blk& k, const double* fw, const double* rd, double* zf, double* t, double* q4) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a) zf[a] = fw[a] / k.dm[a];
+    for (int a = 0; a < 4; ++a) zf[a] = fw[a] * k.idm[a];
     double zl[4] = {fw[4], fw[5], fw[6], fw[7]};
     fsub4(k.LL, zl);
 #pragma unroll
@@ -550,7 +563,7 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
         double s = fw[a];
 #pragma unroll
         for (int r = 0; r < 4; ++r) s += jwm(k, r, a) * yp[r];
-        dwv[a] = -s / k.dm[a];
+        dwv[a] = -s * k.idm[a];
     }
     double v[4];
 #pragma unroll
@@ -570,7 +583,7 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
 // separating-axis dual certificate (see oracle/c/tt_obca.c:dual_certificate)
 __device__ __forceinline__ void dual_certificate(LArgs& a, const double* xk, int j, double* w) {
     Geom g;
-    body_geom(a, xk, j & 1, g);
+    body_geom(a, xk, j & 1, stage_trig(xk), g);
     const auto* ob = a.obs + 4 * (j >> 1);
     double best = -INFINITY, b0 = 1.0, b1 = 0.0;
 #pragma unroll
@@ -681,9 +694,9 @@ __device__ __forceinline__ double grad_row(const Ctx& c, int r, double s, double
 // linearise + factor + rhs of one block at the current iterate; returns false if not positive definite.
 // Outputs D (Sigma_s + dw), E (row regularisation), the elimination and the block's Hessian / gradient
 // contribution to its stage.
-__device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, int j, int k, const double* x, double mu,
-                                            double dw, Blk& bk, double* fw, double* zf, double* t4, double* C4,
-                                            double* q4) {
+__device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, int j, int k, const double* x,
+                                            const Trig& tr, double mu, double dw, Blk& bk, double* fw, double* zf,
+                                            double* t4, double* C4, double* q4) {
     const bool rs = sh.R != 0, lsq = sh.lsq != 0;
     double w[8], y[4], sw[8], rd[4];
 #pragma unroll
@@ -700,7 +713,7 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, int
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
-    blk_lin(*c.a, x, j, w, y, bk);
+    blk_lin(*c.a, x, tr, j, w, y, bk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
@@ -733,10 +746,29 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
         load_x(c, k, x);
         // the OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
         double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
+        const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             double fw[8], zf[8], t4[4];
-            if (!block_setup(c, sh, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+            if (!block_setup(c, sh, j, k, x, tr, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+            auto st = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st(FR_G + 4 * r + q, bk.G[r][q]);
+#pragma unroll
+            for (int i = 0; i < 10; ++i) { st(FR_LT + i, bk.LT[i]); st(FR_LL + i, bk.LL[i]); }
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                st(FR_IDM + a, bk.idm[a]);
+                st(FR_ZFL + a, zf[4 + a]);
+                st(FR_T + a, t4[a]);
+                st(FR_D + a, bk.D[a]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { st(FR_ZL + 4 * a + q, bk.Zl[a][q]); st(FR_YL + 4 * a + q, bk.Yl[a][q]); }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) st(FR_FW + e, fw[e]);
         }
         double Qs[21], qv[6];
         const double sc = (k == N && plan) ? a.tfac : 1.0;
@@ -880,7 +912,7 @@ struct LSrc {
     __device__ void setK(int i, int k, double v) const { B[k * LB + 27 + i] = v; }
     __device__ void setKF(int i, int k, double v) const { B[k * LB + 39 + i] = v; }
 };
-__host__ __device__ inline size_t obca_lds_bytes(int N) { return (size_t)(LA + LB) * (N + 1) * 8; }
+__host__ __device__ inline size_t obca_lds_bytes(int N) { return (size_t)(LA + LB) * (N + 1) * 8; }  // >= the soft records (53, 77)
 constexpr size_t kObcaLdsMax = 150 * 1024;  // dynamic LDS budget for the staged sweeps (+ static Shared)
 
 // all threads: copy the sweep inputs of every stage into region A (field-major reads: coalesced in k)
@@ -1096,35 +1128,93 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
     }
 }
 
-// ======== restoration phase: Riccati sweep with soft dynamics rows (wave 0, HBM operands) ========
+// ======== restoration phase: Riccati sweep with soft dynamics rows (wave 0) ========
 // Row k reads x_k - F(x_{k-1}) - p + n = c: eliminating the elastic pair leaves J dx - E y+ = -r~ with
 // E = 1/D_p + 1/D_n, so x_k = yhat_k + E y+_k.  Before stage k-1 the cost-to-go of stage k is softened:
 // M = I + S P_k S (S = E^1/2; positive definite or the inertia is wrong), Y_k = S M^-1 S,
 // P~_k = P_k - P_k Y_k P_k, p~_k = p_k - P_k Y_k p_k; stage k-1 then runs the hard recursion on P~, p~.
 // M^-1 by in-place Gauss-Jordan (lane (i, j) owns entry (i, j); the pivots are M's LDL' pivots).  Y_k
-// is kept (S_Y) for the forward sweep.  Not latency-tuned: it runs only in restoration iterations.
-__device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh) {
-    const GSrc src{c};
+// is kept (S_Y) for the forward sweep.
+// One wave: its LDS operations complete in program order, so the tiles need only compiler ordering
+// (lds_order), never a memory fence (a fence would also wait for the HBM stores of P, K, Y).  The
+// inputs come from LDS copies staged by all four waves (SoftA) when the dynamic LDS holds them, else
+// straight from HBM (GSrc); either way the next stage's operands are loaded one stage ahead.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// region of the soft sweep's inputs, per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CE 6 | SD 6  (53)
+constexpr int LAS = 53;
+struct SoftA {
+    const lds_double* A;
+    __device__ double QT(int i, int k) const { return A[k * LAS + i]; }
+    __device__ double QV(int i, int k) const { return A[k * LAS + 21 + i]; }
+    __device__ double RT(int i, int k) const { return A[k * LAS + 27 + i]; }
+    __device__ double RV(int i, int k) const { return A[k * LAS + 30 + i]; }
+    __device__ double AJ(int i, int k) const { return A[k * LAS + 32 + i]; }
+    __device__ double CR(int i, int k) const { return A[k * LAS + 41 + i]; }
+    __device__ double SD(int i, int k) const { return A[k * LAS + 47 + i]; }
+};
+struct SoftG {
+    const Ctx& c;
+    __device__ double QT(int i, int k) const { return c.S(S_QT + i, k); }
+    __device__ double QV(int i, int k) const { return c.S(S_QV + i, k); }
+    __device__ double RT(int i, int k) const { return c.S(S_RT + i, k); }
+    __device__ double RV(int i, int k) const { return c.S(S_RV + i, k); }
+    __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
+    __device__ double CR(int i, int k) const { return c.S(S_CE + i, k); }
+    __device__ double SD(int i, int k) const { return c.S(S_SD + i, k); }
+};
+__device__ __noinline__ void stage_soft_inputs(const Ctx& c, double* A) {
+    const int NP = c.NP;
+    for (int idx = threadIdx.x; idx < LAS * NP; idx += T) {
+        const int f = idx / NP, k = idx - f * NP;
+        int g;
+        if (f < 21) g = S_QT + f;
+        else if (f < 27) g = S_QV + f - 21;
+        else if (f < 30) g = S_RT + f - 27;
+        else if (f < 32) g = S_RV + f - 30;
+        else if (f < 41) g = S_AJ + f - 32;
+        else if (f < 47) g = S_CE + f - 41;
+        else g = S_SD + f - 47;
+        A[k * LAS + f] = (k < c.N || f < 27 || f >= 41) ? c.S(g, k) : 0.0;
+    }
+}
+// operands of one soft stage: the softening of stage k (S entries of the lane) and the hard step k-1
+struct SoftOps {
+    double si, sj;
+    RicOps r;
+};
+template <class Src>
+__device__ __forceinline__ void soft_ops(const Src& src, int k, int i, int j, int sij, int r, bool vec, SoftOps& o) {
+    o.si = src.SD(i, k);
+    o.sj = src.SD(j, k);
+    if (k > 0) ric_ops(src, k - 1, sij, r, vec, o.r);
+}
+
+template <class Src>
+__device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& src) {
+    const GSrc out{c};
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt, dt2 = dt * dt;
     const bool act = lane < 36, vec = lane >= 48 && lane < 54;
     const int i = act ? lane / 6 : 0, j = act ? lane % 6 : 0, r = vec ? lane - 48 : 0;
-    const int ii = min(i, j), jj = max(i, j);
+    const int ii = min(i, j), jj = max(i, j), sij = sy6(ii, jj);
+    const ColMask mj(j), mi(ii), mr(r);
     __shared__ double Pt[48], Mt[48], Yt[48], Tt[48];
     if (act) {
-        const double q = src.QT(sy6(ii, jj), N);
+        const double q = src.QT(sij, N);
         Pt[8 * i + j] = q;
-        if (i <= j) src.setP(sy6(i, j), N, q);
+        if (i <= j) out.setP(sij, N, q);
     }
     double pv = vec ? src.QV(r, N) : 0.0;
-    if (vec) src.setPV(r, N, pv);
+    if (vec) out.setPV(r, N, pv);
     bool fail = false;
-    wave_sync();
-    for (int k = N;; --k) {
+    lds_order();
+    auto stage = [&](int k, const SoftOps& cur, SoftOps& nx) __attribute__((always_inline)) {
+        if (k > 0) soft_ops(src, k - 1, i, j, sij, r, vec, nx);  // next stage's operands, one stage ahead
         // ---- soften stage k
-        const double Si = c.S(S_SD + i, k), Sj = c.S(S_SD + j, k);
-        if (act) Mt[8 * i + j] = (i == j ? 1.0 : 0.0) + Si * Pt[8 * ii + jj] * Sj;
-        wave_sync();
+        if (act) Mt[8 * i + j] = (i == j ? 1.0 : 0.0) + cur.si * Pt[8 * ii + jj] * cur.sj;
+        lds_order();
+#pragma unroll
         for (int p = 0; p < 6; ++p) {
             const double piv = Mt[8 * p + p];
             double nv = 0.0;
@@ -1133,16 +1223,17 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh) {
                 nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : aij - aip * apj * ip;
             }
             fail = fail || !(piv > 0.0);
-            wave_sync();
+            lds_order();
             if (act) Mt[8 * i + j] = nv;
-            wave_sync();
+            lds_order();
         }
         if (act) {
-            const double y = c.S(S_SD + ii, k) * Mt[8 * ii + jj] * c.S(S_SD + jj, k);
+            // Y = S M^-1 S from the upper entry (symmetric by construction)
+            const double y = i <= j ? cur.si * Mt[8 * i + j] * cur.sj : cur.sj * Mt[8 * j + i] * cur.si;
             Yt[8 * i + j] = y;
-            if (i <= j) c.S(S_Y + sy6(i, j), k) = y;
+            if (i <= j) c.S(S_Y + sij, k) = y;
         }
-        wave_sync();
+        lds_order();
         if (act) {
             double t = 0.0;
 #pragma unroll
@@ -1152,7 +1243,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh) {
         double pl[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) pl[q] = readlane_d(pv, 48 + q);
-        wave_sync();
+        lds_order();
         double nP = 0.0, npv = pv;
         if (act) {
             double t = Pt[8 * ii + jj];
@@ -1164,33 +1255,28 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh) {
 #pragma unroll
             for (int l = 0; l < 6; ++l) npv = fma(-Tt[8 * r + l], pl[l], npv);
         }
-        wave_sync();
+        lds_order();
         if (act) Pt[8 * i + j] = nP;
         pv = npv;
-        wave_sync();
-        if (k == 0) break;
+        lds_order();
+        if (k == 0) return;
         // ---- stage kk = k-1 on P~_k, p~_k
         const int kk = k - 1;
-        double dj[9], e[6];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) dj[q] = src.AJ(q, kk);
-#pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k);
-        const ColMask mj(j), mi(ii), mr(r), mjj(jj);
+        const RicOps& o = cur.r;
         if (act) {  // PA[i][j] = P[i][j] + sum_{l<4} P[i][l] D[l][j]
             double c0, c1, c2, c3;
-            dcol(dj, mj, c0, c1, c2, c3);
+            dcol(o.dj, mj, c0, c1, c2, c3);
             Tt[8 * i + j] = fma(Pt[8 * i + 0], c0, fma(Pt[8 * i + 1], c1, fma(Pt[8 * i + 2], c2, fma(Pt[8 * i + 3], c3, Pt[8 * i + j]))));
         }
         double pp = 0.0;
         if (vec) {
             pp = pv;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) pp = fma(-Pt[8 * r + q], e[q], pp);
+            for (int q = 0; q < 6; ++q) pp = fma(-Pt[8 * r + q], o.e[q], pp);
         }
-        wave_sync();
-        const double G00 = src.RT(0, kk) + dt2 * Pt[8 * 5 + 5], G01 = src.RT(1, kk) + dt2 * Pt[8 * 5 + 4];
-        const double G11 = src.RT(2, kk) + dt2 * Pt[8 * 4 + 4];
+        lds_order();
+        const double G00 = o.R0 + dt2 * Pt[8 * 5 + 5], G01 = o.R1 + dt2 * Pt[8 * 5 + 4];
+        const double G11 = o.R3 + dt2 * Pt[8 * 4 + 4];
         const double det = G00 * G11 - G01 * G01;
         fail = fail || !(G00 > 0.0) || !(det > 0.0);
         const double idet = 1.0 / det;
@@ -1198,49 +1284,94 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh) {
         double Pk = 0.0;
         if (act) {  // P_kk[ii][jj] = Q~ + (A'PA)[ii][jj] + H'K
             double c0, c1, c2, c3;
-            dcol(dj, mi, c0, c1, c2, c3);
+            dcol(o.dj, mi, c0, c1, c2, c3);
             const double atpa = fma(c0, Tt[8 * 0 + jj], fma(c1, Tt[8 * 1 + jj], fma(c2, Tt[8 * 2 + jj], fma(c3, Tt[8 * 3 + jj], Tt[8 * ii + jj]))));
             const double H0i = dt * Tt[8 * 5 + ii], H1i = dt * Tt[8 * 4 + ii], H0j = dt * Tt[8 * 5 + jj], H1j = dt * Tt[8 * 4 + jj];
             const double K0j = -fma(Gi00, H0j, Gi01 * H1j), K1j = -fma(Gi01, H0j, Gi11 * H1j);
-            Pk = src.QT(sy6(ii, jj), kk) + atpa + fma(H0i, K0j, H1i * K1j);
+            Pk = o.qt + atpa + fma(H0i, K0j, H1i * K1j);
         }
         double ppl[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, 48 + q);
-        const double g0 = fma(dt, ppl[5], src.RV(0, kk)), g1 = fma(dt, ppl[4], src.RV(1, kk));
+        const double g0 = fma(dt, ppl[5], o.rv0), g1 = fma(dt, ppl[4], o.rv1);
         const double kf0 = -fma(Gi00, g0, Gi01 * g1), kf1 = -fma(Gi01, g0, Gi11 * g1);
         double pnew = 0.0;
         if (vec) {
             double c0, c1, c2, c3;
-            dcol(dj, mr, c0, c1, c2, c3);
+            dcol(o.dj, mr, c0, c1, c2, c3);
             double ppr = ppl[0];
 #pragma unroll
             for (int q = 1; q < 6; ++q) ppr = r == q ? ppl[q] : ppr;
             const double H0 = dt * Tt[8 * 5 + r], H1 = dt * Tt[8 * 4 + r];
-            pnew = src.QV(r, kk) + fma(c0, ppl[0], fma(c1, ppl[1], fma(c2, ppl[2], fma(c3, ppl[3], ppr)))) +
-                   fma(H0, kf0, H1 * kf1);
-            src.setK(r, kk, -fma(Gi00, H0, Gi01 * H1));
-            src.setK(6 + r, kk, -fma(Gi01, H0, Gi11 * H1));
-            src.setPV(r, kk, pnew);
+            pnew = o.qv + fma(c0, ppl[0], fma(c1, ppl[1], fma(c2, ppl[2], fma(c3, ppl[3], ppr)))) + fma(H0, kf0, H1 * kf1);
+            out.setK(r, kk, -fma(Gi00, H0, Gi01 * H1));
+            out.setK(6 + r, kk, -fma(Gi01, H0, Gi11 * H1));
+            out.setPV(r, kk, pnew);
         }
         if (lane == 0) {
-            src.setKF(0, kk, kf0);
-            src.setKF(1, kk, kf1);
+            out.setKF(0, kk, kf0);
+            out.setKF(1, kk, kf1);
         }
-        if (act && i <= j) src.setP(sy6(i, j), kk, Pk);
-        wave_sync();
+        if (act && i <= j) out.setP(sij, kk, Pk);
+        lds_order();
         if (act) Pt[8 * i + j] = Pk;
         pv = pnew;
-        wave_sync();
-        (void)mjj;
+        lds_order();
+    };
+    SoftOps oa, ob;
+    soft_ops(src, N, i, j, sij, r, vec, oa);
+    int k = N;
+    for (; k >= 1; k -= 2) {
+        stage(k, oa, ob);
+        stage(k - 1, ob, oa);
     }
+    if (k == 0) stage(0, oa, ob);
     if (lane == 0) sh.flag = fail ? 1 : 0;
     wave_sync();
 }
 
-// forward sweep with soft rows: yhat = A dx + B du - r~; dx = yhat - Y (P yhat + p)
-__device__ __noinline__ void forward_soft(const Ctx& c, int buf) {
-    const GSrc src{c};
+// forward sweep with soft rows: yhat = A dx + B du - r~; dx = yhat - Y (P yhat + p).  Operands from LDS
+// copies staged by all four waves (SoftF) or from HBM (GSrc + S_Y); the 6-vector chain is carried by
+// every lane (wave-uniform), lanes 0..5 write row r of the stage outputs.
+// staged record per stage: P 21 | PV 6 | K 12 | KF 2 | Y 21 | AJ 9 | CE 6  (77)
+constexpr int LFS = 77;
+struct SoftF {
+    const lds_double* A;
+    __device__ double P(int i, int k) const { return A[k * LFS + i]; }
+    __device__ double PV(int i, int k) const { return A[k * LFS + 21 + i]; }
+    __device__ double K(int i, int k) const { return A[k * LFS + 27 + i]; }
+    __device__ double KF(int i, int k) const { return A[k * LFS + 39 + i]; }
+    __device__ double Y(int i, int k) const { return A[k * LFS + 41 + i]; }
+    __device__ double AJ(int i, int k) const { return A[k * LFS + 62 + i]; }
+    __device__ double CR(int i, int k) const { return A[k * LFS + 71 + i]; }
+};
+struct SoftFG {
+    const Ctx& c;
+    __device__ double P(int i, int k) const { return c.S(S_P + i, k); }
+    __device__ double PV(int i, int k) const { return c.S(S_PV + i, k); }
+    __device__ double K(int i, int k) const { return c.S(S_K + i, k); }
+    __device__ double KF(int i, int k) const { return c.S(S_KF + i, k); }
+    __device__ double Y(int i, int k) const { return c.S(S_Y + i, k); }
+    __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
+    __device__ double CR(int i, int k) const { return c.S(S_CE + i, k); }
+};
+__device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A) {
+    const int NP = c.NP;
+    for (int idx = threadIdx.x; idx < LFS * NP; idx += T) {
+        const int f = idx / NP, k = idx - f * NP;
+        int g;
+        if (f < 21) g = S_P + f;
+        else if (f < 27) g = S_PV + f - 21;
+        else if (f < 39) g = S_K + f - 27;
+        else if (f < 41) g = S_KF + f - 39;
+        else if (f < 62) g = S_Y + f - 41;
+        else if (f < 71) g = S_AJ + f - 62;
+        else g = S_CE + f - 71;
+        A[k * LFS + f] = (k < c.N || f < 27 || (f >= 41 && f < 62) || f >= 71) ? c.S(g, k) : 0.0;
+    }
+}
+template <class Src>
+__device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf) {
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
     const int r = lane < 6 ? lane : 0;
@@ -1260,7 +1391,7 @@ __device__ __noinline__ void forward_soft(const Ctx& c, int buf) {
         for (int q = 0; q < 6; ++q) {
             double t = 0.0;
 #pragma unroll
-            for (int l = 0; l < 6; ++l) t = fma(c.S(S_Y + sy6(q, l), k), b[l], t);
+            for (int l = 0; l < 6; ++l) t = fma(src.Y(sy6(q, l), k), b[l], t);
             dx[q] -= t;
         }
         if (lane < 6) {
@@ -1382,11 +1513,30 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 }
                 Dm += g * d;
             }
-        double C4[10], q4[4];
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             double fw[8], zf[8], t4[4], yp[4], dwv[8];
-            (void)block_setup(c, sh, j, k, x, mu, dw, bk, fw, zf, t4, C4, q4);
+            auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) bk.G[r][q] = ld(FR_G + 4 * r + q);
+#pragma unroll
+            for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                bk.idm[a] = ld(FR_IDM + a);
+                zf[4 + a] = ld(FR_ZFL + a);
+                t4[a] = ld(FR_T + a);
+                bk.D[a] = ld(FR_D + a);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { bk.Zl[a][q] = ld(FR_ZL + 4 * a + q); bk.Yl[a][q] = ld(FR_YL + 4 * a + q); }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
+            const bool trailer = (j & 1) != 0;
+            bk.jw0[0] = bk.jw0[2] = 0.5 * (trailer ? c.a->L2 : c.a->L1);
+            bk.jw0[1] = bk.jw0[3] = 0.5 * (trailer ? c.a->W2 : c.a->W1);
             blk_recover(bk, fw, zf, t4, dx, yp, dwv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -1529,6 +1679,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
                 c.S(S_CT + i, 0) = ck[i];
                 th += fabs(ck[i]);
             }
+        const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
             double w[8], d[4];
 #pragma unroll
@@ -1539,7 +1690,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
                 ls.add(sl);
                 if (rs) { const double ew = w[e] - c.B(B_WR + e, j, k); prox += c.B(B_DRW + e, j, k) * ew * ew; }
             }
-            blk_vals(a, x, j, w, d);
+            blk_vals(a, x, tr, j, w, d);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double s = c.B(B_S + r, j, k) + alpha * c.B(B_DS + 4 * buf + r, j, k);
@@ -1880,6 +2031,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
+        const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
             double w[8], y[4], zw[8];
 #pragma unroll
@@ -1887,7 +2039,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
             for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
             Blk bk;
-            blk_lin(a, x, j, w, y, bk);
+            blk_lin(a, x, tr, j, w, y, bk);
 #pragma unroll
             for (int r = 0; r < 4; ++r) c.B(B_D + r, j, k) = bk.d[r];
 #pragma unroll
@@ -2081,12 +2233,24 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
     const bool f = phase_factor(c, sh, mu, dw);
     stamp(sh, on, OPH_FACTOR);
     if (!f) return false;
-    if (sh.R) {  // soft dynamics rows (restoration phase): HBM operands
-        if (threadIdx.x < 64) riccati_soft(c, sh);
+    if (sh.R) {  // soft dynamics rows (restoration phase)
+        if (c.lds) {
+            stage_soft_inputs(c, c.lds);
+            __syncthreads();
+            if (threadIdx.x < 64) riccati_soft(c, sh, SoftA{(const lds_double*)c.lds});
+        } else if (threadIdx.x < 64) {
+            riccati_soft(c, sh, SoftG{c});
+        }
         __syncthreads();
         stamp(sh, on, OPH_RIC_SOFT);
         if (sh.flag) return false;
-        if (threadIdx.x < 64) forward_soft(c, buf);
+        if (c.lds) {
+            stage_soft_forward(c, c.lds);
+            __syncthreads();
+            if (threadIdx.x < 64) forward_soft(c, SoftF{(const lds_double*)c.lds}, buf);
+        } else if (threadIdx.x < 64) {
+            forward_soft(c, SoftFG{c}, buf);
+        }
         __syncthreads();
         stamp(sh, on, OPH_FWD_SOFT);
         return true;
@@ -2540,11 +2704,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 c.S(S_ZLU + i, k) = c.hlu(i) ? 1.0 : 0.0;
                 c.S(S_ZUU + i, k) = c.huu(i) ? 1.0 : 0.0;
             }
+        const Trig tr = stage_trig(x);
         for (int j = 0; j < NBK; ++j) {
             double w[8], d[4];
 #pragma unroll
             for (int e = 0; e < 8; ++e) w[e] = c.B(B_W + e, j, k);
-            blk_vals(a, x, j, w, d);
+            blk_vals(a, x, tr, j, w, d);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 c.B(B_S + r, j, k) = push_into(d[r], c.rL(r), c.rU(r), c.hrl(r), true);

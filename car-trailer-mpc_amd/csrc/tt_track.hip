@@ -11,16 +11,17 @@
 // Solver: the primal-dual barrier method IPOPT runs for these NLPs (mpc_control.py:53 nlpsol
 // 'ipopt'), restated with the same constants (tol/acc, mu_init 0.1, kappa_eps 10, kappa_mu 0.2,
 // theta_mu 1.5, tau = max(.99, 1-mu), bound_relax 1e-8, bound_push/frac 1e-2, kappa_sigma 1e10,
-// exact Lagrangian Hessian) and an l1-merit line search with one second-order correction.  The
+// exact Lagrangian Hessian) and IPOPT's filter line search with one second-order correction.  The
 // Newton system is never assembled: it is the KKT system of an equality-constrained LQ problem,
-// solved by a stage-wise Riccati recursion on the FP64 matrix cores (inertia test = 2x2 Cholesky
-// of each reduced input Hessian), O(N) per iteration instead of IPOPT's sparse LDL^T.
+// solved by a stage-wise Riccati recursion on the FP64 VALU (inertia test = 2x2 Cholesky of each
+// reduced input Hessian), O(N) per iteration instead of IPOPT's sparse LDL^T.
 //
 // Lane mapping (wave-uniform control flow everywhere):
 //   * stage-parallel phases (model + Jacobian + curvature + barrier terms + residuals, step bounds,
 //     merit trials, multiplier updates): lane k owns stage k (loop k += 64 for N >= 64);
-//   * Riccati backward sweep and forward sweep (serial in k): one 16x16 f64 MFMA tile per stage,
-//     the 7x7 affine-augmented blocks spread over the 64 lanes (see phase_riccati).
+//   * Riccati backward sweep and forward sweep (serial in k): entry-parallel on the VALU, lane 8i + j
+//     owns entry (i, j) of the 7x7 affine-augmented blocks (see phase_riccati; the f64 MFMA was
+//     measured and is not faster on this dependent chain).
 //
 // LDS map (doubles).  Head (fixed offsets, immediate addressing): Qw(36) Rw(4) x_init(6) lb(8)
 // ub(8) pad(2) dump(64: per-lane sink for branch-free predicated stores).  Stage k row r at sm[kHead + k*157 + r]; the odd stride keeps lane-per-stage
@@ -1106,11 +1107,11 @@ int bound_mask(const TrackArgs& a) {
 template <int BM, int OCC = 1, int NS = 0>
 hipError_t launch(const TrackArgs& a, hipStream_t stream) {
     const int bytes = lds_bytes(a.N);
-    static int configured = 0;
-    if (bytes > 64 * 1024 && configured < bytes) {
+    // the >64 KB opt-in is per device and cheap: set it on every launch that needs it (no process-global
+    // cache that would miss a second device or race between threads)
+    if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)track_kernel<BM, OCC, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
-        configured = bytes;
     }
     hipLaunchKernelGGL((track_kernel<BM, OCC, NS>), dim3(a.B), dim3(W), bytes, stream, a);
     return hipGetLastError();
@@ -1137,7 +1138,7 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     const bool d = diagonal_weights(a);
     // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 23); at N = 40 the
     // 52 KB per wave caps a CU at 3 and the occupancy build's spills are pure cost (C3 2.01 -> 2.14 ms).
-    const bool occ_room = 5 * lds_bytes(a.N) <= 160 * 1024;
+    const bool occ_room = 5 * lds_bytes(a.N) <= kMaxLdsBytes;
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);

@@ -100,7 +100,9 @@ int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, co
 int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
                         const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
                         int* status, int* iters, double* kkt_res);
-/* Same with DEVICE pointers, asynchronous on `stream` (NULL = the default stream). */
+/* Same with DEVICE pointers, asynchronous on `stream` (NULL = the default stream).  The solver
+ * workspace belongs to the handle (grown, never shrunk, when B exceeds its capacity): calls on one
+ * handle must be serialised on ONE stream; use one handle per stream for concurrent solves. */
 int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
                                const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
                                double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream);

@@ -300,9 +300,9 @@ def test_c5_full_batch_through_the_sharded_path():
 
 
 def test_occupancy_build_is_bitwise_the_latency_build():
-    """Large batches (B > 4096, reference box, diagonal weights) launch the two-waves-per-SIMD build of
-    track_kernel; it runs the same instruction stream with a different register allocation, so every
-    instance must come out bit-identical to the same instance solved in a small (one-wave) batch."""
+    """Large batches (B > 4096, reference box, diagonal weights, N <= 23) launch the two-waves-per-SIMD
+    build of track_kernel; small N = 20 batches launch the stage-unrolled NS = 20 build.  Two different
+    builds of the same arithmetic: every instance must come out bit-identical in both."""
     from ttmpc.scenarios import synthetic_batch
     N, B = 20, 4608
     x0, xr, ur = synthetic_batch(B, N, seed=77, psi_range=0.6)
@@ -312,3 +312,20 @@ def test_occupancy_build_is_bitwise_the_latency_build():
         small = s.solve(x0[lo:lo + 1152], xr[lo:lo + 1152], ur[lo:lo + 1152])
         for a, b in zip(big, small):
             assert np.array_equal(a[lo:lo + 1152], b)
+
+
+def test_occupancy_build_boundary_n23_n24():
+    """launch_track's occupancy switch: B = 4097 at N = 23 still fits 5 waves' LDS per CU (two-waves build),
+    at N = 24 it does not (one-wave build).  Both must equal the same instances solved in small batches
+    (one-wave build)."""
+    from ttmpc.scenarios import synthetic_batch
+    B = 4097
+    for N in (23, 24):
+        x0, xr, ur = synthetic_batch(B, N, seed=5 + N)
+        s = _gpu_solver(N)
+        big = s.solve(x0, xr, ur)
+        for lo in (0, 2048, 4096):
+            hi = min(B, lo + 1024)
+            small = s.solve(x0[lo:hi], xr[lo:hi], ur[lo:hi])
+            for a, b in zip(big, small):
+                assert np.array_equal(a[lo:hi], b), N

@@ -22,9 +22,9 @@ G = REPO / "tests" / "golden"
 g = np.load(G / "reference_numpy.npz")
 obs_all = sc.obstacles_array(sc.load_obstacles(G / "obstacles.json"))
 L = ttmpc.lib()
-L.ttx_obca_set_stamps.argtypes = [C.c_void_p]
+L.ttx_obca_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
 L.ttx_obca_set_stamps.restype = C.c_int
-nph = L.ttx_obca_set_stamps(None)
+nph = L.ttx_obca_set_stamps(None, None)
 d = torch.zeros((B, nph), dtype=torch.int64, device="cuda")
 if wl == "cobs":
     x0, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], B, 50, seed=0)
@@ -41,10 +41,10 @@ else:
                          sc.OBCA_UUB, obs_all[:6], max_iter=mi)
     run = lambda: s.solve(x0, xg, z_guess=zg)  # noqa: E731
 run()  # warm-up
-L.ttx_obca_set_stamps(d.data_ptr())
+L.ttx_obca_set_stamps(s._h, d.data_ptr())
 X, U, Z, st, it, kk = run()
 torch.cuda.synchronize()
-L.ttx_obca_set_stamps(None)
+L.ttx_obca_set_stamps(s._h, None)
 cyc = d.cpu().numpy().astype(np.float64)
 names = ["lin", "compl", "factor", "riccati", "forward", "recover", "trial", "update/other", "riccati_soft",
          "forward_soft", "TOTAL"]
