@@ -24,7 +24,9 @@ struct TrackArgs {
 };
 
 // phases timed by the TT_STAMPS diagnostic build
-enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC, PH_UPDATE, PH_TOTAL, kNumPhases };
+// PH_NRIC / PH_NTRIAL: counts (Riccati attempts, line-search trials), not cycles
+enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC, PH_UPDATE, PH_NRIC, PH_NTRIAL, PH_TOTAL,
+       kNumPhases };
 
 // LDS: fixed head + rows per stage (doubles); see tt_track.hip for the map.
 constexpr int kRowsPerStage = 157;  // 156 used + 1 zero pad (odd stride: conflict-free b64)

@@ -163,8 +163,10 @@ struct Stamps {
     }
 };
 #define STAMP(ph) stamps.mark(ph)
+#define COUNT(ph) (++stamps.acc[ph])
 #else
 #define STAMP(ph) ((void)0)
+#define COUNT(ph) ((void)0)
 #endif
 
 // Armijo test with IPOPT's round-off allowance (Compare_le: lhs - rhs <= 10 eps |reference|)
@@ -415,6 +417,12 @@ template <int BM>
 __device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
     c.sm[valid ? HEAD + k * SR + row : hDUMP + (c.lane & 31)] = v;
 }
+// exec-masked LDS store: with k a compile-time stage (unrolled sweeps) the address is the lane's row
+// register plus an immediate offset, so the store costs no VALU address arithmetic at all
+template <int BM>
+__device__ __forceinline__ void mstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
+    if (valid) c.sm[HEAD + k * SR + row] = v;
+}
 
 // stage-parallel: fold the barrier, curvature and constraint terms into the Riccati operand rows
 template <int BM>
@@ -498,7 +506,8 @@ __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_ca
 
 // Backward Riccati sweep (operand rows from phase_ric_prep).  Returns false when a reduced input
 // Hessian is not positive definite (the caller raises the primal regularisation dw and retries).
-template <int BM>
+// NS > 0: horizon fixed at compile time, every stage unrolled (stage offsets fold into the DS immediates).
+template <int BM, int NS>
 __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
     EpMap m;
@@ -514,6 +523,13 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     pstore(c, m.ps >= 0, m.ps, N, Pij);
     // inertia flag accumulated without branching: a failed stage only poisons the (discarded) factors
     bool pd = true;
+    // The stage's factorisation rows leave in ONE unmasked ds_write per lane (three predicated stores
+    // cost ~100 cycles per stage, tools/ubench_riccati.hip): P^ entries from the lanes that own them
+    // (upper triangle and the p column), K^ rows from the affine/pad rows i = 6, 7 (m0, m1 depend on j
+    // only), H_uu^-1 from (6, 7), (7, 7); every other lane rewrites the uniform i11 into its slot.
+    const bool own_p = m.ps >= 0;
+    const bool spare = i < 6 && !own_p;
+    const int st_row = own_p ? m.ps : spare ? rIH + 2 : j < 6 ? rK + 6 * (i - 6) + j : j == 6 ? rKF + (i - 6) : rIH + (i - 6);
     // one stage; `o` = this stage's operands, `nx` receives stage kn's (prefetch, issued after the
     // P-tile reads so that waiting for the tile never waits for the prefetch)
     auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
@@ -554,19 +570,26 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         Pij = F - fma(g0i, m0, g1i * m1);
         PF[c.lane] = Pij;
         asm volatile("" ::: "memory");
-        // factorisation rows for the forward sweep, the step and the SOC (branch-free stores)
-        pstore(c, i < 2 && j < 7, j < 6 ? rK + 6 * i + j : rKF + i, k, i == 0 ? -m0 : -m1);
-        pstore(c, c.lane < 3, rIH + c.lane, k, c.lane == 0 ? i00 : c.lane == 1 ? i01 : i11);
-        pstore(c, m.ps >= 0, m.ps, k, Pij);
+        // factorisation rows for the forward sweep, the step and the SOC
+        c.r(st_row, k) = own_p ? Pij : spare ? i11 : j < 7 ? (i == 6 ? -m0 : -m1) : (i == 6 ? i00 : i01);
     };
     // two stages per trip with ping-pong operand buffers (no register copies between stages)
     EpOps oa = ep_ops(c, m, N - 1, dw), ob;
-    int k = N - 1;
-    for (; k >= 1; k -= 2) {
-        stage(k, oa, ob, k - 1);
-        stage(k - 1, ob, oa, k - 2);  // k - 2 = -1 prefetches harmless head words (HEAD >= SR)
+    if constexpr (NS > 0) {
+#pragma unroll
+        for (int k = NS - 1; k >= 1; k -= 2) {
+            stage(k, oa, ob, k - 1);
+            stage(k - 1, ob, oa, k >= 2 ? k - 2 : 0);
+        }
+        if constexpr (NS % 2 == 1) stage(0, oa, ob, 0);
+    } else {
+        int k = N - 1;
+        for (; k >= 1; k -= 2) {
+            stage(k, oa, ob, k - 1);
+            stage(k - 1, ob, oa, k - 2);  // k - 2 = -1 prefetches harmless head words (HEAD >= SR)
+        }
+        if (k == 0) stage(0, oa, ob, 0);
     }
-    if (k == 0) stage(0, oa, ob, 0);
     __syncthreads();
     return pd;
 }
@@ -608,8 +631,13 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bh
         y += dppd<0x4E>(y);   // quad_perm [2,3,0,1]
         y += dppd<0x141>(y);  // row_half_mirror: the 8-lane group sum, in every lane of the group
         // rows 0..5 -> dx_{k+1}; groups 6/7 -> du0/du1 at stage k
-        pstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
-        pstore(c, mm == 0 && g >= 6, orow + g, k, y);
+        if constexpr (NS > 0) {
+            mstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
+            mstore(c, mm == 0 && g >= 6, orow + g, k, y);
+        } else {
+            pstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
+            pstore(c, mm == 0 && g >= 6, orow + g, k, y);
+        }
         const double xn = bperm_d(y, src);
         x = mm < 6 ? xn : (mm == 6 ? 1.0 : 0.0);
     };
@@ -1007,7 +1035,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             bool ok = false;
             phase_ric_prep(c);
             for (int attempt = 0; attempt < 30; ++attempt) {
-                if (phase_riccati(c, dw)) { ok = true; break; }
+                COUNT(PH_NRIC);
+                if (phase_riccati<BM, NS>(c, dw)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0))
                                  : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
                 if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
@@ -1042,6 +1071,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             for (int ls = 0; !accepted; ++ls) {
                 const Trial t = phase_trial(c, alpha, rDX, ls == 0);
                 STAMP(PH_MERIT);
+                COUNT(PH_NTRIAL);
                 if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, pD, pT, ftype)) { accepted = 1; break; }
                 if (ls == 0 && isfinite(t.phi) && t.th >= th0) {
                     phase_soc_rhs(c, alpha);
@@ -1140,7 +1170,9 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // 52 KB per wave caps a CU at 3 and the occupancy build's spills are pure cost (C3 2.01 -> 2.14 ms).
     const bool occ_room = 5 * lds_bytes(a.N) <= kMaxLdsBytes;
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
+    // the BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
+    if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
     if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);
     return launch<-1>(a, stream);

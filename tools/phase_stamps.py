@@ -16,7 +16,8 @@ from ttmpc import _lib  # noqa: E402
 from ttmpc.scenarios import synthetic_batch  # noqa: E402
 from oracle import ttmpc_oracle as to  # noqa: E402
 
-PH = ["load", "linearize", "mu+barrier", "riccati", "forward", "step", "merit", "soc", "update", "total"]
+PH = ["load", "linearize", "mu+barrier", "riccati", "forward", "step", "merit", "soc", "update", "#riccati",
+      "#trials", "total"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 psi = 0.9 if N >= 40 else 0.3
@@ -54,4 +55,10 @@ print(f"B={B} N={N} iters mean {iters.mean():.2f}  status {np.bincount(st.cpu().
 tot = S[:, -1].mean()
 for i, name in enumerate(PH):
     m = S[:, i].mean()
+    if name.startswith("#"):
+        print(f"{name:12s} {m:12.2f} per instance  {m / max(iters.mean(), 1):10.2f} per iter")
+        continue
     print(f"{name:12s} {m:12.0f} cyc/instance  {m / max(iters.mean(), 1):10.0f} cyc/iter  {100 * m / tot:6.1f}%")
+nric = S[:, PH.index("#riccati")].mean()
+print(f"riccati cycles per attempt {S[:, PH.index('riccati')].mean() / max(nric, 1):.0f}; "
+      f"merit cycles per trial {S[:, PH.index('merit')].mean() / max(S[:, PH.index('#trials')].mean(), 1):.0f}")
