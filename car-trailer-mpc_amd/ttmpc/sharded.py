@@ -2,22 +2,26 @@
 
 One process per GPU (``torch.distributed``; backend "nccl" = RCCL over xGMI on the GPU box, "gloo" on
 CPU tests).  Rank 0 holds the global batch (B_total instances, e.g. 65536 mixed test_cases.json
-scenarios).  A step is
+scenarios).  A step moves every rank's shard in ``chunks`` pieces so that the transfers run under the
+solves:
 
-    scatter   rank 0 -> every rank: one contiguous input chunk per rank      (one collective)
-    solve     each rank solves its B_total / world instances, no coupling   (tt_solve_batch_device)
-    gather    every rank -> rank 0: one f64 chunk (X, U, kkt) + one i32 chunk (status, iters)
+    scatter   rank 0 -> every rank, chunk by chunk: all C scatters are issued up front (async)
+    solve     chunk c starts on the compute stream once its scatter has landed (stream wait, no host
+              sync), while the scatters of chunks c+1.. are still moving
+    gather    every rank -> rank 0, chunk c issued right behind solve c (the collective stream waits for
+              that solve), so it moves while chunk c+1 solves
     reduce    one SUM (converged, instances) and one MAX (iterations, KKT error) all-reduce
 
-Instances are independent in every iteration of the interior-point method, so these four collectives
-are the only inter-GPU traffic (the reference has no counterpart: simulation.py solves one NLP at a
-time on one core).  Shards are contiguous: rank r owns global instances [r*per, (r+1)*per).  When
-B_total is not a multiple of the world size, the tail is padded with copies of instance 0, which are
-solved but excluded from the outputs and the statistics.
+Only the first scatter and the last gather sit on the critical path; with C chunks the exposed transfer
+time drops to about 2/C of the serial scatter + gather.  Instances are independent in every iteration of
+the interior-point method, so these collectives are the only inter-GPU traffic (the reference has no
+counterpart: simulation.py solves one NLP at a time on one core).  Shards are contiguous: rank r owns
+global instances [r*per, (r+1)*per), chunk c of it [c*pc, (c+1)*pc).  Padding slots (B_total not a
+multiple of world * chunks) hold copies of instance 0: solved, excluded from outputs and statistics.
 
-Chunk layouts (f64, instance-major inside each block, so the solver reads the blocks in place):
-    input  chunk  [x0 (per,6) | xref (per,N+1,6) | uref (per,N,2)]
-    output chunk  [X (per,N+1,6) | U (per,N,2) | kkt (per,)]       + i32 [status (per,) | iters (per,)]
+Chunk layouts (f64, chunk-major, instance-major inside each block, so the solver reads them in place):
+    input  chunk  [x0 (pc,6) | xref (pc,N+1,6) | uref (pc,N,2)]
+    output chunk  [X (pc,N+1,6) | U (pc,N,2) | kkt (pc,)]       + i32 [status (pc,) | iters (pc,)]
 """
 from __future__ import annotations
 
@@ -27,92 +31,126 @@ import numpy as np
 import torch
 
 
+class _Chunk:
+    """Views of one chunk of this rank's shard."""
+
+    def __init__(self, recv_in, out_f, out_i, pc, N):
+        a, b = pc * 6, pc * (N + 1) * 6
+        self.x0 = recv_in[:a].view(pc, 6)
+        self.xr = recv_in[a:a + b].view(pc, N + 1, 6)
+        self.ur = recv_in[a + b:].view(pc, N, 2)
+        a, b = pc * (N + 1) * 6, pc * N * 2
+        self.X = out_f[:a].view(pc, N + 1, 6)
+        self.U = out_f[a:a + b].view(pc, N, 2)
+        self.kkt = out_f[a + b:]
+        self.st = out_i[:pc]
+        self.it = out_i[pc:]
+
+
 class ShardedBatch:
     """Scatter / solve / gather of one global batch across the ranks of a process group.
 
-    ``solve_shard(x0, xref, uref, X, U, status, iters, kkt)`` receives tensor views of this rank's
-    chunk (on ``device``) and must fill X, U, status, iters, kkt; on a GPU it enqueues
-    ``BatchSolver.solve_device`` on the current stream (see ``gpu_shard_solver``)."""
+    ``solve_shard(x0, xref, uref, X, U, status, iters, kkt)`` receives tensor views of one chunk (on
+    ``device``) and must fill X, U, status, iters, kkt; on a GPU it enqueues ``BatchSolver.solve_device``
+    on the current stream (see ``gpu_shard_solver``).  ``chunks`` pieces per shard (>= 1) overlap the
+    transfers with the solves."""
 
-    def __init__(self, B_total: int, N: int, solve_shard, device=None, group=None):
+    def __init__(self, B_total: int, N: int, solve_shard, device=None, group=None, chunks: int = 1):
         import torch.distributed as dist
         self.dist = dist if dist.is_available() and dist.is_initialized() else None
         self.group = group
         self.world = self.dist.get_world_size(group) if self.dist else 1
         self.rank = self.dist.get_rank(group) if self.dist else 0
         self.B_total, self.N = int(B_total), int(N)
-        self.per = max(1, math.ceil(self.B_total / self.world))
+        per0 = max(1, math.ceil(self.B_total / self.world))
+        self.chunks = max(1, min(int(chunks), per0))
+        self.pc = math.ceil(per0 / self.chunks)             # instances per chunk
+        self.per = self.pc * self.chunks                    # shard size (padded)
         self.lo = self.rank * self.per
         self.valid = max(0, min(self.per, self.B_total - self.lo))   # real instances on this rank
         self.device = torch.device("cpu") if device is None else torch.device(device)
         self.solve_shard = solve_shard
-        per, N = self.per, self.N
-        self.in_sizes = (per * 6, per * (N + 1) * 6, per * N * 2)
-        self.out_sizes = (per * (N + 1) * 6, per * N * 2, per)
+        pc, N, C = self.pc, self.N, self.chunks
+        self.in_chunk = pc * (6 + (N + 1) * 6 + N * 2)
+        self.out_chunk = pc * ((N + 1) * 6 + N * 2 + 1)
         f64 = dict(dtype=torch.float64, device=self.device)
-        self.recv_in = torch.empty(sum(self.in_sizes), **f64)
-        self.out_f = torch.empty(sum(self.out_sizes), **f64)
-        self.out_i = torch.empty(2 * per, dtype=torch.int32, device=self.device)
-        a, b, _ = self.in_sizes
-        self.x0 = self.recv_in[:a].view(per, 6)
-        self.xr = self.recv_in[a:a + b].view(per, N + 1, 6)
-        self.ur = self.recv_in[a + b:].view(per, N, 2)
-        a, b, _ = self.out_sizes
-        self.X = self.out_f[:a].view(per, N + 1, 6)
-        self.U = self.out_f[a:a + b].view(per, N, 2)
-        self.kkt = self.out_f[a + b:]
-        self.st = self.out_i[:per]
-        self.it = self.out_i[per:]
-        self.valid_mask = torch.zeros(per, dtype=torch.bool, device=self.device)
+        self.recv_in = torch.empty((C, self.in_chunk), **f64)
+        self.out_f = torch.empty((C, self.out_chunk), **f64)
+        self.out_i = torch.empty((C, 2 * pc), dtype=torch.int32, device=self.device)
+        self.parts = [_Chunk(self.recv_in[c], self.out_f[c], self.out_i[c], pc, N) for c in range(C)]
+        self.valid_mask = torch.zeros(self.per, dtype=torch.bool, device=self.device)
         self.valid_mask[: self.valid] = True
         if self.rank == 0:
-            self.gather_f = torch.empty((self.world, self.out_f.numel()), **f64)
-            self.gather_i = torch.empty((self.world, self.out_i.numel()), dtype=torch.int32, device=self.device)
+            self.gather_f = torch.empty((self.world, C, self.out_chunk), **f64)
+            self.gather_i = torch.empty((self.world, C, 2 * pc), dtype=torch.int32, device=self.device)
         self.send_in = None
 
-    # ---- rank 0: lay the global batch out as one input chunk per rank (done once, outside the step) ----
+    # ---- rank 0: lay the global batch out as chunk records per rank (done once, outside the step) ----
     def pack_inputs(self, x0, xref, uref):
-        """Global arrays (B_total,6), (B_total,N+1,6), (B_total,N,2) on rank 0 -> the (world, chunk)
-        scatter source, resident on this rank's device."""
+        """Global arrays (B_total,6), (B_total,N+1,6), (B_total,N,2) on rank 0 -> the (world, chunks,
+        record) scatter source, resident on this rank's device."""
         if self.rank != 0:
             return None
-        B, N, per, W = self.B_total, self.N, self.per, self.world
+        B, N, pc, W, C = self.B_total, self.N, self.pc, self.world, self.chunks
         t = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64) if not torch.is_tensor(a) else a,  # noqa: E731
                                       dtype=torch.float64)
         x0, xref, uref = t(x0).reshape(B, 6), t(xref).reshape(B, N + 1, 6), t(uref).reshape(B, N, 2)
-        pad = per * W - B
+        pad = pc * C * W - B
         if pad:
             x0 = torch.cat([x0, x0[:1].expand(pad, 6)])
             xref = torch.cat([xref, xref[:1].expand(pad, N + 1, 6)])
             uref = torch.cat([uref, uref[:1].expand(pad, N, 2)])
-        send = torch.cat([x0.reshape(W, -1), xref.reshape(W, -1), uref.reshape(W, -1)], dim=1)
-        self.send_in = send.to(self.device).contiguous()
+        WC = W * C
+        send = torch.cat([x0.reshape(WC, -1), xref.reshape(WC, -1), uref.reshape(WC, -1)], dim=1)
+        self.send_in = send.reshape(W, C, self.in_chunk).to(self.device).contiguous()
         return self.send_in
 
+    def solve_local(self):
+        """Solve every chunk of this rank's shard from recv_in (no communication)."""
+        for p in self.parts:
+            self.solve_shard(p.x0, p.xr, p.ur, p.X, p.U, p.st, p.it, p.kkt)
+
     def step(self):
-        """One scatter -> solve -> gather -> reduce.  Returns the global statistics (every rank):
-        dict(converged, instances, iters_max, kkt_max)."""
+        """One pipelined scatter -> solve -> gather, then the stats reduction.  Returns the global
+        statistics tensors (every rank): see ``stats``."""
         d = self.dist
+        C = self.chunks
         if d is None or self.world == 1:
-            self.recv_in.copy_(self.send_in[0])
+            for c, p in enumerate(self.parts):
+                self.recv_in[c].copy_(self.send_in[0, c])
+                self.solve_shard(p.x0, p.xr, p.ur, p.X, p.U, p.st, p.it, p.kkt)
+                self.gather_f[0, c].copy_(self.out_f[c])
+                self.gather_i[0, c].copy_(self.out_i[c])
         else:
-            src = list(self.send_in.unbind(0)) if self.rank == 0 else None
-            d.scatter(self.recv_in, src, src=0, group=self.group)
-        self.solve_shard(self.x0, self.xr, self.ur, self.X, self.U, self.st, self.it, self.kkt)
-        if d is None or self.world == 1:
-            self.gather_f[0].copy_(self.out_f)
-            self.gather_i[0].copy_(self.out_i)
-        else:
-            d.gather(self.out_f, list(self.gather_f.unbind(0)) if self.rank == 0 else None, dst=0, group=self.group)
-            d.gather(self.out_i, list(self.gather_i.unbind(0)) if self.rank == 0 else None, dst=0, group=self.group)
+            g = self.group
+            root = self.rank == 0
+            sc = [d.scatter(self.recv_in[c], list(self.send_in[:, c].unbind(0)) if root else None, src=0, group=g,
+                            async_op=True) for c in range(C)]
+            gathers = []
+            for c, p in enumerate(self.parts):
+                sc[c].wait()   # NCCL: the compute stream waits for the scatter; gloo: the host does
+                self.solve_shard(p.x0, p.xr, p.ur, p.X, p.U, p.st, p.it, p.kkt)
+                gathers.append(d.gather(self.out_f[c], list(self.gather_f[:, c].unbind(0)) if root else None, dst=0,
+                                        group=g, async_op=True))
+                gathers.append(d.gather(self.out_i[c], list(self.gather_i[:, c].unbind(0)) if root else None, dst=0,
+                                        group=g, async_op=True))
+            for w in gathers:
+                w.wait()
         m = self.valid_mask
-        ssum = torch.stack([((self.st <= 1) & m).sum(), m.sum()]).to(torch.float64)
-        smax = torch.stack([torch.where(m, self.it, 0).max().to(torch.float64),
-                            torch.where(m, self.kkt, float("-inf")).max()])
+        st, it, kk = self.status(), self.iters(), self.out_f[:, -self.pc:].reshape(-1)
+        ssum = torch.stack([((st <= 1) & m).sum(), m.sum()]).to(torch.float64)
+        smax = torch.stack([torch.where(m, it, 0).max().to(torch.float64), torch.where(m, kk, float("-inf")).max()])
         if d is not None and self.world > 1:
             d.all_reduce(ssum, op=d.ReduceOp.SUM, group=self.group)
             d.all_reduce(smax, op=d.ReduceOp.MAX, group=self.group)
         return ssum, smax
+
+    def status(self):
+        """This rank's shard statuses (per,), chunk order = instance order."""
+        return self.out_i[:, :self.pc].reshape(-1)
+
+    def iters(self):
+        return self.out_i[:, self.pc:].reshape(-1)
 
     @staticmethod
     def stats(ssum, smax):
@@ -123,14 +161,15 @@ class ShardedBatch:
         """Rank 0: the global (X, U, status, iters, kkt) in the original instance order (numpy)."""
         if self.rank != 0:
             return None
-        B, N, per, W = self.B_total, self.N, self.per, self.world
-        a, b, _ = self.out_sizes
+        B, N, pc = self.B_total, self.N, self.pc
+        T = self.world * self.chunks * pc
+        a, b = pc * (N + 1) * 6, pc * N * 2
         gf, gi = self.gather_f.cpu(), self.gather_i.cpu()
-        X = gf[:, :a].reshape(W * per, N + 1, 6)[:B].numpy()
-        U = gf[:, a:a + b].reshape(W * per, N, 2)[:B].numpy()
-        kk = gf[:, a + b:].reshape(W * per)[:B].numpy()
-        st = gi[:, :per].reshape(W * per)[:B].numpy()
-        it = gi[:, per:].reshape(W * per)[:B].numpy()
+        X = gf[:, :, :a].reshape(T, N + 1, 6)[:B].numpy()
+        U = gf[:, :, a:a + b].reshape(T, N, 2)[:B].numpy()
+        kk = gf[:, :, a + b:].reshape(T)[:B].numpy()
+        st = gi[:, :, :pc].reshape(T)[:B].numpy()
+        it = gi[:, :, pc:].reshape(T)[:B].numpy()
         return X, U, st, it, kk
 
 

@@ -83,13 +83,13 @@ def _oracle_shard_solver(N):
     return run
 
 
-def _sharded_worker(rank, world, port, B, N, outdir):
+def _sharded_worker(rank, world, port, B, N, outdir, chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import bench
         from ttmpc.sharded import ShardedBatch
-        sb = ShardedBatch(B, N, _oracle_shard_solver(N))
+        sb = ShardedBatch(B, N, _oracle_shard_solver(N), chunks=chunks)
         if rank == 0:
             x0, xr, ur = bench.workload("c5", B, N, seed=3)
             sb.pack_inputs(x0, xr, ur)
@@ -104,13 +104,15 @@ def _sharded_worker(rank, world, port, B, N, outdir):
         dist.destroy_process_group()
 
 
-def test_two_rank_scatter_solve_gather(tmp_path):
-    """Ragged global batch (B=37 over 2 ranks: 19 + 18, one padded slot) scattered from rank 0,
-    solved per shard, gathered back in order; equals one unsharded solve of the whole batch."""
+@pytest.mark.parametrize("chunks, valid", [(1, [19, 18]), (3, [21, 16])])
+def test_two_rank_scatter_solve_gather(tmp_path, chunks, valid):
+    """Ragged global batch (B=37 over 2 ranks) scattered from rank 0 in `chunks` pipelined pieces per
+    shard (1: 19 + 18 with one padded slot; 3: chunks of 7, 21 + 16 with five padded slots), solved per
+    chunk, gathered back in order; equals one unsharded solve of the whole batch."""
     import bench
     from ttmpc import layout
     world, B, N = 2, 37, 20
-    mp.spawn(_sharded_worker, args=(world, _free_port(), B, N, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_sharded_worker, args=(world, _free_port(), B, N, str(tmp_path), chunks), nprocs=world, join=True)
     res = np.load(tmp_path / "res.npz")
     x0, xr, ur = bench.workload("c5", B, N, seed=3)
     X = torch.empty((B, N + 1, 6), dtype=torch.float64)
@@ -123,7 +125,7 @@ def test_two_rank_scatter_solve_gather(tmp_path):
     assert np.array_equal(res["st"], st.numpy()) and np.array_equal(res["it"], it.numpy())
     assert np.allclose(layout.pack(res["X"], res["U"])[:, :6], x0)      # x_0 = x_init survived the round trip
     s = [np.load(tmp_path / f"s{r}.npz") for r in range(world)]
-    assert [int(x["valid"]) for x in s] == [19, 18]
+    assert [int(x["valid"]) for x in s] == valid
     for x in s:
         conv, inst, imax, kmax = x["stats"]
         assert int(inst) == B and int(conv) == int(np.sum(st.numpy() <= 1))
