@@ -207,19 +207,9 @@ __global__ void __launch_bounds__(64) collision_kernel(int B, int K, long long s
 }
 
 // ---- disturbed plant: update(q, u, params, DISTURBANCE_PARAMS), simulation.py:167-199 ------------------
-__global__ void __launch_bounds__(kThreads) plant_kernel(int B, tt_plant p, double* __restrict__ state,
-                                                         const double* __restrict__ u, long long u_stride,
-                                                         const int* __restrict__ status, int zero_on_fail,
-                                                         double* __restrict__ u_applied) {
+// one instance in place: q (6) <- update(q, (a, om)); (a, om) before friction/slippage scaling
+__device__ __forceinline__ void plant_apply(const tt_plant& p, double* q, double a, double om) {
 #pragma clang fp contract(off)
-    const int b = blockIdx.x * kThreads + threadIdx.x;
-    if (b >= B) return;
-    double q[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) q[i] = state[(size_t)b * 6 + i];
-    double a = u[b * u_stride], om = u[b * u_stride + 1];
-    if (zero_on_fail && status && status[b] > TT_ACCEPTABLE) { a = 0.0; om = 0.0; }   // simulation_nmpc.py:208-214
-    if (u_applied) { u_applied[(size_t)b * 2] = a; u_applied[(size_t)b * 2 + 1] = om; }
     if (p.enable) { a *= p.friction_coeff; om *= p.slippage_coeff; }                     // apply_disturbances 66-80
     const double th = q[2], ps = q[3], ph = q[4], v = q[5];
     double qd[6];                                                                        // f_dyn 34-48
@@ -241,8 +231,99 @@ __global__ void __launch_bounds__(kThreads) plant_kernel(int B, tt_plant p, doub
         q[0] += mag * cos(th + M_PI / 2) * p.dt;
         q[1] += mag * sin(th + M_PI / 2) * p.dt;
     }
+}
+
+__global__ void __launch_bounds__(kThreads) plant_kernel(int B, tt_plant p, double* __restrict__ state,
+                                                         const double* __restrict__ u, long long u_stride,
+                                                         const int* __restrict__ status, int zero_on_fail,
+                                                         double* __restrict__ u_applied) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= B) return;
+    double q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = state[(size_t)b * 6 + i];
+    double a = u[b * u_stride], om = u[b * u_stride + 1];
+    if (zero_on_fail && status && status[b] > TT_ACCEPTABLE) { a = 0.0; om = 0.0; }   // simulation_nmpc.py:208-214
+    if (u_applied) { u_applied[(size_t)b * 2] = a; u_applied[(size_t)b * 2 + 1] = om; }
+    plant_apply(p, q, a, om);
 #pragma unroll
     for (int i = 0; i < 6; ++i) state[(size_t)b * 6 + i] = q[i];
+}
+
+// ---- closed-loop failure policies of the three drivers, fused with the plant update ----------------------
+// success (status <= acceptable): u = inputs[:, 0], last = u, consecutive = 0.  On failure (failure_count++,
+// consecutive++):
+//   TT_POLICY_TRACK  simulation.py:519-527        u = inputs[:, 0] as returned (no failure branch)
+//   TT_POLICY_NMPC   simulation_nmpc.py:206-216   u = 0, last = 0; consecutive > 20: stop
+//   TT_POLICY_FUZZY  simulation_fuzzy.py:207-221  u = last; consecutive > 15: u = 0; consecutive > 30: stop
+// A stopped instance (the reference's `break`, before update) keeps its state and applies nothing from then on.
+__global__ void __launch_bounds__(kThreads) policy_plant_kernel(int B, tt_plant p, int policy, double* __restrict__ state,
+                                                                const double* __restrict__ u, long long u_stride,
+                                                                const int* __restrict__ status, double* __restrict__ u_last,
+                                                                int* __restrict__ consec, int* __restrict__ fails,
+                                                                int* __restrict__ active, double* __restrict__ u_applied) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= B) return;
+    double a = 0.0, om = 0.0;
+    bool go = active[b] != 0;
+    if (go) {
+        if (status[b] <= TT_ACCEPTABLE) {
+            a = u[b * u_stride];
+            om = u[b * u_stride + 1];
+            u_last[(size_t)b * 2] = a;
+            u_last[(size_t)b * 2 + 1] = om;
+            consec[b] = 0;
+        } else {
+            fails[b] += 1;
+            const int cf = consec[b] + 1;
+            consec[b] = cf;
+            if (policy == TT_POLICY_NMPC) {
+                u_last[(size_t)b * 2] = u_last[(size_t)b * 2 + 1] = 0.0;
+                if (cf > 20) go = false;
+            } else if (policy == TT_POLICY_FUZZY) {
+                a = u_last[(size_t)b * 2];
+                om = u_last[(size_t)b * 2 + 1];
+                if (cf > 15) { a = 0.0; om = 0.0; }
+                if (cf > 30) go = false;
+            } else {
+                a = u[b * u_stride];
+                om = u[b * u_stride + 1];
+            }
+        }
+        if (!go) { a = 0.0; om = 0.0; active[b] = 0; }
+    }
+    if (u_applied) { u_applied[(size_t)b * 2] = a; u_applied[(size_t)b * 2 + 1] = om; }
+    if (!go) return;
+    double q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) q[i] = state[(size_t)b * 6 + i];
+    plant_apply(p, q, a, om);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) state[(size_t)b * 6 + i] = q[i];
+}
+
+// ---- fuzzy weights (mpc_control_fuzzy.py:90-119) from the measured state and the window's first reference
+// speed: hitch-angle severity h = min(|psi| / 0.35, 1), reversing (ref v or v < -0.1) scales by 1.1 / 1.2,
+// weights clipped to [1, 3.5].  w[b] = (q0..q5, r0, r1).
+__global__ void __launch_bounds__(kThreads) fuzzy_kernel(int B, int N, const double* __restrict__ x,
+                                                         const double* __restrict__ xref, double* __restrict__ w) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= B) return;
+    const double psi = x[(size_t)b * 6 + 3], v = x[(size_t)b * 6 + 5];
+    const double ref_v = xref[(size_t)b * (N + 1) * 6 + 5];
+    const double h = fmin(fabs(psi) / 0.35, 1.0);
+    const bool reversing = (ref_v < -0.1) || (v < -0.1);
+    double hitch = 1.0 + 2.0 * h, steer = 1.0 + 1.2 * h, steer_rate = 1.0 + 1.5 * h;
+    if (reversing) { hitch *= 1.1; steer *= 1.1; steer_rate *= 1.2; }
+    auto clip = [](double t) { return fmin(fmax(t, 1.0), 3.5); };
+    double* o = w + (size_t)b * 8;
+    o[0] = 1.0; o[1] = 1.0;
+    o[2] = clip(fmax(1.0, steer));
+    o[3] = clip(fmax(1.0, hitch));
+    o[4] = clip(fmax(1.0, steer));
+    o[5] = 1.0;
+    o[6] = 1.0;
+    o[7] = clip(fmax(1.0, steer_rate));
 }
 
 // ---- NMPC warm start: z_guess = have ? shift(last) : [xr_0, ur_0, ..., xr_N] ----------------------------
@@ -384,6 +465,25 @@ int tt_plant_update_device(int B, const tt_plant* p, double* state, const double
     hipLaunchKernelGGL(plant_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, *p, state, u,
                        u_stride, status, zero_on_fail, u_applied);
     return launched("plant_kernel");
+}
+
+int tt_policy_plant_device(int B, const tt_plant* p, int policy, double* state, const double* u, long long u_stride,
+                           const int* status, double* u_last, int* consecutive, int* failures, int* active,
+                           double* u_applied, void* stream) {
+    if (B < 0 || !p || !state || !u || u_stride < 2 || !status || !u_last || !consecutive || !failures || !active ||
+        policy < TT_POLICY_TRACK || policy > TT_POLICY_FUZZY)
+        return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(policy_plant_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, *p, policy,
+                       state, u, u_stride, status, u_last, consecutive, failures, active, u_applied);
+    return launched("policy_plant_kernel");
+}
+
+int tt_fuzzy_weights_device(int B, int N, const double* x, const double* xref, double* wq_wr, void* stream) {
+    if (B < 0 || N < 1 || !x || !xref || !wq_wr) return -EINVAL;
+    if (B == 0) return 0;
+    hipLaunchKernelGGL(fuzzy_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, N, x, xref, wq_wr);
+    return launched("fuzzy_kernel");
 }
 
 int tt_warm_start_device(int B, int N, const double* last, const int* have, const double* xref, const double* uref,

@@ -107,7 +107,9 @@ def lib():
            "tt_interpolate_device": [i, i, i, vp, vp, vp, vp, vp],
            "tt_lqr_score_device": [i, C.POINTER(TTPlant), _dp, _dp, vp, vp, vp, vp, vp, vp, vp],
            "tt_sim_window_indexed_device": [i, i, vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp],
-           "tt_sim_log_advance_device": [i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]}
+           "tt_sim_log_advance_device": [i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+           "tt_policy_plant_device": [i, C.POINTER(TTPlant), i, vp, vp, ll, vp, vp, vp, vp, vp, vp, vp],
+           "tt_fuzzy_weights_device": [i, i, vp, vp, vp, vp]}
     for name, args in sim.items():
         if os.environ.get("TTMPC_LIB") and not hasattr(L, name):
             continue  # A/B diagnostics against an older build
@@ -123,7 +125,8 @@ EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_
                     "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version", "tt_sim_window_device",
                     "tt_collision_device", "tt_plant_update_device", "tt_warm_start_device",
                     "tt_record_solution_device", "tt_interpolate_device", "tt_lqr_score_device",
-                    "tt_sim_window_indexed_device", "tt_sim_log_advance_device")
+                    "tt_sim_window_indexed_device", "tt_sim_log_advance_device", "tt_policy_plant_device",
+                    "tt_fuzzy_weights_device")
 
 
 def _ptr(a):

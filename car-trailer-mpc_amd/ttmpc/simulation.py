@@ -24,7 +24,10 @@ import math
 import numpy as np
 import torch
 
-from ._lib import TT_ACCEPTABLE, TTError, TTPlant, lib
+from ._lib import TT_ACCEPTABLE, TT_VARIANT_FUZZY, TTError, TTPlant, lib
+
+# closed-loop failure policies (include/ttmpc.h TT_POLICY_*): what a driver does after a failed solve
+POLICIES = {"track": 0, "nmpc": 1, "fuzzy": 2}
 
 # simulation.py:26-32
 DISTURBANCE_PARAMS = {"friction_coeff": 0.9, "slippage_coeff": 0.9, "process_noise_std": 0.02,
@@ -151,12 +154,21 @@ class ClosedLoop:
     """B independent closed loops driven by one tracking solver (a ttmpc.BatchSolver of horizon N).
 
     plan_x / plan_u: one shared plan in the reference's (6,Np+1) / (2,Np) orientation (e.g.
-    do_interpolation(state_traj.txt, ...)), or (B,Np+1,6) / (B,Np,2) per-instance plans.  warm_start=True is TruckTrailerNMPC's shifted warm start (NMPC / fuzzy solvers);
-    zero_on_fail=True applies zero control after a failed solve (simulation_nmpc.py:204-214)."""
+    do_interpolation(state_traj.txt, ...)), or (B,Np+1,6) / (B,Np,2) per-instance plans.  warm_start=True
+    is TruckTrailerNMPC's shifted warm start (NMPC / fuzzy solvers).
+
+    policy: the driver's reaction to a failed solve, on the device per instance (tt_policy_plant_device):
+      "track" (simulation.py:519-527) applies the returned inputs; "nmpc" (simulation_nmpc.py:206-216)
+      applies zero control and stops the instance after 20 consecutive failures; "fuzzy"
+      (simulation_fuzzy.py:207-221) re-applies the last successful control, zero after 15 consecutive
+      failures, stops after 30.  Default: "fuzzy" for a TT_VARIANT_FUZZY solver, "nmpc" when
+      zero_on_fail=True, else "track".  A TT_VARIANT_FUZZY solver gets per-instance fuzzy weights each step
+      (tt_fuzzy_weights_device, mpc_control_fuzzy.py:90-119) and its failed instances are re-solved once
+      with unit weights from the same guess (145-159)."""
 
     def __init__(self, solver, plan_x, plan_u, params, disturbance_params=None, measurement_noise=None,
                  obstacles=None, check_collision=True, switch_solver=None, warm_start=False, bug_compatible=True,
-                 zero_on_fail=False, device=None, seed=0):
+                 zero_on_fail=False, device=None, seed=0, policy=None):
         self.solver = solver
         self.N = solver.N
         self.dev = torch.device("cuda", solver.device if device is None else device)
@@ -173,6 +185,12 @@ class ClosedLoop:
         self.check_collision = check_collision and self.obstacles is not None
         self.switch = switch_solver
         self.warm, self.bug_compatible, self.zero_on_fail = warm_start, bug_compatible, zero_on_fail
+        self.fuzzy = getattr(solver, "variant", None) == TT_VARIANT_FUZZY
+        if policy is None:
+            policy = "fuzzy" if self.fuzzy else ("nmpc" if zero_on_fail else "track")
+        if policy not in POLICIES:
+            raise ValueError(f"policy must be one of {sorted(POLICIES)}")
+        self.policy = policy
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
         self.stream = torch.cuda.Stream(self.dev)
@@ -191,6 +209,13 @@ class ClosedLoop:
         self.kkt = torch.empty(B, dtype=f, device=d)
         self.flag = torch.zeros(B, dtype=torch.int32, device=d)
         self.u_applied = torch.empty((B, 2), dtype=f, device=d)
+        # failure-policy state (tt_policy_plant_device)
+        self.u_last = torch.zeros((B, 2), dtype=f, device=d)
+        self.consec = torch.zeros(B, dtype=torch.int32, device=d)
+        self.fails = torch.zeros(B, dtype=torch.int32, device=d)
+        self.active = torch.ones(B, dtype=torch.int32, device=d)
+        if self.fuzzy:
+            self.wq = torch.empty((B, 8), dtype=f, device=d)
         if self.warm:
             self.zg = torch.empty((B, 8 * N + 6), dtype=f, device=d)
             self.last = torch.zeros((B, 8 * N + 6), dtype=f, device=d)
@@ -220,18 +245,52 @@ class ClosedLoop:
                                               self.uref.data_ptr(), int(self.bug_compatible), self.zg.data_ptr(), sp),
                        "tt_warm_start_device")
                 zg = self.zg.data_ptr()
+            wq = 0
+            if self.fuzzy:
+                _check(L.tt_fuzzy_weights_device(B, N, self.x_meas.data_ptr(), self.xref.data_ptr(), self.wq.data_ptr(),
+                                                 sp), "tt_fuzzy_weights_device")
+                wq = self.wq.data_ptr()
             self.solver.solve_device(B, self.x_meas.data_ptr(), self.xref.data_ptr(), self.uref.data_ptr(),
                                      self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(), self.it.data_ptr(),
-                                     self.kkt.data_ptr(), z_guess=zg, stream=s.cuda_stream)
+                                     self.kkt.data_ptr(), wq_wr=wq, z_guess=zg, stream=s.cuda_stream)
+            if self.fuzzy:
+                self._fuzzy_retry(s)
             if self.switch is not None and self.check_collision:
                 self._switch_solve(s)
             if self.warm:
                 _check(L.tt_record_solution_device(B, N, self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(),
                                                    self.last.data_ptr(), self.have.data_ptr(), sp),
                        "tt_record_solution_device")
-            plant_update(self.state, self.U, self.params, self.dist, self.st, self.zero_on_fail, self.u_applied,
-                         stream=s)
+            self._policy_plant(sp)
         self.first = False
+
+    def _policy_plant(self, sp):
+        p = plant(self.params, self.dist)
+        _check(lib().tt_policy_plant_device(self.B, C.byref(p), POLICIES[self.policy], self.state.data_ptr(),
+                                            self.U.data_ptr(), self.U.stride(0), self.st.data_ptr(),
+                                            self.u_last.data_ptr(), self.consec.data_ptr(), self.fails.data_ptr(),
+                                            self.active.data_ptr(), self.u_applied.data_ptr(), sp),
+               "tt_policy_plant_device")
+
+    def _fuzzy_retry(self, s):
+        """mpc_control_fuzzy.py:145-159: failed instances re-solve once with unit weights, same guess."""
+        idx = torch.nonzero((self.st > TT_ACCEPTABLE) & (self.active != 0), as_tuple=True)[0]
+        n = int(idx.numel())          # host sync: the compaction size decides the retry launch
+        if n == 0:
+            return
+        N = self.N
+        x0, xr, ur = self.x_meas[idx].contiguous(), self.xref[idx].contiguous(), self.uref[idx].contiguous()
+        w = torch.ones((n, 8), dtype=torch.float64, device=self.dev)
+        zg = self.zg[idx].contiguous() if self.warm else None
+        X = torch.empty((n, N + 1, 6), dtype=torch.float64, device=self.dev)
+        U = torch.empty((n, N, 2), dtype=torch.float64, device=self.dev)
+        st = torch.empty(n, dtype=torch.int32, device=self.dev)
+        it = torch.empty(n, dtype=torch.int32, device=self.dev)
+        kk = torch.empty(n, dtype=torch.float64, device=self.dev)
+        self.solver.solve_device(n, x0.data_ptr(), xr.data_ptr(), ur.data_ptr(), X.data_ptr(), U.data_ptr(),
+                                 st.data_ptr(), it.data_ptr(), kk.data_ptr(), wq_wr=w.data_ptr(),
+                                 z_guess=0 if zg is None else zg.data_ptr(), stream=s.cuda_stream)
+        self.X[idx], self.U[idx], self.st[idx], self.it[idx], self.kkt[idx] = X, U, st, it, kk
 
     # ---------------- hipGraph replay of the closed loop ----------------
     def _graph_step(self, first, d_ks, d_step, noise_all, logs):
@@ -261,7 +320,7 @@ class ClosedLoop:
             _check(L.tt_record_solution_device(B, N, self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(),
                                                self.last.data_ptr(), self.have.data_ptr(), sp),
                    "tt_record_solution_device")
-        plant_update(self.state, self.U, self.params, self.dist, self.st, self.zero_on_fail, self.u_applied, stream=s)
+        self._policy_plant(sp)
         S, Ua, Ss, Si, Sc = logs
         _check(L.tt_sim_log_advance_device(B, d_step.data_ptr(), self.state.data_ptr(), self.u_applied.data_ptr(),
                                            self.st.data_ptr(), self.it.data_ptr(),
@@ -275,8 +334,9 @@ class ClosedLoop:
         simulation.py:503-506), steps 1.. replay the captured step.  The step index, the reference's k
         sequence and the measurement noise of every step are device-resident.  Not available with a switch
         solver (its compaction needs the host).  Same logs as run()."""
-        if self.switch is not None:
-            raise ValueError("run_graph does not support the switch solver; use run()")
+        if self.switch is not None or self.fuzzy:
+            raise ValueError("run_graph supports neither the switch solver nor the fuzzy retry (host compaction); "
+                             "use run()")
         ks = step_indices(T_sim, float(self.params["dt"]))
         self.reset(x_init)
         B, K, d, s = self.B, len(ks), self.dev, self.stream
@@ -307,8 +367,8 @@ class ClosedLoop:
         torch.cuda.synchronize(d)
         self.first = False
         S, Ua, Ss, Si, Sc = (t.cpu().numpy() for t in logs)
-        return {"k": np.array(ks), "states": S, "controls": Ua, "status": Ss, "iters": Si,
-                "collide": Sc.astype(bool), "success": Ss <= TT_ACCEPTABLE}
+        return dict(self._policy_logs(), k=np.array(ks), states=S, controls=Ua, status=Ss, iters=Si,
+                    collide=Sc.astype(bool), success=Ss <= TT_ACCEPTABLE)
 
     def _switch_solve(self, s):
         """USE_SWITCH_MPC: instances whose check collided use MPCTrackingControlObs (simulation.py:506-512)."""
@@ -340,6 +400,7 @@ class ClosedLoop:
             Ss = torch.empty((K, B), dtype=torch.int32, device=self.dev)
             Si = torch.empty((K, B), dtype=torch.int32, device=self.dev)
             Sc = torch.empty((K, B), dtype=torch.int32, device=self.dev)
+            Sa = torch.empty((K, B), dtype=torch.int32, device=self.dev)
             S[0].copy_(self.state)
         nz = None if noise is None else _dev(noise, self.dev)
         for j, k in enumerate(ks):
@@ -351,9 +412,19 @@ class ClosedLoop:
                     Ss[j].copy_(self.st)
                     Si[j].copy_(self.it)
                     Sc[j].copy_(self.flag)
+                    Sa[j].copy_(self.active)
         torch.cuda.synchronize(self.dev)
+        pol = self._policy_logs()
         if not record:
-            return {"k": np.array(ks), "state": self.state.cpu().numpy()}
-        return {"k": np.array(ks), "states": S.cpu().numpy(), "controls": Ua.cpu().numpy(),
-                "status": Ss.cpu().numpy(), "iters": Si.cpu().numpy(), "collide": Sc.cpu().numpy().astype(bool),
-                "success": Ss.cpu().numpy() <= TT_ACCEPTABLE}
+            return dict(pol, k=np.array(ks), state=self.state.cpu().numpy())
+        act = Sa.cpu().numpy()
+        stop = np.where((act == 0).any(axis=0), (act == 0).argmax(axis=0), -1)
+        return dict(pol, k=np.array(ks), states=S.cpu().numpy(), controls=Ua.cpu().numpy(), status=Ss.cpu().numpy(),
+                    iters=Si.cpu().numpy(), collide=Sc.cpu().numpy().astype(bool),
+                    success=Ss.cpu().numpy() <= TT_ACCEPTABLE, active=act.astype(bool), stop_step=stop)
+
+    def _policy_logs(self):
+        """failure_count / consecutive_failures of the reference drivers, per instance, and whether the
+        instance is still running (False = stopped by the policy)."""
+        return {"failures": self.fails.cpu().numpy(), "consecutive_failures": self.consec.cpu().numpy(),
+                "running": self.active.cpu().numpy().astype(bool)}

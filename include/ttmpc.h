@@ -155,6 +155,22 @@ int tt_collision_device(int B, int K, const double* poses, long long stride_b, i
  * u_applied [B][2] (may be NULL) receives the control before friction/slippage scaling. */
 int tt_plant_update_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
                            const int* status, int zero_on_fail, double* u_applied, void* stream);
+/* Closed-loop failure policy of the driver, fused with the plant update (one launch per step):
+ * success (status <= TT_ACCEPTABLE): u = u[b*u_stride + 0..1], u_last = u, consecutive = 0.  Failure:
+ * failures++, consecutive++, then TT_POLICY_TRACK applies u as returned (simulation.py:519-527),
+ * TT_POLICY_NMPC zero control and u_last = 0, stop after 20 consecutive (simulation_nmpc.py:206-216),
+ * TT_POLICY_FUZZY u_last, zero after 15 consecutive, stop after 30 (simulation_fuzzy.py:207-221).
+ * Stopping (the reference's `break` before update) clears active[b]; inactive instances keep their state.
+ * u_last [B][2], consecutive / failures / active [B] are device state owned by the caller (active = 1 and
+ * the rest 0 at the start); u_applied [B][2] (may be NULL) receives the applied control. */
+enum { TT_POLICY_TRACK = 0, TT_POLICY_NMPC = 1, TT_POLICY_FUZZY = 2 };
+int tt_policy_plant_device(int B, const tt_plant* p, int policy, double* state, const double* u, long long u_stride,
+                           const int* status, double* u_last, int* consecutive, int* failures, int* active,
+                           double* u_applied, void* stream);
+/* _compute_fuzzy_weights (mpc_control_fuzzy.py:90-119) per instance from the measured state x [B][6]
+ * and the window's reference xref [B][N+1][6] (speed of stage 0): wq_wr [B][8] = (q0..q5, r0, r1), the
+ * per-instance weights of a TT_VARIANT_FUZZY solve. */
+int tt_fuzzy_weights_device(int B, int N, const double* x, const double* xref, double* wq_wr, void* stream);
 /* NMPC / fuzzy warm start (mpc_control_nmpc.py:90-100): z_guess [B][8N+6] = shift(last) where have[b],
  * else the reference-copy guess from xref / uref.  bug_compatible = the reference's last-stage slicing
  * (mpc_control_nmpc.py:83-84). */

@@ -429,29 +429,80 @@ def step_indices(T_sim, dt):
     return ks
 
 
-def closed_loop(solve, x_init, plan_x, plan_u, horizon, T_sim, p, dist=None, noise=None, zero_on_fail=False):
+def closed_loop(solve, x_init, plan_x, plan_u, horizon, T_sim, p, dist=None, noise=None, zero_on_fail=False,
+                policy=None, fuzzy=False):
     """The reference loop for B instances sharing one plan (plan_x (6,Np+1), plan_u (2,Np)).
-    solve(x_meas (B,6), Xr (B,N+1,6), Ur (B,N,2)) -> (X (B,N+1,6), U (B,N,2), status (B,)).
+    solve(x_meas (B,6), Xr (B,N+1,6), Ur (B,N,2)[, w (B,8)]) -> (X (B,N+1,6), U (B,N,2), status (B,)).
     noise: (steps, B, 6) measurement noise (simulation.py:509-513) or None.
-    Returns states (steps+1,B,6), applied controls (steps,B,2), status (steps,B)."""
+    policy: what follows a failed solve (status > 1) -- "track" (simulation.py:519-527: the returned
+    inputs), "nmpc" (simulation_nmpc.py:206-216: zero control, stop after 20 consecutive failures),
+    "fuzzy" (simulation_fuzzy.py:207-221: last successful control, zero after 15, stop after 30).  A
+    stopped instance (the reference's `break`) keeps its state and applies nothing.  fuzzy=True: the solve
+    gets the per-instance fuzzy weights and failed instances are re-solved once with unit weights
+    (mpc_control_fuzzy.py:132-161).
+    Returns states (steps+1,B,6), applied controls (steps,B,2), status (steps,B), and when policy or fuzzy is
+    given also dict(failures, consecutive_failures, running)."""
+    legacy = policy is None and not fuzzy
+    if policy is None:
+        policy = "nmpc" if zero_on_fail else "track"
     x = np.array(x_init, dtype=np.float64).reshape(-1, 6)
     B = x.shape[0]
     ks = step_indices(T_sim, p["dt"])
     S, Ua, St = [x.copy()], [], []
+    u_last = np.zeros((B, 2))
+    consec = np.zeros(B, dtype=np.int64)
+    fails = np.zeros(B, dtype=np.int64)
+    active = np.ones(B, dtype=bool)
     for j, k in enumerate(ks):
         Xr, Ur = reference_window(plan_x, plan_u, k, horizon)
         Xr = np.broadcast_to(Xr.T, (B, horizon + 1, NX)).copy()
         Ur = np.broadcast_to(Ur.T, (B, horizon, NU)).copy()
         xm = x + noise[j] if noise is not None else x
-        _, U, st = solve(xm, Xr, Ur)
-        u0 = U[:, 0].copy()
-        if zero_on_fail:
-            u0[st > 1] = 0.0
-        x = plant_update(x, u0, p, dist)
+        if fuzzy:
+            w = np.stack([np.concatenate(fuzzy_weights(xm[b], Xr[b].T)) for b in range(B)])
+            X, U, st = solve(xm, Xr, Ur, w)
+            st = np.asarray(st).copy()
+            bad = np.where((st > 1) & active)[0]
+            if bad.size:
+                _, U2, st2 = solve(xm[bad], Xr[bad], Ur[bad], np.ones((bad.size, 8)))
+                U = U.copy()
+                U[bad], st[bad] = U2, st2
+        else:
+            _, U, st = solve(xm, Xr, Ur)
+            st = np.asarray(st)
+        u0 = np.zeros((B, 2))
+        for b in range(B):
+            if not active[b]:
+                continue
+            if st[b] <= 1:
+                u0[b] = U[b, 0]
+                u_last[b] = u0[b]
+                consec[b] = 0
+                continue
+            fails[b] += 1
+            consec[b] += 1
+            if policy == "nmpc":
+                u_last[b] = 0.0
+                if consec[b] > 20:
+                    active[b] = False
+            elif policy == "fuzzy":
+                u0[b] = u_last[b]
+                if consec[b] > 15:
+                    u0[b] = 0.0
+                if consec[b] > 30:
+                    active[b] = False
+                    u0[b] = 0.0
+            else:
+                u0[b] = U[b, 0]
+        xn = plant_update(x, u0, p, dist)
+        x = np.where(active[:, None], xn, x)
         S.append(x.copy())
         Ua.append(u0)
-        St.append(np.asarray(st).copy())
-    return np.array(S), np.array(Ua), np.array(St)
+        St.append(st.copy())
+    out = np.array(S), np.array(Ua), np.array(St)
+    if legacy:
+        return out
+    return out + ({"failures": fails, "consecutive_failures": consec, "running": active},)
 
 
 def lqr_riccati(p, Q, R, x_goal):

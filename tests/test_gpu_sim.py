@@ -268,3 +268,50 @@ def test_graph_replay_equals_eager_loop(plan, golden_ref, warm):
     graph = sim.ClosedLoop(mk(), S, U, P, sim.DISTURBANCE_PARAMS, **kw).run_graph(x0, T, noise=noise)
     for key in ("states", "controls", "status", "iters", "collide"):
         assert np.array_equal(eager[key], graph[key]), key
+
+
+def _oracle_solver_cfg(N, tol, acc_tol, max_iter, acc_iter):
+    """Oracle solve with the NMPC / fuzzy IPOPT options and optional per-instance weights w (B,8)."""
+    from oracle import c_oracle as co
+    from oracle import ttmpc_oracle as to
+    from ttmpc import layout
+    nlp = to.TrackingNLP(N)
+    Pp = co.make_problem(N, P, nlp.Q, nlp.R, nlp.xlb, nlp.xub, nlp.ulb, nlp.uub, tol=tol, acc_tol=acc_tol,
+                         max_iter=max_iter, acc_iter=acc_iter)
+
+    def solve(x, Xr, Ur, w=None):
+        z, st, _, _ = co.solve_batch(Pp, x, Xr, Ur, wq=None if w is None else w[:, :6], wr=None if w is None else w[:, 6:])
+        X, Uo = layout.unpack(z, N)
+        return X, Uo, st
+    return solve
+
+
+@pytest.mark.parametrize("policy, variant", [("nmpc", "NMPC"), ("fuzzy", "FUZZY")])
+def test_failure_policies_match_oracle_loop(plan, policy, variant):
+    """simulation_nmpc.py / simulation_fuzzy.py failure handling on the device (tt_policy_plant_device,
+    tt_fuzzy_weights_device + the unit-weight retry) against the oracle loop.  max_iter is cut to 3 so that
+    most solves fail and every branch runs: zero / last control, the 15-failure zero-control switch and the
+    20 / 30 consecutive-failure stop."""
+    import ttmpc
+    from oracle import ttmpc_oracle as to
+    from ttmpc import simulation as sim
+    S, U = plan
+    N, B, T = 20, 8, 2.0
+    rng = np.random.default_rng(21)
+    x0 = S[:, 0][None] + rng.normal(scale=[0.4, 0.4, 0.05, 0.05, 0.0, 0.0], size=(B, 6))
+    tol, acc, mi, ai = 1e-3, 1e-2, 3, 5
+    solver = ttmpc.BatchSolver(N, P, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB, to.MPC_UUB,
+                               variant=getattr(ttmpc, f"TT_VARIANT_{variant}"), tol=tol, acc_tol=acc, max_iter=mi,
+                               acc_iter=ai)
+    cl = sim.ClosedLoop(solver, S, U, P, None, policy=policy)
+    out = cl.run(x0, T)
+    ref_S, ref_u, ref_st, pol = to.closed_loop(_oracle_solver_cfg(N, tol, acc, mi, ai), x0, S, U, N, T, P,
+                                               policy=policy, fuzzy=variant == "FUZZY")
+    assert np.array_equal(out["status"], ref_st)
+    assert np.array_equal(out["failures"], pol["failures"])
+    assert np.array_equal(out["running"], pol["running"])
+    assert np.max(np.abs(out["controls"] - ref_u)) <= 1e-6
+    assert np.max(np.abs(out["states"] - ref_S)) <= 1e-6
+    assert out["failures"].max() > 20            # the failure branches ran
+    if policy == "nmpc":
+        assert not out["running"].all()          # some instance hit the 20-failure stop
