@@ -261,13 +261,14 @@ def main():
     traffic = None
     traffic_src = None
     csvs = [p for p in args.traffic_csv.split(",") if p]
-    if not csvs and args.config == "c2" and B == 1024 and N == 20:
-        csvs = [str(REPO / "profiles" / "r01" / "final3" / f) for f in ("fetch_counter_collection.csv",
-                                                                          "write_counter_collection.csv")]
+    prof = REPO / "profiles" / "r02" / f"track_{TRAFFIC_COMMIT}"
+    if not csvs and (args.config, B, N) in (("c2", 1024, 20), ("c3", 8192, 40)):
+        csvs = [str(prof / f"{pas}_{args.config}_counter_collection.csv") for pas in ("fetch", "write")]
     if csvs and all(Path(p).exists() for p in csvs):
         traffic = read_traffic(csvs)
         traffic_src = ", ".join(str(Path(p).relative_to(REPO)) if str(p).startswith(str(REPO)) else p for p in csvs) + \
-            " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of this bench config; HBM bytes per launch)"
+            f" (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of this bench config at commit " \
+            f"{TRAFFIC_COMMIT}; HBM bytes per launch; profiles/r02/track_{TRAFFIC_COMMIT}/SOURCE.txt)"
     out = {
         "metric": "MPC solves/sec (N=20, nx=6, nu=2; BASELINE label says nx=5, the reference model has 6 states)"
         if N == 20 else f"MPC solves/sec (N={N}, nx=6, nu=2)",
@@ -752,6 +753,11 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
     return {"value": solved / el, "unit": "solves/s", "cores": threads, "kind": "port", "host_cores_visible": ncores,
             "sample": f"{done} instances ({solved} solved) of the same {cfg} workload in {el:.1f}s, OpenMP {threads} "
                       f"threads on {ncores} visible host cores; oracle/c/tt_obca.c (same restated IPOPT)"}
+
+
+# commit whose rocprofv3 PMC passes the default C2 / C3 lines quote as roofline.traffic (the kernel has not
+# changed since; re-profile with tools/gpu_track_prof.sh after a kernel change)
+TRAFFIC_COMMIT = "06e88e9"
 
 
 def read_traffic(paths):
