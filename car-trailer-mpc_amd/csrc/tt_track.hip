@@ -967,11 +967,14 @@ __device__ __forceinline__ void phase_init(const Ctx<BM>& c) {
 template <int BM, int OCC, int NS>
 __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void track_kernel(TrackArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    // XCD-aware instance map: the dispatcher deals workgroups round-robin over the 8 XCDs (workgroup i ->
-    // XCD i % 8), so XCD x gets the contiguous instance range [x*q + min(x, r), ...) (B = 8q + r) and the
-    // 128-B lines at instance boundaries are fetched through one XCD's L2 instead of two
+    // Instance b = workgroup b.  An XCD-aware map (contiguous instance ranges per XCD, -DTT_XCD_MAP) was
+    // measured: C2 +0.7 %, C3 -6 % (1.896 -> 2.01 ms, profiles/r02/ab_xcd.txt), so the plain map ships.
+#ifdef TT_XCD_MAP
     const int wg = blockIdx.x, q8 = a.B >> 3, r8 = a.B & 7, x8 = wg & 7;
     const int b = x8 * q8 + min(x8, r8) + (wg >> 3);
+#else
+    const int b = blockIdx.x;
+#endif
     const int N = NS > 0 ? NS : a.N, S = N + 1;  // NS: horizon fixed at compile time (stage offsets fold)
     Ctx<BM> c;
     c.sm = sm;
