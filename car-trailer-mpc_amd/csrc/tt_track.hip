@@ -24,16 +24,19 @@
 //     measured and is not faster on this dependent chain).
 //
 // LDS map (doubles).  Head (fixed offsets, immediate addressing): Qw(36) Rw(4) x_init(6) lb(8)
-// ub(8) pad(2) dump(64: per-lane sink for branch-free predicated stores).  Stage k row r at sm[kHead + k*157 + r]; the odd stride keeps lane-per-stage
-// ds_read_b64 bank-conflict-free:
-//   0-5 X | 6-7 U | 8-13 Y (eq. multipliers, IPOPT sign) | 14-21 zL | 22-29 zU | 30-35 Xref
-//   36-37 Uref | 38-45 dX,dU | 46-51 Y+ | 52-60 dt*J (9 nnz) | 61-67 curvature (7 nnz)
-//   68-75 Sigma = zL/sL + zU/sU | 76-83 grad F | 84-89 c | 90-95 c(trial)/c_soc | 96-107 K
-//   108-109 k_ff | 110-112 inv(H_uu) | 113-133 P_k (upper) | 134-139 p_k | 140-147 dX,dU (soc)
-//   148-155 dB = 1/sU - 1/sL (barrier gradient = grad F + mu dB) | 156 zero pad
-// Rows reused with a second life (their first owner is dead at that point of the iteration):
-//   during the Riccati sweep  38-45 g = grad F + mu dB | 140-145 diag(Sigma) + diag(W) | 46-51 -c_{k+1}
-//   during the SOC            61-66 -c_soc_{k+1} (b^ of the SOC forward sweep)
+// ub(8) pad(2) dump(32: per-lane sink for branch-free predicated stores), filter, Riccati tiles.  Stage
+// k row r at sm[kHead + k*117 + r]; the odd stride keeps lane-per-stage ds_read_b64 bank-conflict-free:
+//   0-5 X | 6-7 U | 8-13 Y (eq. multipliers, IPOPT sign) | 14-21 zL | 22-29 zU | 30-37 dX,dU
+//   38-43 Y+ | 44-52 dt*J (9 nnz) | 53-60 grad F (+ mu dB from ric_prep on) | 61-66 c | 67-78 K
+//   79-80 k_ff | 81-101 P_k (upper) | 102-107 p_k | 108-115 dX,dU (soc) | 116 zero pad
+// The reference window (Xref, Uref) is read from HBM (L2-resident, stage-parallel phases only).  Rows with
+// a second life (their first owner is dead over that span of the iteration):
+//   linearise .. Riccati   30-36 curvature W (7 nnz)          [dX is produced by the forward sweep]
+//   linearise .. ric_prep  81-88 Sigma = zL/sL + zU/sU, 89-96 dB = 1/sU - 1/sL   [P_k: Riccati]
+//   ric_prep .. Riccati    108-113 diag(Sigma) + diag(W), 114-115 Sigma_u      [dX_soc: SOC]
+//                          38-43 b^ = -c_{k+1}                                  [Y+: step]
+//   trial .. SOC forward   108-113 c(trial) / c_soc                             [dX_soc: SOC forward]
+// 117 rows keep four N = 40 instances (40.4 KB each) on one CU (C3).
 //
 // Bound pattern: template parameter BM (bit v = finite lower bound on variable v, bit 8+v = finite
 // upper bound; v = 0..5 states, 6..7 inputs) so the common patterns compile to straight-line code;
@@ -57,13 +60,12 @@ static_assert(hFTH + kTrackFilter == hFPH && hFPH + kTrackFilter <= 128, "filter
 static_assert(HEAD >= SR, "stage -1 of the Riccati prefetch addresses head words");
 // (128..255: the P and transposed-PA tiles of the Riccati sweep, see phase_riccati)
 // rows
-constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rXR = 30, rUR = 36, rDX = 38, rYP = 46, rAJ = 52, rWC = 61;
-constexpr int rSG = 68, rGF = 76, rCC = 84, rCT = 90, rK = 96, rKF = 108, rIH = 110, rPS = 113, rPV = 134;
-constexpr int rDXS = 140, rDB = 148, PAD = 156;
-// Riccati operand rows, written by phase_ric_prep into rows that are dead during the backward sweep
-// (dX, dX_soc and Y+ are all produced after it): g = grad F + mu dB (8), diag(Sigma) + diag(W) (6),
-// b^ = -c_{k+1} stored at stage k (6).
-constexpr int rHG = rDX, rHD = rDXS, rBH = rYP;
+constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rDX = 30, rYP = 38, rAJ = 44, rGF = 53, rCC = 61, rK = 67;
+constexpr int rKF = 79, rPS = 81, rPV = 102, rDXS = 108, PAD = 116;
+static_assert(PAD + 1 == kRowsPerStage, "stage record");
+// second lives (see the LDS map): curvature, Sigma, dB from the linearisation to the Riccati sweep; the
+// Riccati operands diag(Sigma) + diag(W), Sigma_u and b^ = -c_{k+1} (stage k); the trial residual c
+constexpr int rWC = rDX, rSG = rPS, rDB = rPS + 8, rHD = rDXS, rSGU = rDXS + 6, rBH = rYP, rCT = rDXS;
 
 // ---- wave reductions: DPP inside each 16-lane row (xor 1, xor 2, half-mirror, mirror), then the four
 // row results by v_readlane into SGPRs.  No LDS; the result is wave-uniform and bitwise identical in
@@ -204,7 +206,13 @@ struct Ctx {
     __device__ __forceinline__ double lb(int v) const { return sm[hLB + v]; }
     __device__ __forceinline__ double ub(int v) const { return sm[hUB + v]; }
     // barrier gradient component: grad F + mu * (1/sU - 1/sL)
-    __device__ __forceinline__ double gr(int v, int k) const { return r(rGF + v, k) + mu * r(rDB + v, k); }
+    // barrier gradient grad F + mu dB: folded into the rGF rows by phase_ric_prep (valid from there on)
+    __device__ __forceinline__ double gr(int v, int k) const { return r(rGF + v, k); }
+    // the instance's reference window in HBM: Xref [N+1][6], Uref [N][2]
+    const double* gxr;
+    const double* gur;
+    __device__ __forceinline__ double xr(int i, int k) const { return gxr[k * 6 + i]; }
+    __device__ __forceinline__ double ur(int i, int k) const { return gur[k * 2 + i]; }
 };
 
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
@@ -305,9 +313,9 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
         // tracking cost and its gradient (no 1/2: F = dx' Qw dx + du' Rw du, grad = 2 Qw dx)
         double dxr[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.r(rXR + i, k);
+        for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.xr(i, k);
         double du0 = 0.0, du1 = 0.0;
-        if (k < N) { du0 = u[0] - c.r(rUR, k); du1 = u[1] - c.r(rUR + 1, k); }
+        if (k < N) { du0 = u[0] - c.ur(0, k); du1 = u[1] - c.ur(1, k); }
         LogSum ls;
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
@@ -429,18 +437,26 @@ template <int BM>
 __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
     const int N = c.N;
     for (int k = c.lane; k <= N; k += W) {
+        double g[8], hd[6], su0 = 0.0, su1 = 0.0;   // read every source row before the first overlay write
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == N) break;
-            c.r(rHG + v, k) = c.gr(v, k);
-        }
+        for (int v = 0; v < 8; ++v) g[v] = (v >= 6 && k == N) ? 0.0 : c.r(rGF + v, k) + c.mu * c.r(rDB + v, k);
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const int wi = w_idx(i, i);
             double d = c.r(rSG + i, k);
             if (wi >= 0 && k < N) d += c.r(rWC + wi, k);
-            c.r(rHD + i, k) = d;
+            hd[i] = d;
         }
+        if (k < N) { su0 = c.r(rSG + 6, k); su1 = c.r(rSG + 7, k); }
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            if (v >= 6 && k == N) break;
+            c.r(rGF + v, k) = g[v];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c.r(rHD + i, k) = hd[i];
+        c.r(rSGU, k) = su0;
+        c.r(rSGU + 1, k) = su1;
         if (k < N) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) c.r(rBH + i, k) = -c.r(rCC + i, k + 1);
@@ -469,14 +485,14 @@ struct EpMap {
         }
         const int gi = (i < 6 && j == 6) ? i : (i == 6 && j < 6) ? j : -1;
         hs = (i == j && i < 6) ? rHD + i : (i < 6 && j < 6 && w_idx(i, j) >= 0) ? rWC + w_idx(i, j)
-           : gi >= 0 ? rHG + gi : PAD;
+           : gi >= 0 ? rGF + gi : PAD;
         q2 = (i < 6 && j < 6) ? 2.0 * QW[i * 6 + j] : 0.0;
         dg = (i == j && i < 6) ? 1.0 : 0.0;
         ps = (i <= j && j < 6) ? rPS + sym_idx(i, j) : (i < 6 && j == 6) ? rPV + i : -1;
-        gj0 = j == 6 ? rHG + 6 : PAD;
-        gj1 = j == 6 ? rHG + 7 : PAD;
-        gi0 = i == 6 ? rHG + 6 : PAD;
-        gi1 = i == 6 ? rHG + 7 : PAD;
+        gj0 = j == 6 ? rGF + 6 : PAD;
+        gj1 = j == 6 ? rGF + 7 : PAD;
+        gi0 = i == 6 ? rGF + 6 : PAD;
+        gi1 = i == 6 ? rGF + 7 : PAD;
     }
 };
 
@@ -493,8 +509,8 @@ __device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k,
         o.di[t] = c.r(m.di[t], k);
     }
     o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
-    o.sgu0 = c.r(rSG + 6, k);
-    o.sgu1 = c.r(rSG + 7, k);
+    o.sgu0 = c.r(rSGU, k);
+    o.sgu1 = c.r(rSGU + 1, k);
     o.gj0 = c.r(m.gj0, k);
     o.gj1 = c.r(m.gj1, k);
     o.gi0 = c.r(m.gi0, k);
@@ -526,10 +542,10 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     // The stage's factorisation rows leave in ONE unmasked ds_write per lane (three predicated stores
     // cost ~100 cycles per stage, tools/ubench_riccati.hip): P^ entries from the lanes that own them
     // (upper triangle and the p column), K^ rows from the affine/pad rows i = 6, 7 (m0, m1 depend on j
-    // only), H_uu^-1 from (6, 7), (7, 7); every other lane rewrites the uniform i11 into its slot.
+    // only); every other lane writes into the last dX row, which the forward sweep overwrites.
     const bool own_p = m.ps >= 0;
-    const bool spare = i < 6 && !own_p;
-    const int st_row = own_p ? m.ps : spare ? rIH + 2 : j < 6 ? rK + 6 * (i - 6) + j : j == 6 ? rKF + (i - 6) : rIH + (i - 6);
+    const bool k_row = i >= 6 && j < 7;
+    const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
     // one stage; `o` = this stage's operands, `nx` receives stage kn's (prefetch, issued after the
     // P-tile reads so that waiting for the tile never waits for the prefetch)
     auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
@@ -571,7 +587,7 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         PF[c.lane] = Pij;
         asm volatile("" ::: "memory");
         // factorisation rows for the forward sweep, the step and the SOC
-        c.r(st_row, k) = own_p ? Pij : spare ? i11 : j < 7 ? (i == 6 ? -m0 : -m1) : (i == 6 ? i00 : i01);
+        c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
     };
     // two stages per trip with ping-pong operand buffers (no register copies between stages)
     EpOps oa = ep_ops(c, m, N - 1, dw), ob;
@@ -608,24 +624,28 @@ __device__ __forceinline__ double bperm_d(double v, int src_lane) {
 
 // NS > 0: the horizon is a compile-time constant and the sweep is fully unrolled, so every stage's LDS
 // offsets fold into the ds_read/ds_write immediates (no per-stage address arithmetic)
-template <int BM, int NS>
+template <int BM, int NS, bool BHN = false>
 __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bhrow, int orow) {
     const int N = c.N, g = c.lane >> 3, mm = c.lane & 7;
     // output row of this lane's group: 0..5 = dx_{k+1}[g], 6/7 = du0/du1 (rows 7/8 of [Phi; K^])
     const int u = (g == 5 || g == 6) ? 0 : (g == 4 || g == 7) ? 1 : -1;
     const double fone = (g < 6 && mm == g) ? 1.0 : 0.0;
-    const int fas = (g < 6 && mm < 6 && d_idx(g, mm) >= 0) ? rAJ + d_idx(g, mm) : (g < 6 && mm == 6) ? bhrow + g : PAD;
+    // BHN: b^_k = -c_{k+1} read straight from the residual rows of stage k+1 (row SR + crow + g of stage k)
+    // instead of a stored b^ row (the SOC sweep: c_soc lives where its own output dX_soc goes)
+    const int fas = (g < 6 && mm < 6 && d_idx(g, mm) >= 0) ? rAJ + d_idx(g, mm)
+                  : (g < 6 && mm == 6) ? (BHN ? SR + crow + g : bhrow + g) : PAD;
+    const double fsg = (BHN && g < 6 && mm == 6) ? -1.0 : 1.0;
     const int fk = (u >= 0 && mm < 6) ? rK + 6 * u + mm : (u >= 0 && mm == 6) ? rKF + u : PAD;
     const double fkc = u >= 0 ? (g < 6 ? c.dt : 1.0) : 0.0;
     // x^_0[m] = -c_0[m] (m < 6), 1 (m = 6), 0 (m = 7)
     double x = mm < 6 ? -c.r(crow + mm, 0) : (mm == 6 ? 1.0 : 0.0);
     if (c.lane < 6) c.r(orow + c.lane, 0) = -c.r(crow + c.lane, 0);
     const int src = 8 * (mm < 6 ? mm : 0);  // group holding x_{k+1}[mm]
-    double nph = fone + c.r(fas, 0) + fkc * c.r(fk, 0);
+    double nph = fone + fsg * c.r(fas, 0) + fkc * c.r(fk, 0);
     auto step = [&](int k) {
         const double ph = nph;
         const int kn = k + 1 < N ? k + 1 : k;
-        nph = fone + c.r(fas, kn) + fkc * c.r(fk, kn);
+        nph = fone + fsg * c.r(fas, kn) + fkc * c.r(fk, kn);
         double y = ph * x;
         y += dppd<0xB1>(y);   // quad_perm [1,0,3,2]
         y += dppd<0x4E>(y);   // quad_perm [2,3,0,1]
@@ -652,10 +672,11 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bh
 
 // ============ SOC: backward vector pass with the stored factorisation, rhs c_soc in rCT ============
 template <int BM>
-__device__ __forceinline__ void phase_soc_backward(const Ctx<BM>& c) {
+__device__ __forceinline__ void phase_soc_backward(const Ctx<BM>& c, double dw) {
     if (c.lane == 0) {
         const int N = c.N;
-        const double dt = c.dt;
+        const double dt = c.dt, dt2 = dt * dt;
+        const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
         double p[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) p[i] = c.gr(i, N);
@@ -673,7 +694,11 @@ __device__ __forceinline__ void phase_soc_backward(const Ctx<BM>& c) {
                 w[rr] = s;
             }
             const double h0 = c.gr(6, k) + dt * w[5], h1 = c.gr(7, k) + dt * w[4];
-            const double i00 = c.r(rIH, k), i01 = c.r(rIH + 1, k), i11 = c.r(rIH + 2, k);
+            // H_uu^-1 of the Riccati stage (R~ + Sigma_u + dw + dt^2 P_{k+1}[{5,4}]), recomputed
+            const double h00 = r00 + c.r(rSGU, k) + dw + dt2 * c.r(rPS + sym_idx(5, 5), k + 1);
+            const double h01 = r01 + dt2 * c.r(rPS + sym_idx(4, 5), k + 1);
+            const double h11 = r11 + c.r(rSGU + 1, k) + dw + dt2 * c.r(rPS + sym_idx(4, 4), k + 1);
+            const double id = frcp(h00 * h11 - h01 * h01), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
             c.r(rKF, k) = -(i00 * h0 + i01 * h1);
             c.r(rKF + 1, k) = -(i01 * h0 + i11 * h1);
 #pragma unroll
@@ -757,7 +782,7 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
         }
         double dxr[6], cost = 0.0, th = 0.0;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.r(rXR + i, k);
+        for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.xr(i, k);
         if constexpr (Ctx<BM>::kDiag) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) cost += dxr[i] * (c.h(hQW + i * 7) * dxr[i]);
@@ -771,7 +796,7 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
             }
         }
         if (k < N) {
-            const double e0 = u[0] - c.r(rUR, k), e1 = u[1] - c.r(rUR + 1, k);
+            const double e0 = u[0] - c.ur(0, k), e1 = u[1] - c.ur(1, k);
             if constexpr (Ctx<BM>::kDiag)
                 cost += e0 * (c.h(hRW) * e0) + e1 * (c.h(hRW + 3) * e1);
             else
@@ -869,7 +894,6 @@ __device__ __forceinline__ void phase_soc_rhs(const Ctx<BM>& c, double alpha) {
         for (int i = 0; i < 6; ++i) {
             const double cs = alpha * c.r(rCC + i, k) + c.r(rCT + i, k);
             c.r(rCT + i, k) = cs;
-            if (k > 0) c.r(rWC + i, k - 1) = -cs;  // b^ of the SOC forward sweep (rWC is dead after Riccati)
         }
     }
     __syncthreads();
@@ -893,7 +917,7 @@ __device__ __forceinline__ double phase_soc_alpha(const Ctx<BM>& c) {
 // ---------------- load one instance into LDS (coalesced flat copies) ----------------
 template <int BM>
 __device__ __forceinline__ void phase_load(const Ctx<BM>& c, const TrackArgs& a, int b) {
-    const int lane = c.lane, N = c.N, S = N + 1, n = 8 * N + 6;
+    const int lane = c.lane, N = c.N, n = 8 * N + 6;
     if (lane < 8) {  // relaxed bounds (bound_relax_factor 1e-8), -inf/+inf = free
         const int v = lane;
         const double l = v < 6 ? a.xlb[v] : a.ulb[v - 6];
@@ -914,10 +938,6 @@ __device__ __forceinline__ void phase_load(const Ctx<BM>& c, const TrackArgs& a,
     } else if (lane < 46) {
         c.h(hXI + lane - 40) = a.x0[(size_t)b * 6 + (lane - 40)];
     }
-    const double* xr = a.xref + (size_t)b * S * 6;
-    for (int t = lane; t < S * 6; t += W) c.r(rXR + t % 6, t / 6) = xr[t];
-    const double* ur = a.uref + (size_t)b * N * 2;
-    for (int t = lane; t < N * 2; t += W) c.r(rUR + t % 2, t / 2) = ur[t];
     if (a.zg) {
         const double* zg = a.zg + (size_t)b * n;
         for (int t = lane; t < n; t += W) c.r(t % 8, t / 8) = zg[t];
@@ -928,7 +948,7 @@ __device__ __forceinline__ void phase_load(const Ctx<BM>& c, const TrackArgs& a,
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 if (v >= 6 && k == N) break;
-                c.r(rX + v, k) = c.r(rXR + v, k);
+                c.r(rX + v, k) = v < 6 ? c.xr(v, k) : c.ur(v - 6, k);
             }
     }
     __syncthreads();
@@ -978,6 +998,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
     const int N = NS > 0 ? NS : a.N, S = N + 1;  // NS: horizon fixed at compile time (stage offsets fold)
     Ctx<BM> c;
     c.sm = sm;
+    c.gxr = a.xref + (size_t)b * S * 6;
+    c.gur = a.uref + (size_t)b * N * 2;
     c.N = N;
     c.lane = threadIdx.x;
     c.dt = a.dt;
@@ -1082,8 +1104,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
                 if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, pD, pT, ftype)) { accepted = 1; break; }
                 if (ls == 0 && isfinite(t.phi) && t.th >= th0) {
                     phase_soc_rhs(c, alpha);
-                    phase_soc_backward(c);
-                    phase_forward<BM, NS>(c, rCT, rWC, rDXS);
+                    phase_soc_backward(c, dw);
+                    phase_forward<BM, NS, true>(c, rCT, 0, rDXS);
                     const double as = phase_soc_alpha(c);
                     const Trial ts = phase_trial(c, as, rDXS, false);
                     STAMP(PH_SOC);
@@ -1173,8 +1195,8 @@ bool diagonal_weights(const TrackArgs& a) {
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     const int m = bound_mask(a);
     const bool d = diagonal_weights(a);
-    // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 23); at N = 40 the
-    // 52 KB per wave caps a CU at 3 and the occupancy build's spills are pure cost (C3 2.01 -> 2.14 ms).
+    // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 31 with the 117-double
+    // stage record); at N = 40 four waves share a CU and the occupancy build's spills would be pure cost.
     const bool occ_room = 5 * lds_bytes(a.N) <= kMaxLdsBytes;
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     // the BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds

@@ -222,11 +222,11 @@ def test_reference_call_surface():
 
 
 def test_max_horizon_matches_oracle():
-    """The largest horizon whose instance fits one CU's LDS (tt_max_horizon: 127 doubles-stage records)."""
+    """The largest horizon whose instance fits one CU's LDS (tt_max_horizon: 117-double stage records)."""
     import ttmpc
     from ttmpc.scenarios import synthetic_batch
     N = ttmpc.lib().tt_max_horizon()
-    assert N >= 120
+    assert N >= 170
     x0, xr, ur = synthetic_batch(32, N, seed=77)
     X, U, st, it, kk = _gpu_solver(N).solve(x0, xr, ur)
     zc, stc, itc, kkc = _oracle(N, x0, xr, ur)
@@ -300,7 +300,7 @@ def test_c5_full_batch_through_the_sharded_path():
 
 
 def test_occupancy_build_is_bitwise_the_latency_build():
-    """Large batches (B > 4096, reference box, diagonal weights, N <= 23) launch the two-waves-per-SIMD
+    """Large batches (B > 4096, reference box, diagonal weights, N <= 31) launch the two-waves-per-SIMD
     build of track_kernel; small N = 20 batches launch the stage-unrolled NS = 20 build.  Two different
     builds of the same arithmetic: every instance must come out bit-identical in both."""
     from ttmpc.scenarios import synthetic_batch
@@ -314,13 +314,13 @@ def test_occupancy_build_is_bitwise_the_latency_build():
             assert np.array_equal(a[lo:lo + 1152], b)
 
 
-def test_occupancy_build_boundary_n23_n24():
-    """launch_track's occupancy switch: B = 4097 at N = 23 still fits 5 waves' LDS per CU (two-waves build),
-    at N = 24 it does not (one-wave build).  Both must equal the same instances solved in small batches
+def test_occupancy_build_boundary_n31_n32():
+    """launch_track's occupancy switch: B = 4097 at N = 31 still fits 5 waves' LDS per CU (two-waves build),
+    at N = 32 it does not (one-wave build).  Both must equal the same instances solved in small batches
     (one-wave build)."""
     from ttmpc.scenarios import synthetic_batch
     B = 4097
-    for N in (23, 24):
+    for N in (31, 32):
         x0, xr, ur = synthetic_batch(B, N, seed=5 + N)
         s = _gpu_solver(N)
         big = s.solve(x0, xr, ur)
