@@ -208,20 +208,35 @@ struct Ctx {
     // barrier gradient component: grad F + mu * (1/sU - 1/sL)
     // barrier gradient grad F + mu dB: folded into the rGF rows by phase_ric_prep (valid from there on)
     __device__ __forceinline__ double gr(int v, int k) const { return r(rGF + v, k); }
-    // the instance's reference window in HBM: Xref [N+1][6], Uref [N][2]
+    // the instance's reference window in HBM: Xref [N+1][6], Uref [N][2].  regref: one stage per lane
+    // (stage-unrolled builds, N < 64), so lane k keeps its stage's 8 reference values in registers for the
+    // whole solve (the stage-parallel phases only ever ask for k = lane); else every read goes to HBM / L2.
     const double* gxr;
     const double* gur;
-    __device__ __forceinline__ double xr(int i, int k) const { return gxr[k * 6 + i]; }
-    __device__ __forceinline__ double ur(int i, int k) const { return gur[k * 2 + i]; }
+    bool regref;
+    double rc0, rc1, rc2, rc3, rc4, rc5, rc6, rc7;  // scalars (an array member would live in scratch)
+    __device__ __forceinline__ double rcv(int i) const {
+        return i == 0 ? rc0 : i == 1 ? rc1 : i == 2 ? rc2 : i == 3 ? rc3 : i == 4 ? rc4 : i == 5 ? rc5 : i == 6 ? rc6 : rc7;
+    }
+    __device__ __forceinline__ double xr(int i, int k) const { return regref ? rcv(i) : gxr[k * 6 + i]; }
+    __device__ __forceinline__ double ur(int i, int k) const { return regref ? rcv(6 + i) : gur[k * 2 + i]; }
+    // Trig cache (regref builds): the trial point's sin/cos of theta, psi, phi, kept by the lane of its stage.
+    // The accepted step lands exactly on the last trial point (update computes x + alpha dz with the same
+    // expression), so the next linearisation reuses them instead of three more FP64 sincos.
+    mutable double ts0, tc0, ts1, tc1, ts2, tc2;
+    mutable double t_alpha;
+    mutable int t_dz, t_ok;
 };
 
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
 template <int BM>
 __device__ __forceinline__ void model_f(const Ctx<BM>& c, const double* x, const double* u, double* fo) {
-    double sth, cth, sps, cps;
+    double sth, cth, sps, cps, sph, cph;
     sincos(x[2], &sth, &cth);
     sincos(x[3], &sps, &cps);
-    const double t = tan(x[4]), v = x[5];
+    sincos(x[4], &sph, &cph);
+    if (c.regref) { c.ts0 = sth; c.tc0 = cth; c.ts1 = sps; c.tc1 = cps; c.ts2 = sph; c.tc2 = cph; }
+    const double t = sph * frcp(cph), v = x[5];
     fo[0] = v * cth;
     fo[1] = v * sth;
     fo[2] = v * t * c.iL1;
@@ -235,9 +250,13 @@ template <int BM>
 __device__ __forceinline__ void model_lin(const Ctx<BM>& c, const double* x, const double* u, const double* y,
                                           double* fo, double* aj, double* wc) {
     double sth, cth, sps, cps, sph, cph;
-    sincos(x[2], &sth, &cth);
-    sincos(x[3], &sps, &cps);
-    sincos(x[4], &sph, &cph);
+    if (c.t_ok) {
+        sth = c.ts0; cth = c.tc0; sps = c.ts1; cps = c.tc1; sph = c.ts2; cph = c.tc2;
+    } else {
+        sincos(x[2], &sth, &cth);
+        sincos(x[3], &sps, &cps);
+        sincos(x[4], &sph, &cph);
+    }
     const double v = x[5], dt = c.dt, Mh = c.Mh, iL1 = c.iL1, iL2 = c.iL2, iL1L2 = iL1 * iL2;
     const double ic = frcp(cph), t = sph * ic, c2 = ic * ic;
     const double k = 1.0 + Mh * iL2 * cps;
@@ -770,6 +789,8 @@ struct Trial {
 template <int BM>
 __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int dzr, bool storeC) {
     const int N = c.N;
+    c.t_alpha = alpha;
+    c.t_dz = dzr;
     double val = 0.0, thl = 0.0;
     bool bad = false;
     for (int k = c.lane; k <= N; k += W) {
@@ -1000,6 +1021,18 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
     c.sm = sm;
     c.gxr = a.xref + (size_t)b * S * 6;
     c.gur = a.uref + (size_t)b * N * 2;
+    c.regref = NS > 0 && NS < W;
+    c.rc0 = c.rc1 = c.rc2 = c.rc3 = c.rc4 = c.rc5 = c.rc6 = c.rc7 = 0.0;
+    c.ts0 = c.tc0 = c.ts1 = c.tc1 = c.ts2 = c.tc2 = 0.0;
+    c.t_alpha = 0.0;
+    c.t_dz = -1;
+    c.t_ok = 0;
+    if (NS > 0 && NS < W) {
+        const int k = min((int)threadIdx.x, N), ku = min(k, N - 1);
+        c.rc0 = c.gxr[k * 6 + 0]; c.rc1 = c.gxr[k * 6 + 1]; c.rc2 = c.gxr[k * 6 + 2];
+        c.rc3 = c.gxr[k * 6 + 3]; c.rc4 = c.gxr[k * 6 + 4]; c.rc5 = c.gxr[k * 6 + 5];
+        c.rc6 = c.gur[ku * 2 + 0]; c.rc7 = c.gur[ku * 2 + 1];
+    }
     c.N = N;
     c.lane = threadIdx.x;
     c.dt = a.dt;
@@ -1095,6 +1128,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             amin *= 0.05;
             double alpha = si.ap, az = si.az;
             int accepted = si.rel < 1e-15 ? 1 : 0;
+            c.t_dz = -1;  // no trial point of this iteration yet (a tiny step is taken without one)
             const bool tiny = accepted;
             bool soc = false, ftype = false;
             for (int ls = 0; !accepted; ++ls) {
@@ -1131,6 +1165,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
                 __syncthreads();
             }
             phase_update(c, soc ? rDXS : rDX, alpha, az);
+            // the next linearisation point is the last trial point: reuse its trig (wave-uniform test)
+            c.t_ok = c.regref && alpha == c.t_alpha && (soc ? rDXS : rDX) == c.t_dz;
             STAMP(PH_UPDATE);
         }
     }
