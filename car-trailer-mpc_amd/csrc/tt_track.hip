@@ -134,6 +134,14 @@ __device__ __forceinline__ double frcp(double x) {
     return fma(r, e, r);
 }
 
+// b if p else a, for two elements of a register array: the empty asm makes both operands opaque values, so
+// the compiler cannot turn the select of two array loads into one load at a lane-dependent address (which
+// would send the whole array to scratch)
+__device__ __forceinline__ double psel(bool p, double a, double b) {
+    asm("" : "+v"(a), "+v"(b));
+    return p ? b : a;
+}
+
 // sum of logs as log(prod of mantissas) + (sum of exponents) ln 2: one log per stage instead of 16
 struct LogSum {
     double m = 1.0;
@@ -206,6 +214,14 @@ struct Ctx {
     __device__ __forceinline__ double lb(int v) const { return sm[hLB + v]; }
     __device__ __forceinline__ double ub(int v) const { return sm[hUB + v]; }
     // barrier gradient component: grad F + mu * (1/sU - 1/sL)
+    // Lane pairs (stage-unrolled builds, N < 32, bound pattern symmetric in variable pairs (2t, 2t+1)):
+    // stage k is owned by lanes 2k and 2k+1, which split its per-variable work (variables 2t + part) and its
+    // six dynamics / multiplier rows (2q + part), halving the dependent chain of the stage-parallel phases.
+    static constexpr bool kPairSym = BM >= 0 && (((BM ^ (BM >> 1)) & 0x5555) == 0);
+    bool pair;
+    __device__ __forceinline__ int k0() const { return pair ? (lane >> 1) : lane; }
+    __device__ __forceinline__ int kst() const { return pair ? (W >> 1) : W; }
+    __device__ __forceinline__ int part() const { return pair ? (lane & 1) : 0; }
     // barrier gradient grad F + mu dB: folded into the rGF rows by phase_ric_prep (valid from there on)
     __device__ __forceinline__ double gr(int v, int k) const { return r(rGF + v, k); }
     // the instance's reference window in HBM: Xref [N+1][6], Uref [N][2].  regref: one stage per lane
@@ -228,13 +244,32 @@ struct Ctx {
     mutable int t_dz, t_ok;
 };
 
+// sin / cos of theta, psi, phi of a stage.  Lane pairs: the two lanes evaluate theta (part 0) and phi
+// (part 1) in the same instruction stream and swap the results with one DPP quad_perm [1,0,3,2], so the
+// stage pays two sincos of latency instead of three.
+template <int BM>
+__device__ __forceinline__ void stage_trig(const Ctx<BM>& c, const double* x, double& sth, double& cth, double& sps,
+                                           double& cps, double& sph, double& cph) {
+    if (c.pair) {
+        const bool p = c.part() != 0;
+        double s1, c1;
+        sincos(psel(p, x[2], x[4]), &s1, &c1);
+        sincos(x[3], &sps, &cps);
+        const double os = dppd<0xB1>(s1), oc = dppd<0xB1>(c1);
+        sth = p ? os : s1; cth = p ? oc : c1;
+        sph = p ? s1 : os; cph = p ? c1 : oc;
+    } else {
+        sincos(x[2], &sth, &cth);
+        sincos(x[3], &sps, &cps);
+        sincos(x[4], &sph, &cph);
+    }
+}
+
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
 template <int BM>
 __device__ __forceinline__ void model_f(const Ctx<BM>& c, const double* x, const double* u, double* fo) {
     double sth, cth, sps, cps, sph, cph;
-    sincos(x[2], &sth, &cth);
-    sincos(x[3], &sps, &cps);
-    sincos(x[4], &sph, &cph);
+    stage_trig(c, x, sth, cth, sps, cps, sph, cph);
     if (c.regref) { c.ts0 = sth; c.tc0 = cth; c.ts1 = sps; c.tc1 = cps; c.ts2 = sph; c.tc2 = cph; }
     const double t = sph * frcp(cph), v = x[5];
     fo[0] = v * cth;
@@ -253,9 +288,7 @@ __device__ __forceinline__ void model_lin(const Ctx<BM>& c, const double* x, con
     if (c.t_ok) {
         sth = c.ts0; cth = c.tc0; sps = c.ts1; cps = c.tc1; sph = c.ts2; cph = c.tc2;
     } else {
-        sincos(x[2], &sth, &cth);
-        sincos(x[3], &sps, &cps);
-        sincos(x[4], &sph, &cph);
+        stage_trig(c, x, sth, cth, sps, cps, sph, cph);
     }
     const double v = x[5], dt = c.dt, Mh = c.Mh, iL1 = c.iL1, iL2 = c.iL2, iL1L2 = iL1 * iL2;
     const double ic = frcp(cph), t = sph * ic, c2 = ic * ic;
@@ -297,6 +330,104 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
     const int N = c.N;
     double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0, cost = 0.0, th = 0.0, logs = 0.0;
     bool fin = true, bad = false;
+    if (c.pair) {
+        // lane pairs: both lanes linearise the dynamics (the curvature and dt*J feed both lanes' gradient
+        // rows), each writes and accounts for its own rows (2q + part) and its own variables (2t + part)
+        const int p = c.part();
+        for (int k = c.k0(); k <= N; k += c.kst()) {
+            double x[6], u[2] = {0.0, 0.0}, yk[6], y1[6] = {0, 0, 0, 0, 0, 0}, aj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { x[i] = c.r(rX + i, k); yk[i] = c.r(rY + i, k); }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) sy += fabs(psel(p, yk[2 * q], yk[2 * q + 1]));
+            if (k == 0) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int i = 2 * q + p;
+                    const double cc = psel(p, x[2 * q], x[2 * q + 1]) - c.h(hXI + i);
+                    c.r(rCC + i, 0) = cc;
+                    pinf = fmax(pinf, fabs(cc));
+                    th += fabs(cc);
+                }
+            }
+            if (k < N) {
+                double fo[6], wc[7];
+                u[0] = c.r(rX + 6, k);
+                u[1] = c.r(rX + 7, k);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) y1[i] = c.r(rY + i, k + 1);
+                model_lin(c, x, u, y1, fo, aj, wc);
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    if (q == 4 && p) break;
+                    c.r(rAJ + 2 * q + p, k) = psel(p, aj[2 * q], aj[2 * q + 1]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q == 3 && p) break;
+                    c.r(rWC + 2 * q + p, k) = psel(p, wc[2 * q], wc[2 * q + 1]);
+                }
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int i = 2 * q + p;
+                    const double cc = c.r(rX + i, k + 1) - (psel(p, x[2 * q], x[2 * q + 1]) + c.dt * psel(p, fo[2 * q], fo[2 * q + 1]));
+                    c.r(rCC + i, k + 1) = cc;
+                    pinf = fmax(pinf, fabs(cc));
+                    th += fabs(cc);
+                }
+            }
+            LogSum ls;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int vb = 2 * t, v = vb + p;
+                if (vb >= 6 && k == N) break;
+                double gf, g, xv;
+                if (vb < 6) {
+                    const double dxr = psel(p, x[vb], x[vb + 1]) - c.xr(v, k);
+                    gf = c.h(hQW + v * 7) * dxr;
+                    cost += dxr * gf;
+                    gf *= 2.0;
+                    g = gf + psel(p, yk[vb], yk[vb + 1]);
+                    if (k < N) g -= psel(p, y1[vb], y1[vb + 1]) + (p ? colJ(aj, vb + 1, y1, 1) : colJ(aj, vb, y1, 1));
+                    xv = psel(p, x[vb], x[vb + 1]);
+                } else {
+                    const double du = psel(p, u[0], u[1]) - c.ur(p, k);
+                    gf = c.h(hRW + p * 3) * du;
+                    cost += du * gf;
+                    gf *= 2.0;
+                    g = gf - c.dt * psel(p, y1[5], y1[4]);
+                    xv = psel(p, u[0], u[1]);
+                }
+                c.r(rGF + v, k) = gf;
+                double sg = 0.0, db = 0.0;
+                if (c.hl(vb)) {
+                    const double zl = c.r(rZL + v, k), sl = xv - c.lb(v), rs = frcp(sl);
+                    g -= zl;
+                    c0 = fmax(c0, fabs(zl * sl));
+                    cmu = fmax(cmu, fabs(zl * sl - c.mu));
+                    sz += zl;
+                    sg += zl * rs;
+                    db -= rs;
+                    if (sl <= 0.0) bad = true; else ls.add(sl);
+                }
+                if (c.hu(vb)) {
+                    const double zu = c.r(rZU + v, k), su = c.ub(v) - xv, rs = frcp(su);
+                    g += zu;
+                    c0 = fmax(c0, fabs(zu * su));
+                    cmu = fmax(cmu, fabs(zu * su - c.mu));
+                    sz += zu;
+                    sg += zu * rs;
+                    db += rs;
+                    if (su <= 0.0) bad = true; else ls.add(su);
+                }
+                c.r(rSG + v, k) = sg;
+                c.r(rDB + v, k) = db;
+                if (!isfinite(g)) fin = false;
+                dinf = fmax(dinf, fabs(g));
+            }
+            logs += ls.value();
+        }
+    } else
     for (int k = c.lane; k <= N; k += W) {
         double x[6], u[2] = {0.0, 0.0}, yk[6], y1[6] = {0, 0, 0, 0, 0, 0}, aj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -414,13 +545,16 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
 template <int BM>
 __device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
     double cm = 0.0;
-    for (int k = c.lane; k <= c.N; k += W) {
+    const int p = c.part();
+    for (int k = c.k0(); k <= c.N; k += c.kst()) {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == c.N) break;
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;   // vb carries the (pair-symmetric) bound flags
+            if (vb >= 6 && k == c.N) break;
             const double xv = c.r(rX + v, k);
-            if (c.hl(v)) cm = fmax(cm, fabs(c.r(rZL + v, k) * (xv - c.lb(v)) - c.mu));
-            if (c.hu(v)) cm = fmax(cm, fabs(c.r(rZU + v, k) * (c.ub(v) - xv) - c.mu));
+            if (c.hl(vb)) cm = fmax(cm, fabs(c.r(rZL + v, k) * (xv - c.lb(v)) - c.mu));
+            if (c.hu(vb)) cm = fmax(cm, fabs(c.r(rZU + v, k) * (c.ub(v) - xv) - c.mu));
         }
     }
     return wmax(cm);
@@ -739,29 +873,34 @@ template <int BM>
 __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool primal_pieces) {
     const int N = c.N;
     double ap = 1.0, az = 1.0, Dg = 0.0, rel = 0.0;
-    for (int k = c.lane; k <= N; k += W) {
+    const int p = c.part();
+    for (int k = c.k0(); k <= N; k += c.kst()) {
         double dx[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) dx[i] = c.r(dzr + i, k);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
+        for (int q = 0; q < 6; ++q) {
+            if (c.pair && q >= 3) break;
+            const int i = c.pair ? 2 * q + p : q;
             double s = c.r(rPV + i, k);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) s += c.r(rPS + sym_idx(i, j), k) * dx[j];
+            for (int j = 0; j < 6; ++j) s += c.r(rPS + (c.pair ? (p ? sym_idx(2 * q + 1, j) : sym_idx(2 * q, j)) : sym_idx(q, j)), k) * dx[j];
             c.r(rYP + i, k) = -s;
         }
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == N) break;
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;
+            if (vb >= 6 && k == N) break;
             const double d = c.r(dzr + v, k), xv = c.r(rX + v, k);
             Dg += c.gr(v, k) * d;
             rel = fmax(rel, fabs(d) * frcp(1.0 + fabs(xv)));  // only tested against 1e-15
-            if (c.hl(v)) {
+            if (c.hl(vb)) {
                 const double s = xv - c.lb(v), rs = frcp(s), zl = c.r(rZL + v, k);
                 ftb(s, d, c.tau, ap);
                 ftb(zl, (c.mu - zl * d) * rs - zl, c.tau, az);
             }
-            if (c.hu(v)) {
+            if (c.hu(vb)) {
                 const double s = c.ub(v) - xv, rs = frcp(s), zu = c.r(rZU + v, k);
                 ftb(s, -d, c.tau, ap);
                 ftb(zu, (c.mu + zu * d) * rs - zu, c.tau, az);
@@ -793,7 +932,8 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
     c.t_dz = dzr;
     double val = 0.0, thl = 0.0;
     bool bad = false;
-    for (int k = c.lane; k <= N; k += W) {
+    const int p = c.part();
+    for (int k = c.k0(); k <= N; k += c.kst()) {
         double x[6], u[2] = {0.0, 0.0};
 #pragma unroll
         for (int i = 0; i < 6; ++i) x[i] = c.r(rX + i, k) + alpha * c.r(dzr + i, k);
@@ -804,7 +944,13 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
         double dxr[6], cost = 0.0, th = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.xr(i, k);
-        if constexpr (Ctx<BM>::kDiag) {
+        if (c.pair) {  // (pair mode implies diagonal weights) variables 2t + part of the stage
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const double e = psel(p, dxr[2 * t], dxr[2 * t + 1]);
+                cost += e * (c.h(hQW + (2 * t + p) * 7) * e);
+            }
+        } else if constexpr (Ctx<BM>::kDiag) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) cost += dxr[i] * (c.h(hQW + i * 7) * dxr[i]);
         } else {
@@ -818,23 +964,30 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
         }
         if (k < N) {
             const double e0 = u[0] - c.ur(0, k), e1 = u[1] - c.ur(1, k);
-            if constexpr (Ctx<BM>::kDiag)
+            if (c.pair)
+                cost += p ? e1 * (c.h(hRW + 3) * e1) : e0 * (c.h(hRW) * e0);
+            else if constexpr (Ctx<BM>::kDiag)
                 cost += e0 * (c.h(hRW) * e0) + e1 * (c.h(hRW + 3) * e1);
             else
                 cost += e0 * (c.h(hRW) * e0 + c.h(hRW + 1) * e1) + e1 * (c.h(hRW + 2) * e0 + c.h(hRW + 3) * e1);
         }
         LogSum ls;
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == N) break;
-            const double xv = v < 6 ? x[v] : u[v - 6];
-            if (c.hl(v)) { const double s = xv - c.lb(v); if (s <= 0.0) bad = true; else ls.add(s); }
-            if (c.hu(v)) { const double s = c.ub(v) - xv; if (s <= 0.0) bad = true; else ls.add(s); }
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;
+            if (vb >= 6 && k == N) break;
+            const double xv = vb < 6 ? psel(p, x[vb], x[c.pair ? vb + 1 : vb]) : psel(p, u[vb - 6], u[c.pair ? vb - 5 : vb - 6]);
+            if (c.hl(vb)) { const double s = xv - c.lb(v); if (s <= 0.0) bad = true; else ls.add(s); }
+            if (c.hu(vb)) { const double s = c.ub(v) - xv; if (s <= 0.0) bad = true; else ls.add(s); }
         }
+        const int nrow = c.pair ? 3 : 6;
         if (k == 0) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const double cc = x[i] - c.h(hXI + i);
+            for (int q = 0; q < 6; ++q) {
+                if (q >= nrow) break;
+                const int i = c.pair ? 2 * q + p : q;
+                const double cc = psel(p, x[c.pair ? 2 * q : q], x[c.pair ? 2 * q + 1 : q]) - c.h(hXI + i);
                 th += fabs(cc);
                 if (storeC) c.r(rCT + i, 0) = cc;
             }
@@ -843,9 +996,13 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
             double fo[6];
             model_f(c, x, u, fo);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
+            for (int q = 0; q < 6; ++q) {
+                if (q >= nrow) break;
+                const int i = c.pair ? 2 * q + p : q;
+                const double xi = psel(p, x[c.pair ? 2 * q : q], x[c.pair ? 2 * q + 1 : q]);
+                const double fi = psel(p, fo[c.pair ? 2 * q : q], fo[c.pair ? 2 * q + 1 : q]);
                 const double xn = c.r(rX + i, k + 1) + alpha * c.r(dzr + i, k + 1);
-                const double cc = xn - (x[i] + c.dt * fo[i]);
+                const double cc = xn - (xi + c.dt * fi);
                 th += fabs(cc);
                 if (storeC) c.r(rCT + i, k + 1) = cc;
             }
@@ -883,18 +1040,20 @@ __device__ __forceinline__ bool filter_ok(const Ctx<BM>& c, int nf, const Trial&
 // ============ accept the step (stage-parallel) ============
 template <int BM>
 __device__ __forceinline__ void phase_update(const Ctx<BM>& c, int dzr, double alpha, double az) {
-    const int N = c.N;
-    for (int k = c.lane; k <= N; k += W) {
+    const int N = c.N, p = c.part();
+    for (int k = c.k0(); k <= N; k += c.kst()) {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == N) break;
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;
+            if (vb >= 6 && k == N) break;
             const double d = c.r(dzr + v, k), xo = c.r(rX + v, k), xn = xo + alpha * d;
-            if (c.hl(v)) {
+            if (c.hl(vb)) {
                 const double zl = c.r(rZL + v, k), rs = frcp(xo - c.lb(v));
                 const double znew = zl + az * ((c.mu - zl * d) * rs - zl), rn = c.mu * frcp(xn - c.lb(v));
                 c.r(rZL + v, k) = fmax(fmin(znew, 1e10 * rn), 1e-10 * rn);  // kappa_sigma = 1e10
             }
-            if (c.hu(v)) {
+            if (c.hu(vb)) {
                 const double zu = c.r(rZU + v, k), rs = frcp(c.ub(v) - xo);
                 const double znew = zu + az * ((c.mu + zu * d) * rs - zu), rn = c.mu * frcp(c.ub(v) - xn);
                 c.r(rZU + v, k) = fmax(fmin(znew, 1e10 * rn), 1e-10 * rn);
@@ -902,7 +1061,11 @@ __device__ __forceinline__ void phase_update(const Ctx<BM>& c, int dzr, double a
             c.r(rX + v, k) = xn;
         }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) c.r(rY + i, k) += alpha * (c.r(rYP + i, k) - c.r(rY + i, k));
+        for (int q = 0; q < 6; ++q) {
+            if (c.pair && q >= 3) break;
+            const int i = c.pair ? 2 * q + p : q;
+            c.r(rY + i, k) += alpha * (c.r(rYP + i, k) - c.r(rY + i, k));
+        }
     }
     __syncthreads();
 }
@@ -923,13 +1086,16 @@ __device__ __forceinline__ void phase_soc_rhs(const Ctx<BM>& c, double alpha) {
 template <int BM>
 __device__ __forceinline__ double phase_soc_alpha(const Ctx<BM>& c) {
     double as = 1.0;
-    for (int k = c.lane; k <= c.N; k += W) {
+    const int p = c.part();
+    for (int k = c.k0(); k <= c.N; k += c.kst()) {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            if (v >= 6 && k == c.N) break;
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;
+            if (vb >= 6 && k == c.N) break;
             const double d = c.r(rDXS + v, k), xv = c.r(rX + v, k);
-            if (c.hl(v)) ftb(xv - c.lb(v), d, c.tau, as);
-            if (c.hu(v)) ftb(c.ub(v) - xv, -d, c.tau, as);
+            if (c.hl(vb)) ftb(xv - c.lb(v), d, c.tau, as);
+            if (c.hu(vb)) ftb(c.ub(v) - xv, -d, c.tau, as);
         }
     }
     return wmin(as);
@@ -969,7 +1135,7 @@ __device__ __forceinline__ void phase_load(const Ctx<BM>& c, const TrackArgs& a,
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 if (v >= 6 && k == N) break;
-                c.r(rX + v, k) = v < 6 ? c.xr(v, k) : c.ur(v - 6, k);
+                c.r(rX + v, k) = v < 6 ? c.gxr[k * 6 + v] : c.gur[k * 2 + v - 6];
             }
     }
     __syncthreads();
@@ -1019,22 +1185,23 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
     const int N = NS > 0 ? NS : a.N, S = N + 1;  // NS: horizon fixed at compile time (stage offsets fold)
     Ctx<BM> c;
     c.sm = sm;
+    c.N = N;
+    c.lane = threadIdx.x;
     c.gxr = a.xref + (size_t)b * S * 6;
     c.gur = a.uref + (size_t)b * N * 2;
     c.regref = NS > 0 && NS < W;
+    c.pair = Ctx<BM>::kPairSym && Ctx<BM>::kDiag && NS > 0 && NS < W / 2;
     c.rc0 = c.rc1 = c.rc2 = c.rc3 = c.rc4 = c.rc5 = c.rc6 = c.rc7 = 0.0;
     c.ts0 = c.tc0 = c.ts1 = c.tc1 = c.ts2 = c.tc2 = 0.0;
     c.t_alpha = 0.0;
     c.t_dz = -1;
     c.t_ok = 0;
     if (NS > 0 && NS < W) {
-        const int k = min((int)threadIdx.x, N), ku = min(k, N - 1);
+        const int k = min(c.k0(), N), ku = min(k, N - 1);
         c.rc0 = c.gxr[k * 6 + 0]; c.rc1 = c.gxr[k * 6 + 1]; c.rc2 = c.gxr[k * 6 + 2];
         c.rc3 = c.gxr[k * 6 + 3]; c.rc4 = c.gxr[k * 6 + 4]; c.rc5 = c.gxr[k * 6 + 5];
         c.rc6 = c.gur[ku * 2 + 0]; c.rc7 = c.gur[ku * 2 + 1];
     }
-    c.N = N;
-    c.lane = threadIdx.x;
     c.dt = a.dt;
     c.iL1 = 1.0 / a.L1;
     c.iL2 = 1.0 / a.L2;
