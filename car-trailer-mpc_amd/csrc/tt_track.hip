@@ -795,6 +795,11 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bh
     if (c.lane < 6) c.r(orow + c.lane, 0) = -c.r(crow + c.lane, 0);
     const int src = 8 * (mm < 6 ? mm : 0);  // group holding x_{k+1}[mm]
     double nph = fone + fsg * c.r(fas, 0) + fkc * c.r(fk, 0);
+    // unrolled builds: one unmasked store per lane and stage.  Lane 8g writes its output (dx_{k+1}[g] or
+    // du_k[g-6]); the other 56 lanes write a row that is dead here -- the Hessian diagonal (rHD, consumed
+    // by the Riccati) in the Newton sweep, the residual c (rCC, consumed by the SOC right-hand side) in
+    // the SOC sweep
+    const int fst = mm == 0 ? (g < 6 ? SR + orow + g : orow + g) : (BHN ? rCC : rHD) + (g % 6);
     auto step = [&](int k) {
         const double ph = nph;
         const int kn = k + 1 < N ? k + 1 : k;
@@ -805,8 +810,7 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bh
         y += dppd<0x141>(y);  // row_half_mirror: the 8-lane group sum, in every lane of the group
         // rows 0..5 -> dx_{k+1}; groups 6/7 -> du0/du1 at stage k
         if constexpr (NS > 0) {
-            mstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
-            mstore(c, mm == 0 && g >= 6, orow + g, k, y);
+            c.sm[HEAD + k * SR + fst] = y;
         } else {
             pstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
             pstore(c, mm == 0 && g >= 6, orow + g, k, y);
