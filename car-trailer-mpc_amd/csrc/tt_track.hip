@@ -98,6 +98,57 @@ __device__ __forceinline__ double wsum(double v) { return wred(v, OpSum()); }
 __device__ __forceinline__ double wmax(double v) { return wred(v, OpMax()); }
 __device__ __forceinline__ double wmin(double v) { return wred(v, OpMin()); }
 
+// Two or four reductions with one op at once.  The first log2(Q) butterfly stages (quad xor 1, xor 2)
+// exchange complementary halves of the value set, so from then on each lane carries a single value: row
+// rotations by 4 and 8, then the gfx950 permlane16 / permlane32 swaps across rows and wave halves finish
+// every lane.  Value q is read (v_readlane, wave-uniform) from a lane that carries it.  ~40 instructions for
+// four reductions instead of ~100 (and 32 fewer v_readlane).
+__device__ __forceinline__ void plswap16(double v, double& a, double& b) {
+    const long long w = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((int)(w & 0xffffffffll), (int)(w & 0xffffffffll), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((int)(w >> 32), (int)(w >> 32), false, false);
+    a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
+    b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
+}
+__device__ __forceinline__ void plswap32(double v, double& a, double& b) {
+    const long long w = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((int)(w & 0xffffffffll), (int)(w & 0xffffffffll), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((int)(w >> 32), (int)(w >> 32), false, false);
+    a = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned int)lo[0]);
+    b = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned int)lo[1]);
+}
+template <class Op>
+__device__ __forceinline__ double wtail(double v, Op op) {
+    v = op(v, dppd<0x124>(v));  // row_ror:4
+    v = op(v, dppd<0x128>(v));  // row_ror:8
+    double a, b;
+    plswap16(v, a, b);          // rows (0,1), (2,3)
+    v = op(a, b);
+    plswap32(v, a, b);          // wave halves
+    return op(a, b);
+}
+template <class Op>
+__device__ __forceinline__ void wred2(int lane, double& a, double& b, Op op) {
+    const bool o = lane & 1;
+    double v = op(o ? b : a, dppd<0xB1>(o ? a : b));  // even lanes: a, odd lanes: b
+    v = op(v, dppd<0x4E>(v));
+    v = wtail(v, op);
+    a = readlane_d(v, 0);
+    b = readlane_d(v, 1);
+}
+template <class Op>
+__device__ __forceinline__ void wred4(int lane, double& a, double& b, double& c, double& d, Op op) {
+    const bool o = lane & 1, t = lane & 2;
+    const double k0 = op(o ? c : a, dppd<0xB1>(o ? a : c));  // even lanes: a, c; odd lanes: b, d
+    const double k1 = op(o ? d : b, dppd<0xB1>(o ? b : d));
+    double v = op(t ? k1 : k0, dppd<0x4E>(t ? k0 : k1));    // lane 4m + (0, 1, 2, 3): a, c, b, d
+    v = wtail(v, op);
+    a = readlane_d(v, 0);
+    c = readlane_d(v, 1);
+    b = readlane_d(v, 2);
+    d = readlane_d(v, 3);
+}
+
 // packed upper-triangle index of a symmetric 6x6
 __host__ __device__ constexpr int sym_idx(int i, int j) {
     return i <= j ? i * 6 - (i * (i - 1)) / 2 + (j - i) : j * 6 - (j * (j - 1)) / 2 + (i - j);
@@ -319,8 +370,13 @@ __device__ __forceinline__ void model_lin(const Ctx<BM>& c, const double* x, con
 }
 
 struct Lin {
-    double dinf, pinf, c0, cmu, sy, sz;  // optimality-error pieces
-    double cost, logs, th;               // merit pieces at the current point: F, sum log s, ||c||_1
+    double dinf, pinf, sy, sz;   // optimality-error pieces
+    double zmx, zmn;             // max / min of z*s over the bounds (-inf / +inf without bounds)
+    double cost, logs, th;       // merit pieces at the current point: F, sum log s, ||c||_1
+    // complementarity errors max |z s| and max |z s - mu| from the extremes of z s, exactly (rounding is
+    // monotone: max_i fl(a_i - mu) = fl(max_i a_i - mu)), so a barrier update needs no pass over the stages
+    __device__ __forceinline__ double c0() const { return zmx >= zmn ? fmax(fabs(zmx), fabs(zmn)) : 0.0; }
+    __device__ __forceinline__ double cmu(double mu) const { return zmx >= zmn ? fmax(zmx - mu, mu - zmn) : 0.0; }
 };
 
 // ============ linearise at the current point (stage-parallel) ============
@@ -328,7 +384,8 @@ struct Lin {
 template <int BM>
 __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
     const int N = c.N;
-    double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0, cost = 0.0, th = 0.0, logs = 0.0;
+    double dinf = 0.0, pinf = 0.0, zmx = -INFINITY, zmn = INFINITY, sy = 0.0, sz = 0.0, cost = 0.0, th = 0.0,
+           logs = 0.0;
     bool fin = true, bad = false;
     if (c.pair) {
         // lane pairs: both lanes linearise the dynamics (the curvature and dt*J feed both lanes' gradient
@@ -403,8 +460,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
                 if (c.hl(vb)) {
                     const double zl = c.r(rZL + v, k), sl = xv - c.lb(v), rs = frcp(sl);
                     g -= zl;
-                    c0 = fmax(c0, fabs(zl * sl));
-                    cmu = fmax(cmu, fabs(zl * sl - c.mu));
+                    zmx = fmax(zmx, zl * sl);
+                    zmn = fmin(zmn, zl * sl);
                     sz += zl;
                     sg += zl * rs;
                     db -= rs;
@@ -413,8 +470,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
                 if (c.hu(vb)) {
                     const double zu = c.r(rZU + v, k), su = c.ub(v) - xv, rs = frcp(su);
                     g += zu;
-                    c0 = fmax(c0, fabs(zu * su));
-                    cmu = fmax(cmu, fabs(zu * su - c.mu));
+                    zmx = fmax(zmx, zu * su);
+                    zmn = fmin(zmn, zu * su);
                     sz += zu;
                     sg += zu * rs;
                     db += rs;
@@ -504,8 +561,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
             if (c.hl(v)) {
                 const double zl = c.r(rZL + v, k), s = xv - c.lb(v), rs = frcp(s);
                 g -= zl;
-                c0 = fmax(c0, fabs(zl * s));
-                cmu = fmax(cmu, fabs(zl * s - c.mu));
+                zmx = fmax(zmx, zl * s);
+                zmn = fmin(zmn, zl * s);
                 sz += zl;
                 sg += zl * rs;
                 db -= rs;
@@ -514,8 +571,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
             if (c.hu(v)) {
                 const double zu = c.r(rZU + v, k), s = c.ub(v) - xv, rs = frcp(s);
                 g += zu;
-                c0 = fmax(c0, fabs(zu * s));
-                cmu = fmax(cmu, fabs(zu * s - c.mu));
+                zmx = fmax(zmx, zu * s);
+                zmn = fmin(zmn, zu * s);
                 sz += zu;
                 sg += zu * rs;
                 db += rs;
@@ -529,35 +586,20 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
         logs += ls.value();
     }
     Lin e;
-    e.dinf = wmax((fin && !bad) ? dinf : INFINITY);
-    e.pinf = wmax(pinf);
-    e.c0 = wmax(c0);
-    e.cmu = wmax(cmu);
-    e.sy = wsum(sy);
-    e.sz = wsum(sz);
-    e.cost = wsum(cost);
-    e.logs = wsum(logs);
+    e.dinf = (fin && !bad) ? dinf : INFINITY;
+    e.pinf = pinf;
+    e.zmx = zmx;
+    double nzmn = -zmn;
+    wred4(c.lane, e.dinf, e.pinf, e.zmx, nzmn, OpMax());
+    e.zmn = -nzmn;
+    e.sy = sy;
+    e.sz = sz;
+    e.cost = cost;
+    e.logs = logs;
+    wred4(c.lane, e.sy, e.sz, e.cost, e.logs, OpSum());
     e.th = wsum(th);
     __syncthreads();
     return e;
-}
-
-template <int BM>
-__device__ __forceinline__ double phase_compl_mu(const Ctx<BM>& c) {
-    double cm = 0.0;
-    const int p = c.part();
-    for (int k = c.k0(); k <= c.N; k += c.kst()) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            if (c.pair && t >= 4) break;
-            const int vb = c.pair ? 2 * t : t, v = vb + p;   // vb carries the (pair-symmetric) bound flags
-            if (vb >= 6 && k == c.N) break;
-            const double xv = c.r(rX + v, k);
-            if (c.hl(vb)) cm = fmax(cm, fabs(c.r(rZL + v, k) * (xv - c.lb(v)) - c.mu));
-            if (c.hu(vb)) cm = fmax(cm, fabs(c.r(rZU + v, k) * (c.ub(v) - xv) - c.mu));
-        }
-    }
-    return wmax(cm);
 }
 
 // ============ Riccati recursion, entry-parallel on the VALU ============
@@ -653,21 +695,30 @@ struct EpMap {
 struct EpOps {
     double dj[6], di[6], h, sgu0, sgu1, gj0, gj1, gi0, gi1;
 };
+// in two halves: A (D[.][j], Sigma_u) is issued behind the P-row reads, B (D[.][i], H^, g_u) behind the
+// PA-column reads, which spreads the LDS queue over the stage (tools/ubench_riccati.hip: -44 cycles/stage)
 template <int BM>
-__device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k, double dw) {
-    EpOps o;
+__device__ __forceinline__ void ep_ops_a(const Ctx<BM>& c, const EpMap& m, int k, EpOps& o) {
 #pragma unroll
-    for (int t = 0; t < 6; ++t) {
-        o.dj[t] = c.r(m.dj[t], k);
-        o.di[t] = c.r(m.di[t], k);
-    }
-    o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
+    for (int t = 0; t < 6; ++t) o.dj[t] = c.r(m.dj[t], k);
     o.sgu0 = c.r(rSGU, k);
     o.sgu1 = c.r(rSGU + 1, k);
+}
+template <int BM>
+__device__ __forceinline__ void ep_ops_b(const Ctx<BM>& c, const EpMap& m, int k, double dw, EpOps& o) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) o.di[t] = c.r(m.di[t], k);
+    o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
     o.gj0 = c.r(m.gj0, k);
     o.gj1 = c.r(m.gj1, k);
     o.gi0 = c.r(m.gi0, k);
     o.gi1 = c.r(m.gi1, k);
+}
+template <int BM>
+__device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k, double dw) {
+    EpOps o;
+    ep_ops_a(c, m, k, o);
+    ep_ops_b(c, m, k, dw, o);
     return o;
 }
 
@@ -699,13 +750,16 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const bool own_p = m.ps >= 0;
     const bool k_row = i >= 6 && j < 7;
     const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
-    // one stage; `o` = this stage's operands, `nx` receives stage kn's (prefetch, issued after the
-    // P-tile reads so that waiting for the tile never waits for the prefetch)
+    // one stage; `o` = this stage's operands, `nx` receives stage kn's (prefetch in two halves, each issued
+    // after a tile read so that waiting for the tile never waits for the prefetch)
     auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
         // row i of P^_{k+1} and the reduced input Hessian entries (uniform)
         const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
         const double2 p5 = ld2(PF + 44);  // P[5][4], P[5][5]
         const double p44 = PF[36];
+        __builtin_amdgcn_sched_barrier(0);
+        ep_ops_a(c, m, kn, nx);  // next stage's operands, first half
+        __builtin_amdgcn_sched_barrier(0);
         const double h00 = r00 + o.sgu0 + dw + dt2 * p5.y, h01 = r01 + dt2 * p5.x, h11 = r11 + o.sgu1 + dw + dt2 * p44;
         const double det = h00 * h11 - h01 * h01;
         pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
@@ -722,9 +776,9 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         // column j of PA (rows 0..5; rows 4, 5 also give G[.][j]) and G[.][i]
         const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
         const double2 gi = ld2(PT + 8 * i + 4);  // PA[4][i], PA[5][i]
-        // next stage's operands: issued behind the tile reads (LDS serves a wave in order)
+        // next stage's operands, second half: issued behind the tile reads (LDS serves a wave in order)
         __builtin_amdgcn_sched_barrier(0);
-        nx = ep_ops(c, m, kn, dw);
+        ep_ops_b(c, m, kn, dw, nx);
         // F[i][j] = PA[i][j] + sum_l D[l][i] PA[l][j] + H^[i][j]
         double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
         fa = fma(o.di[2], c23.x, fa);
@@ -912,12 +966,18 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
         }
     }
     StepInfo r;
-    r.az = wmin(az);
-    r.ap = wmin(ap);
     if (primal_pieces) {
+        double naz = -az, nap = -ap, dum = 0.0;
+        r.rel = rel;
+        wred4(c.lane, naz, nap, r.rel, dum, OpMax());
+        r.az = -naz;
+        r.ap = -nap;
         r.Dg = wsum(Dg);
-        r.rel = wmax(rel);
     } else {
+        double naz = -az, nap = -ap;
+        wred2(c.lane, naz, nap, OpMax());
+        r.az = -naz;
+        r.ap = -nap;
         r.Dg = r.rel = 0.0;
     }
     __syncthreads();
@@ -1015,8 +1075,9 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
         thl += th;
     }
     Trial t;
-    t.phi = wsum(bad ? INFINITY : val);  // any lane outside the relaxed box -> +inf
-    t.th = wsum(thl);
+    t.phi = bad ? INFINITY : val;  // any lane outside the relaxed box -> +inf
+    t.th = thl;
+    wred2(c.lane, t.phi, t.th, OpSum());
     __syncthreads();
     return t;
 }
@@ -1244,7 +1305,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             if (!isfinite(e.dinf) || !isfinite(e.pinf)) { status = 4; break; }
             const double sd = fmax(100.0, (e.sy + e.sz) / (double)(6 * (N + 1) + nb)) / 100.0;
             const double sc = nb ? fmax(100.0, e.sz / (double)nb) / 100.0 : 1.0;
-            E0 = fmax(fmax(e.dinf / sd, e.pinf), e.c0 / sc);
+            E0 = fmax(fmax(e.dinf / sd, e.pinf), e.c0() / sc);
             if (E0 <= a.tol) { status = 0; break; }
             if (E0 <= a.acc_tol) {
                 if (++acc_count >= a.acc_iter) { status = 1; break; }
@@ -1253,14 +1314,14 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             }
             if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; break; }
             // barrier parameter (monotone Fiacco-McCormick)
-            double cmu = e.cmu;
+            double cmu = e.cmu(c.mu);
             for (;;) {
                 const double Emu = fmax(fmax(e.dinf / sd, e.pinf), cmu / sc);
                 if (!(Emu <= 10.0 * c.mu && c.mu > a.tol / 10.0 * 1.0000001)) break;
                 c.mu = fmax(a.tol / 10.0, fmin(0.2 * c.mu, c.mu * sqrt(c.mu)));
                 c.tau = fmax(0.99, 1.0 - c.mu);
                 nf = 0;  // IPOPT resets the filter on every barrier update
-                cmu = phase_compl_mu(c);
+                cmu = e.cmu(c.mu);
             }
             STAMP(PH_MU_BAR);
             // Newton step: Riccati with inertia correction

@@ -7,6 +7,8 @@
 #include "../car-trailer-mpc_amd/csrc/tt_track.hip"
 
 #include <cstdio>
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 namespace ttmpc {
@@ -14,27 +16,48 @@ namespace {
 
 constexpr int UB_BM = kMaskMPC | kDiagBit;
 constexpr int UB_N = 20;
-constexpr int UB_SR2 = 118;  // even stride for the paired-row emulation (V = 8)
+constexpr int UB_SR2 = 118;  // even stride for the paired-row emulation (V = 8); V = 10 uses SR (odd)
 
 // V: 0 = copy of the shipped stage; 1 = no next-stage prefetch (operands reused); 2 = no factor-row
 //    store; 5 = 1 + 2; 8 = prefetch as 10 reads (D pairs / g_u pairs / Sigma_u pair as b128 from an even
-//    stride) instead of 19; 9 = the real phase_riccati
+//    stride) instead of 19; 9 = the real phase_riccati; 10 = 8 on the odd stride (b128 at 8-byte
+//    alignment: the unaligned DS mode); 12 = dj, Sigma_u prefetched after the P-row reads, the rest after
+//    the PA-column reads; 13 = all after the P-row reads; 14 = 8 on the odd stride as ds_read2_b64
+__device__ __forceinline__ double2 ldu(const double* p) {  // b128 at 8-byte alignment (V = 10)
+    return *reinterpret_cast<const double2*>(__builtin_assume_aligned(p, 16));
+}
 template <int V>
 __device__ __forceinline__ EpOps ub_ops(const Ctx<UB_BM>& c, const EpMap& m, int k, double dw) {
-    if constexpr (V != 8) {
+    if constexpr (V == 14) {  // the paired layout on the odd stride, as adjacent b64 reads (ds_read2_b64)
+        EpOps o;
+        const double* s = c.sm + HEAD + k * SR;
+        const int pj = 2 * (c.lane & 7), pi = 2 * (c.lane >> 3);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const double* a = s + pj + 16 * t;
+            const double* b = s + pi + 16 * t + 48;
+            o.dj[2 * t] = a[0]; o.dj[2 * t + 1] = a[1];
+            o.di[2 * t] = b[0]; o.di[2 * t + 1] = b[1];
+        }
+        o.h = m.q2 + m.dg * dw + s[m.hs];
+        const double* gj = s + 96 + pj / 8 * 2;
+        const double* gi = s + 100 + pi / 8 * 2;
+        o.sgu0 = s[108]; o.sgu1 = s[109]; o.gj0 = gj[0]; o.gj1 = gj[1]; o.gi0 = gi[0]; o.gi1 = gi[1];
+        return o;
+    } else if constexpr (V != 8 && V != 10) {
         return ep_ops(c, m, k, dw);
     } else {
         EpOps o;
-        const double* s = c.sm + HEAD + k * UB_SR2;
+        const double* s = c.sm + HEAD + k * (V == 8 ? UB_SR2 : SR);
         const int pj = 2 * (c.lane & 7), pi = 2 * (c.lane >> 3);  // even row offsets per lane
 #pragma unroll
         for (int t = 0; t < 3; ++t) {
-            const double2 a = ld2(s + pj + 16 * t), b = ld2(s + pi + 16 * t + 48);
+            const double2 a = ldu(s + pj + 16 * t), b = ldu(s + pi + 16 * t + 48);
             o.dj[2 * t] = a.x; o.dj[2 * t + 1] = a.y;
             o.di[2 * t] = b.x; o.di[2 * t + 1] = b.y;
         }
         o.h = m.q2 + m.dg * dw + s[m.hs];
-        const double2 su = ld2(s + 108), gj = ld2(s + 96 + pj / 8 * 2), gi = ld2(s + 100 + pi / 8 * 2);
+        const double2 su = ldu(s + 108), gj = ldu(s + 96 + pj / 8 * 2), gi = ldu(s + 100 + pi / 8 * 2);
         o.sgu0 = su.x; o.sgu1 = su.y; o.gj0 = gj.x; o.gj1 = gj.y; o.gi0 = gi.x; o.gi1 = gi.y;
         return o;
     }
@@ -62,6 +85,20 @@ __device__ __forceinline__ bool ub_riccati(const Ctx<UB_BM>& c, double dw) {
         const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
         const double2 p5 = ld2(PF + 44);
         const double p44 = PF[36];
+        if constexpr (V == 12 || V == 13) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < 6; ++t) nx.dj[t] = c.r(m.dj[t], kn);
+            nx.sgu0 = c.r(rSGU, kn);
+            nx.sgu1 = c.r(rSGU + 1, kn);
+            if constexpr (V == 13) {
+#pragma unroll
+                for (int t = 0; t < 6; ++t) nx.di[t] = c.r(m.di[t], kn);
+                nx.h = m.q2 + m.dg * dw + c.r(m.hs, kn);
+                nx.gj0 = c.r(m.gj0, kn); nx.gj1 = c.r(m.gj1, kn); nx.gi0 = c.r(m.gi0, kn); nx.gi1 = c.r(m.gi1, kn);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
         const double h00 = r00 + o.sgu0 + dw + dt2 * p5.y, h01 = r01 + dt2 * p5.x, h11 = r11 + o.sgu1 + dw + dt2 * p44;
         const double det = h00 * h11 - h01 * h01;
         pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
@@ -77,8 +114,17 @@ __device__ __forceinline__ bool ub_riccati(const Ctx<UB_BM>& c, double dw) {
         const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
         const double2 gi = ld2(PT + 8 * i + 4);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (V != 1 && V != 5) nx = ub_ops<V>(c, m, kn, dw);
-        else nx = o;
+        if constexpr (V == 12) {
+#pragma unroll
+            for (int t = 0; t < 6; ++t) nx.di[t] = c.r(m.di[t], kn);
+            nx.h = m.q2 + m.dg * dw + c.r(m.hs, kn);
+            nx.gj0 = c.r(m.gj0, kn); nx.gj1 = c.r(m.gj1, kn); nx.gi0 = c.r(m.gi0, kn); nx.gi1 = c.r(m.gi1, kn);
+        } else if constexpr (V == 13) {
+        } else if constexpr (V != 1 && V != 5) {
+            nx = ub_ops<V>(c, m, kn, dw);
+        } else {
+            nx = o;
+        }
         double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
         fa = fma(o.di[2], c23.x, fa);
         fb = fma(o.di[3], c23.y, fb);
@@ -153,6 +199,63 @@ void run(const char* name, int B = 1024) {
     (void)hipFree(d_bad);
 }
 
+__global__ __launch_bounds__(64) void ua_kernel(double* out) {
+    __shared__ __attribute__((aligned(16))) double t[256];
+    for (int q = threadIdx.x; q < 256; q += 64) t[q] = (double)q + 0.25;
+    __syncthreads();
+    const int off = 2 * threadIdx.x + 1;  // odd: 8-byte aligned only
+    const double2 v = *reinterpret_cast<const double2*>(__builtin_assume_aligned(t + off, 16));
+    out[2 * threadIdx.x] = v.x;
+    out[2 * threadIdx.x + 1] = v.y;
+}
+
+__global__ __launch_bounds__(64) void wred_kernel(const double* in, double* out) {
+    const int l = threadIdx.x;
+    double a = in[l], b = in[64 + l], c = in[128 + l], d = in[192 + l];
+    double e = a, f = b;
+    wred4(l, a, b, c, d, OpSum());
+    wred2(l, e, f, OpMax());
+    double g = in[l], h = in[64 + l], i2 = in[128 + l], j2 = in[192 + l];
+    wred4(l, g, h, i2, j2, OpMax());
+    if (l == 0) { out[0] = a; out[1] = b; out[2] = c; out[3] = d; out[4] = e; out[5] = f; }
+    if (l == 5) { out[6] = g; out[7] = h; out[8] = i2; out[9] = j2; }
+}
+
+void check_wred() {
+    std::vector<double> h(256);
+    for (int t = 0; t < 256; ++t) h[t] = (double)((t * 7919) % 1000) / 7.0 - 50.0;
+    double *din, *dout;
+    (void)hipMalloc(&din, 256 * sizeof(double));
+    (void)hipMalloc(&dout, 16 * sizeof(double));
+    (void)hipMemcpy(din, h.data(), 256 * sizeof(double), hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(wred_kernel, dim3(1), dim3(64), 0, 0, din, dout);
+    double o[16];
+    (void)hipMemcpy(o, dout, 10 * sizeof(double), hipMemcpyDeviceToHost);
+    double sm[4] = {0, 0, 0, 0}, mx[4] = {-1e300, -1e300, -1e300, -1e300};
+    for (int q = 0; q < 4; ++q)
+        for (int l = 0; l < 64; ++l) { sm[q] += h[64 * q + l]; mx[q] = std::max(mx[q], h[64 * q + l]); }
+    int bad = 0;
+    for (int q = 0; q < 4; ++q) bad += std::fabs(o[q] - sm[q]) > 1e-9 * (1 + std::fabs(sm[q]));
+    bad += o[4] != mx[0] || o[5] != mx[1];
+    for (int q = 0; q < 4; ++q) bad += o[6 + q] != mx[q];
+    printf("wred2/wred4: %d wrong (sums %.6f %.6f %.6f %.6f vs %.6f %.6f %.6f %.6f)\n", bad, o[0], o[1], o[2], o[3],
+           sm[0], sm[1], sm[2], sm[3]);
+    (void)hipFree(din);
+    (void)hipFree(dout);
+}
+
+void check_unaligned() {
+    double* d;
+    (void)hipMalloc(&d, 128 * sizeof(double));
+    hipLaunchKernelGGL(ua_kernel, dim3(1), dim3(64), 0, 0, d);
+    std::vector<double> h(128);
+    (void)hipMemcpy(h.data(), d, 128 * sizeof(double), hipMemcpyDeviceToHost);
+    int bad = 0;
+    for (int l = 0; l < 64; ++l) bad += h[2 * l] != 2 * l + 1.25 || h[2 * l + 1] != 2 * l + 2.25;
+    printf("8-byte aligned ds_read_b128: %d of 64 lanes wrong (lane 0: %.2f %.2f)\n", bad, h[0], h[1]);
+    (void)hipFree(d);
+}
+
 }  // namespace
 }  // namespace ttmpc
 
@@ -164,5 +267,10 @@ int main() {
     run<2>("no factor-row store");
     run<5>("no prefetch, no store");
     run<8>("prefetch as 10 paired reads");
+    run<14>("10 paired reads as read2_b64, odd stride");
+    run<12>("prefetch split: dj+sgu after the P-row reads");
+    run<13>("prefetch all after the P-row reads");
+    check_unaligned();
+    check_wred();
     return 0;
 }
