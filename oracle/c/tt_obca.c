@@ -67,6 +67,9 @@
 #define BOUND_MULT_RESET 1000.0 /* bound_mult_reset_threshold */
 #define CONSTR_MULT_INIT_MAX 1000.0
 #define SOFT_RESTO_FACTOR 0.9999
+#define WD_TRIGGER 10            /* watchdog_shortened_iter_trigger */
+#define WD_TRIAL_MAX 3           /* watchdog_trial_iter_max */
+#define KAPPA_D 1e-5            /* kappa_d: linear damping of variables with one finite bound */
 #define MAX_SOFT_RESTO 10
 
 static int isfree(double b) { return !isfinite(b) || fabs(b) >= 1e19; }
@@ -82,6 +85,7 @@ typedef struct {
     const tto_obca_problem* P;
     int N, M, nbk, nb, n, mode;
     int R;          /* M_ORIG / M_RESTO: which NLP the Newton machinery assembles */
+    double kd;      /* kappa_d (0 when switched off) */
     int lsq;        /* least-squares multiplier system: unit Hessian, gradients grad f - z */
     double Qc[36], Rc[4];
     double xl[6], xu[6], ul[2], uu[2];
@@ -122,8 +126,9 @@ typedef struct {
     /* last acceptable iterate (IPOPT's stored acceptable point) */
     double *xacc, *uacc, *wacc;
     int have_acc;
-    /* soft restoration / SOC save area */
+    /* soft restoration / SOC save area; watchdog save area (iterate + search direction) */
     double* sv;
+    double* wdv;
     double* mem;
 } ws_t;
 
@@ -335,6 +340,7 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->svL, nb * 4); TAKE(W->svU, nb * 4);
     TAKE(W->xacc, N1 * 6); TAKE(W->uacc, N * 2); TAKE(W->wacc, nb * 8);
     TAKE(W->sv, 4 * (N1 * 6 + N * 2 + nb * 8 + nb * 4) + 2 * nr + nsv);
+    TAKE(W->wdv, 2 * (N1 * 6 * 4 + N * 2 * 3 + nb * 8 * 2 + nb * 4 * 4 + 4 * nr + 24) + 64);
 #undef TAKE
     W->mem = (double*)calloc(tot, sizeof(double));
     if (!W->mem) return -1;
@@ -448,32 +454,43 @@ static double barrier(const ws_t* W, const double* x, const double* u, const dou
                       const double* sf, const double* p, const double* n, double mu, int* bad) {
     double b = 0.0;
     *bad = 0;
+    const double kdm = W->kd * mu;
 #define BL(val, lo) do { double t_ = (val) - (lo); if (!(t_ > 0)) { *bad = 1; return 0; } b -= mu * log(t_); } while (0)
 #define BU(val, hi) do { double t_ = (hi) - (val); if (!(t_ > 0)) { *bad = 1; return 0; } b -= mu * log(t_); } while (0)
+#define DL(val, lo) (b += kdm * ((val) - (lo)))
+#define DU(val, hi) (b += kdm * ((hi) - (val)))
     for (int k = 0; k <= W->N; ++k) {
         for (int i = 0; i < 6; ++i) {
             if (W->hxl[i]) BL(x[6 * k + i], W->xl[i]);
             if (W->hxu[i]) BU(x[6 * k + i], W->xu[i]);
+            if (W->hxl[i] && !W->hxu[i]) DL(x[6 * k + i], W->xl[i]);
+            if (W->hxu[i] && !W->hxl[i]) DU(x[6 * k + i], W->xu[i]);
         }
         if (k < W->N)
             for (int i = 0; i < 2; ++i) {
                 if (W->hul[i]) BL(u[2 * k + i], W->ul[i]);
                 if (W->huu[i]) BU(u[2 * k + i], W->uu[i]);
+                if (W->hul[i] && !W->huu[i]) DL(u[2 * k + i], W->ul[i]);
+                if (W->huu[i] && !W->hul[i]) DU(u[2 * k + i], W->uu[i]);
             }
     }
     for (int bi = 0; bi < W->nb; ++bi) {
-        for (int e = 0; e < 8; ++e) BL(w[8 * bi + e], -RELAX);
+        for (int e = 0; e < 8; ++e) { BL(w[8 * bi + e], -RELAX); DL(w[8 * bi + e], -RELAX); }
         for (int r = 0; r < 4; ++r) {
             if (W->hrL[r]) BL(s[4 * bi + r], W->rL[r]);
             if (W->hrU[r]) BU(s[4 * bi + r], W->rU[r]);
+            if (W->hrL[r] && !W->hrU[r]) DL(s[4 * bi + r], W->rL[r]);
+            if (W->hrU[r] && !W->hrL[r]) DU(s[4 * bi + r], W->rU[r]);
         }
     }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) { BL(sf[i], W->fL); BU(sf[i], W->fU); }
     if (p)
-        for (int i = 0; i < W->nrow; ++i) { BL(p[i], 0.0); BL(n[i], 0.0); }
+        for (int i = 0; i < W->nrow; ++i) { BL(p[i], 0.0); BL(n[i], 0.0); DL(p[i], 0.0); DL(n[i], 0.0); }
 #undef BL
 #undef BU
+#undef DL
+#undef DU
     return b;
 }
 
@@ -530,6 +547,7 @@ static double bgrad_x(const ws_t* W, int k, int i, double mu) {
     if (W->lsq) return g - (W->hxl[i] ? W->zLx[6 * k + i] : 0.0) + (W->hxu[i] ? W->zUx[6 * k + i] : 0.0);
     if (W->hxl[i]) g -= mu / (v - W->xl[i]);
     if (W->hxu[i]) g += mu / (W->xu[i] - v);
+    if (W->hxl[i] != W->hxu[i]) g += W->hxl[i] ? W->kd * mu : -W->kd * mu;
     return g;
 }
 static double bgrad_u(const ws_t* W, int k, int i, double mu) {
@@ -538,11 +556,12 @@ static double bgrad_u(const ws_t* W, int k, int i, double mu) {
     if (W->lsq) return g - (W->hul[i] ? W->zLu[2 * k + i] : 0.0) + (W->huu[i] ? W->zUu[2 * k + i] : 0.0);
     if (W->hul[i]) g -= mu / (v - W->ul[i]);
     if (W->huu[i]) g += mu / (W->uu[i] - v);
+    if (W->hul[i] != W->huu[i]) g += W->hul[i] ? W->kd * mu : -W->kd * mu;
     return g;
 }
 static double bgrad_w(const ws_t* W, int v, double mu) {
     if (W->lsq) return W->gw[v] - W->zw[v];
-    return W->gw[v] - mu / (W->w[v] + RELAX);
+    return W->gw[v] - mu / (W->w[v] + RELAX) + W->kd * mu;
 }
 static double bgrad_s(const ws_t* W, int bi, int r, double mu) {
     const int v = 4 * bi + r;
@@ -551,6 +570,7 @@ static double bgrad_s(const ws_t* W, int bi, int r, double mu) {
     double g = 0.0;
     if (W->hrL[r]) g -= mu / (sv - W->rL[r]);
     if (W->hrU[r]) g += mu / (W->rU[r] - sv);
+    if (W->hrL[r] != W->hrU[r]) g += W->hrL[r] ? W->kd * mu : -W->kd * mu;
     return g;
 }
 static double bgrad_sf(const ws_t* W, int i, double mu) {
@@ -809,8 +829,8 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
     const int rs = W->R == M_RESTO;
     if (rs)
         for (int i = 0; i < W->nrow; ++i) {
-            const double gp = W->rho - (W->lsq ? W->zp[i] : mu / W->pr[i]);
-            const double gn = W->rho - (W->lsq ? W->zn[i] : mu / W->nr[i]);
+            const double gp = W->rho - (W->lsq ? W->zp[i] : mu / W->pr[i] - W->kd * mu);
+            const double gn = W->rho - (W->lsq ? W->zn[i] : mu / W->nr[i] - W->kd * mu);
             W->gpn[i] = gp / W->Dpr[i] - gn / W->Dnr[i];
         }
     for (int i = 0; i < W->nrc; ++i) W->rct[i] = cres[i] + (rs ? W->gpn[i] : 0.0);
@@ -962,8 +982,8 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
     if (rs) /* elastic variables: D_p dp - y+ = -(rho - mu/p),  D_n dn + y+ = -(rho - mu/n) */
         for (int i = 0; i < W->nrow; ++i) {
             const double yp = i < W->nrc ? W->ycp[i] : i < W->nrc + W->nrd ? W->ydp[i - W->nrc] : W->ydpf[i - W->nrc - W->nrd];
-            W->dpr[i] = (yp - (W->rho - mu / W->pr[i])) / W->Dpr[i];
-            W->dnr[i] = (-yp - (W->rho - mu / W->nr[i])) / W->Dnr[i];
+            W->dpr[i] = (yp - (W->rho - mu / W->pr[i] + W->kd * mu)) / W->Dpr[i];
+            W->dnr[i] = (-yp - (W->rho - mu / W->nr[i] + W->kd * mu)) / W->Dnr[i];
         }
 }
 
@@ -1147,6 +1167,42 @@ static double ftb_primal(const ws_t* W, double tau) {
     return a;
 }
 
+/* TTO_DEBUG: the primal fraction to the boundary per variable class (x u w s sf p n) */
+static void ftb_classes(const ws_t* W, double tau, double* c) {
+    for (int q = 0; q < 7; ++q) c[q] = 1.0;
+    for (int k = 0; k <= W->N; ++k) {
+        for (int i = 0; i < 6; ++i) {
+            const int v = 6 * k + i;
+            if (W->hxl[i]) FTB_P(W->x[v], W->xl[i], W->dx[v], tau, c[0]);
+            if (W->hxu[i]) FTB_PU(W->x[v], W->xu[i], W->dx[v], tau, c[0]);
+        }
+        if (k < W->N)
+            for (int i = 0; i < 2; ++i) {
+                const int v = 2 * k + i;
+                if (W->hul[i]) FTB_P(W->u[v], W->ul[i], W->du[v], tau, c[1]);
+                if (W->huu[i]) FTB_PU(W->u[v], W->uu[i], W->du[v], tau, c[1]);
+            }
+    }
+    for (int bi = 0; bi < W->nb; ++bi) {
+        for (int e = 0; e < 8; ++e) FTB_P(W->w[8 * bi + e], -RELAX, W->dw[8 * bi + e], tau, c[2]);
+        for (int r = 0; r < 4; ++r) {
+            const int v = 4 * bi + r;
+            if (W->hrL[r]) FTB_P(W->s[v], W->rL[r], W->ds[v], tau, c[3]);
+            if (W->hrU[r]) FTB_PU(W->s[v], W->rU[r], W->ds[v], tau, c[3]);
+        }
+    }
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            FTB_P(W->sf[i], W->fL, W->dsf[i], tau, c[4]);
+            FTB_PU(W->sf[i], W->fU, W->dsf[i], tau, c[4]);
+        }
+    if (W->R == M_RESTO)
+        for (int i = 0; i < W->nrow; ++i) {
+            FTB_P(W->pr[i], 0.0, W->dpr[i], tau, c[5]);
+            FTB_P(W->nr[i], 0.0, W->dnr[i], tau, c[6]);
+        }
+}
+
 static double ftb_dual(const ws_t* W, double tau) {
     double a = 1.0;
     for (int k = 0; k <= W->N; ++k) {
@@ -1194,8 +1250,9 @@ static opterr_t opt_error(ws_t* W, double mu) {
     double dinf = 0.0, pinf = 0.0, c0 = 0.0, cmu = 0.0, sy = 0.0, sz = 0.0, d1 = 0.0, p1 = 0.0, cm1 = 0.0;
     long nb_ = 0, my = 0;
     opterr_t o;
+    double dcl[8] = {0};
     o.finite = 1;
-#define DINF(t) do { const double t_ = (t); dinf = fmax(dinf, fabs(t_)); d1 += fabs(t_); if (!isfinite(t_)) o.finite = 0; } while (0)
+#define DINF(t, c_) do { const double t_ = (t); dinf = fmax(dinf, fabs(t_)); dcl[c_] = fmax(dcl[c_], fabs(t_)); d1 += fabs(t_); if (!isfinite(t_)) o.finite = 0; } while (0)
 #define CMPL(z, sl) do { const double z_ = (z), s_ = (sl); c0 = fmax(c0, fabs(z_ * s_)); cmu = fmax(cmu, fabs(z_ * s_ - mu)); cm1 += fabs(z_ * s_ - mu); sz += z_; ++nb_; } while (0)
     for (int k = 0; k <= N; ++k) {
         double gl[6];
@@ -1212,12 +1269,12 @@ static opterr_t opt_error(ws_t* W, double mu) {
             for (int a = 0; a < 8; ++a) {
                 double t = W->gw[8 * bi + a] - W->zw[8 * bi + a];
                 for (int r = 0; r < 4; ++r) t += W->Jw[32 * bi + r * 8 + a] * W->yd[4 * bi + r];
-                DINF(t);
+                DINF(t, 2);
                 CMPL(W->zw[8 * bi + a], W->w[8 * bi + a] + RELAX);
             }
             for (int r = 0; r < 4; ++r) {
                 const int v = 4 * bi + r;
-                DINF(-W->yd[v] - W->vL[v] + W->vU[v]);
+                DINF(-W->yd[v] - W->vL[v] + W->vU[v], 3);
                 pinf = fmax(pinf, fabs(W->rd0[v]));
                 p1 += fabs(W->rd0[v]);
                 sy += fabs(W->yd[v]); ++my;
@@ -1228,7 +1285,7 @@ static opterr_t opt_error(ws_t* W, double mu) {
         for (int i = 0; i < 6; ++i) {
             const int v = 6 * k + i;
             gl[i] += -W->zLx[v] + W->zUx[v];
-            DINF(gl[i]);
+            DINF(gl[i], 0);
             if (W->hxl[i]) CMPL(W->zLx[v], W->x[v] - W->xl[i]);
             if (W->hxu[i]) CMPL(W->zUx[v], W->xu[i] - W->x[v]);
             pinf = fmax(pinf, fabs(W->rc0[v]));
@@ -1238,14 +1295,14 @@ static opterr_t opt_error(ws_t* W, double mu) {
         if (k < N)
             for (int i = 0; i < 2; ++i) {
                 const int v = 2 * k + i;
-                DINF(W->gu[v] - P->dt * W->yc[6 * (k + 1) + (i == 0 ? 5 : 4)] - W->zLu[v] + W->zUu[v]);
+                DINF(W->gu[v] - P->dt * W->yc[6 * (k + 1) + (i == 0 ? 5 : 4)] - W->zLu[v] + W->zUu[v], 1);
                 if (W->hul[i]) CMPL(W->zLu[v], W->u[v] - W->ul[i]);
                 if (W->huu[i]) CMPL(W->zUu[v], W->uu[i] - W->u[v]);
             }
     }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) {
-            DINF(-W->ydf[i] - W->vLf[i] + W->vUf[i]);
+            DINF(-W->ydf[i] - W->vLf[i] + W->vUf[i], 4);
             pinf = fmax(pinf, fabs(W->rf0[i]));
             p1 += fabs(W->rf0[i]);
             sy += fabs(W->ydf[i]); ++my;
@@ -1255,8 +1312,8 @@ static opterr_t opt_error(ws_t* W, double mu) {
     if (rs) /* elastic variables: rho - y - z_p = 0, rho + y - z_n = 0 */
         for (int i = 0; i < W->nrow; ++i) {
             const double y = i < W->nrc ? W->yc[i] : i < W->nrc + W->nrd ? W->yd[i - W->nrc] : W->ydf[i - W->nrc - W->nrd];
-            DINF(W->rho - y - W->zp[i]);
-            DINF(W->rho + y - W->zn[i]);
+            DINF(W->rho - y - W->zp[i], 5);
+            DINF(W->rho + y - W->zn[i], 6);
             CMPL(W->zp[i], W->pr[i]);
             CMPL(W->zn[i], W->nr[i]);
         }
@@ -1271,6 +1328,16 @@ static opterr_t opt_error(ws_t* W, double mu) {
     o.dinf = dinf;
     o.pinf = pinf;
     o.pderr = d1 + p1 + cm1;
+    if (getenv("TTO_DEBUG2")) {
+        double my_ = 0, mz = 0, mzw = 0, mv = 0;
+        for (int i = 0; i < W->nrc; ++i) my_ = fmax(my_, fabs(W->yc[i]));
+        double myd = 0; for (int i = 0; i < W->nrd; ++i) myd = fmax(myd, fabs(W->yd[i]));
+        for (int i = 0; i < 6 * (N + 1); ++i) mz = fmax(mz, fmax(W->zLx[i], W->zUx[i]));
+        for (int i = 0; i < 8 * W->nb; ++i) mzw = fmax(mzw, W->zw[i]);
+        for (int i = 0; i < 4 * W->nb; ++i) mv = fmax(mv, fmax(W->vL[i], W->vU[i]));
+        fprintf(stderr, "   dinf by class: w %.1e s %.1e x %.1e u %.1e sf %.1e p %.1e n %.1e | |yc| %.1e |yd| %.1e zx %.1e zw %.1e v %.1e sd %.1e\n",
+                dcl[2], dcl[3], dcl[0], dcl[1], dcl[4], dcl[5], dcl[6], my_, myd, mz, mzw, mv, sd);
+    }
     return o;
 }
 
@@ -1395,6 +1462,27 @@ static void snapshot(ws_t* W, int restore) {
     SV(W->zLx, N1 * 6); SV(W->zUx, N1 * 6); SV(W->zLu, N * 2); SV(W->zUu, N * 2); SV(W->zw, nb * 8);
     SV(W->vL, nb * 4); SV(W->vU, nb * 4); SV(W->yc, N1 * 6); SV(W->yd, nb * 4);
     SV(W->sf, 6); SV(W->vLf, 6); SV(W->vUf, 6); SV(W->ydf, 6);
+#undef SV
+}
+
+/* watchdog save area: the iterate and the search direction of the iteration the watchdog started at */
+static void wd_save(ws_t* W, int restore) {
+    double* o = W->wdv;
+    const size_t N1 = (size_t)W->N + 1, N = (size_t)W->N, nb = (size_t)W->nb, nr = (size_t)W->nrow;
+    const int rs = W->R == M_RESTO;
+#define SV(ptr, cnt) do { if (restore) memcpy(ptr, o, (cnt) * 8); else memcpy(o, ptr, (cnt) * 8); o += (cnt); } while (0)
+    SV(W->x, N1 * 6); SV(W->u, N * 2); SV(W->w, nb * 8); SV(W->s, nb * 4);
+    SV(W->zLx, N1 * 6); SV(W->zUx, N1 * 6); SV(W->zLu, N * 2); SV(W->zUu, N * 2); SV(W->zw, nb * 8);
+    SV(W->vL, nb * 4); SV(W->vU, nb * 4); SV(W->yc, N1 * 6); SV(W->yd, nb * 4);
+    SV(W->sf, 6); SV(W->vLf, 6); SV(W->vUf, 6); SV(W->ydf, 6);
+    SV(W->dx, N1 * 6); SV(W->du, N * 2); SV(W->dw, nb * 8); SV(W->ds, nb * 4); SV(W->ycp, N1 * 6); SV(W->ydp, nb * 4);
+    SV(W->dzLx, N1 * 6); SV(W->dzUx, N1 * 6); SV(W->dzLu, N * 2); SV(W->dzUu, N * 2); SV(W->dzw, nb * 8);
+    SV(W->dvL, nb * 4); SV(W->dvU, nb * 4);
+    SV(W->dsf, 6); SV(W->ydpf, 6); SV(W->dvLf, 6); SV(W->dvUf, 6);
+    if (rs) {
+        SV(W->pr, nr); SV(W->nr, nr); SV(W->zp, nr); SV(W->zn, nr);
+        SV(W->dpr, nr); SV(W->dnr, nr); SV(W->dzp, nr); SV(W->dzn, nr);
+    }
 #undef SV
 }
 
@@ -1581,6 +1669,9 @@ typedef struct {
     double mu, tau, th_max, th_min, dw_last;
     int acc_count;
     filter_t F;
+    /* watchdog (IPOPT BacktrackingLineSearch): shortened-step count, active flag, trials, reference point */
+    int wd_short, wd_on, wd_trial;
+    double wd_th, wd_ph, wd_Dm, wd_alpha;
 } ipm_state_t;
 
 static void ipm_reset(ipm_state_t* S, double mu) {
@@ -1590,6 +1681,7 @@ static void ipm_reset(ipm_state_t* S, double mu) {
     S->dw_last = 0.0;
     S->acc_count = 0;
     S->F.n = 0;
+    S->wd_short = S->wd_on = S->wd_trial = 0;
 }
 
 static double dir_deriv(ws_t* W, double mu, double* rel_out) {
@@ -1623,7 +1715,7 @@ static double dir_deriv(ws_t* W, double mu, double* rel_out) {
         }
     if (W->R == M_RESTO)
         for (int i = 0; i < W->nrow; ++i) {
-            Dm += (W->rho - mu / W->pr[i]) * W->dpr[i] + (W->rho - mu / W->nr[i]) * W->dnr[i];
+            Dm += (W->rho - mu / W->pr[i] + W->kd * mu) * W->dpr[i] + (W->rho - mu / W->nr[i] + W->kd * mu) * W->dnr[i];
             rel = fmax(rel, fmax(fabs(W->dpr[i]) / (1.0 + fabs(W->pr[i])), fabs(W->dnr[i]) / (1.0 + fabs(W->nr[i]))));
         }
     *rel_out = rel;
@@ -1727,10 +1819,10 @@ static void check_newton(ws_t* W, double mu, double dw) {
         for (int i = 0; i < W->nrow; ++i) {
             const double yp = i < W->nrc ? W->ycp[i] : i < W->nrc + W->nrd ? W->ydp[i - W->nrc] : W->ydpf[i - W->nrc - W->nrd];
             double t = 0, sc = 0;
-            ACC((W->zp[i] / W->pr[i] + dw) * W->dpr[i], 0); ACC(-yp, 0); ACC(W->rho - mu / W->pr[i], 0);
+            ACC((W->zp[i] / W->pr[i] + dw) * W->dpr[i], 0); ACC(-yp, 0); ACC(W->rho - mu / W->pr[i] + W->kd * mu, 0);
             wpn = fmax(wpn, fabs(t) / (sc + 1e-300));
             t = 0; sc = 0;
-            ACC((W->zn[i] / W->nr[i] + dw) * W->dnr[i], 0); ACC(yp, 0); ACC(W->rho - mu / W->nr[i], 0);
+            ACC((W->zn[i] / W->nr[i] + dw) * W->dnr[i], 0); ACC(yp, 0); ACC(W->rho - mu / W->nr[i] + W->kd * mu, 0);
             wpn = fmax(wpn, fabs(t) / (sc + 1e-300));
         }
 #undef ACC
@@ -1759,12 +1851,74 @@ static int newton(ws_t* W, ipm_state_t* S, double* dw_out) {
 
 /* filter line search with second-order corrections on the current system.  Returns 1 (accepted, h-type
  * adds a filter entry), 0 (line search failed); *alpha_out / *az_out the step sizes. */
-static int line_search(ws_t* W, ipm_state_t* S, int iter0, double th0, double phi0, double* alpha_out, double* az_out) {
+static _Thread_local double g_dbg_ap, g_dbg_sw; /* TTO_DEBUG trace of the last line search */
+static _Thread_local int g_dbg_acc;
+
+/* filter acceptability of a trial (th, ph) against the reference (th0, phi0, Dm) at the step alpha
+ * (FilterLSAcceptor::CheckAcceptabilityOfTrialPoint); *ftype: the switching condition held (f-type) */
+static int acceptable(const ipm_state_t* S, double th, double ph, double th0, double phi0, double Dm, double alpha,
+                      int* ftype) {
+    const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8;
+    const double tolc = 10.0 * DBL_EPSILON;
+    const int sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
+    *ftype = 0;
+    if (!(isfinite(ph) && th <= S->th_max && !in_filter(&S->F, th, ph))) return 0;
+    if (th0 <= S->th_min && sw) { *ftype = 1; return ph - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
+    return th <= (1.0 - g_th) * th0 || ph - (phi0 - g_ph * th0) <= tolc * fabs(phi0);
+}
+
+/* filter line search with second-order corrections and IPOPT's watchdog on the current system.  Returns 1
+ * (accepted; h-type steps add a filter entry), 0 (line search failed); *alpha_out / *az_out the step sizes.
+ * *th0 / *phi0 are the reference values; they change when a failed watchdog restores its stored iterate
+ * (the iterate is then re-linearised, so a caller that falls back to restoration sees the restored point). */
+static int line_search(ws_t* W, ipm_state_t* S, int iter0, double* th0p, double* phi0p, double* alpha_out,
+                       double* az_out) {
     const double mu = S->mu, tau = S->tau;
+    double th0 = *th0p, phi0 = *phi0p;
     double ap = ftb_primal(W, tau), az = ftb_dual(W, tau), rel = 0.0;
-    const double Dm = dir_deriv(W, mu, &rel);
+    double Dm = dir_deriv(W, mu, &rel);
     if (iter0 || !(S->th_max > 0)) { S->th_max = 1e4 * fmax(1.0, th0); S->th_min = 1e-4 * fmax(1.0, th0); }
-    const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
+    const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, g_al = 0.05;
+    const int rs = W->R == M_RESTO;
+    const size_t nx_ = 6 * (size_t)(W->N + 1), nu_ = 2 * (size_t)W->N, nw_ = 8 * (size_t)W->nb, ns_ = 4 * (size_t)W->nb;
+    const size_t nr_ = (size_t)W->nrow;
+    double tht = 0.0, pht = 0.0;
+    int accepted = 0, ftype = 0, skip_first = 0, nsteps = 0;
+    const int use_wd = (W->P->opts & TTO_OPT_WATCHDOG) && rel >= 1e-15;
+    /* watchdog: after WD_TRIGGER consecutive shortened steps, store the iterate and direction and take full
+     * steps, each tested against the stored point, for at most WD_TRIAL_MAX iterations */
+    if (use_wd && !S->wd_on && S->wd_short >= WD_TRIGGER) {
+        wd_save(W, 0);
+        S->wd_on = 1;
+        S->wd_trial = 0;
+        S->wd_th = th0; S->wd_ph = phi0; S->wd_Dm = Dm; S->wd_alpha = ap;
+    }
+    if (S->wd_on) {
+        set_trial(W, ap);
+        trial_eval(W, mu, &tht, &pht);
+        if (acceptable(S, tht, pht, S->wd_th, S->wd_ph, S->wd_Dm, S->wd_alpha, &ftype)) {
+            S->wd_on = 0; /* watchdog successful */
+            S->wd_short = 0;
+            if (!ftype) add_filter(&S->F, (1.0 - g_th) * S->wd_th, S->wd_ph - g_ph * S->wd_th);
+            g_dbg_ap = ap; g_dbg_acc = 3; g_dbg_sw = Dm;
+            *alpha_out = ap; *az_out = az;
+            return 1;
+        }
+        if (isfinite(pht) && ++S->wd_trial <= WD_TRIAL_MAX) {
+            /* watchdog step: the full step is taken anyway; the filter gets the stored reference */
+            add_filter(&S->F, (1.0 - g_th) * S->wd_th, S->wd_ph - g_ph * S->wd_th);
+            g_dbg_ap = ap; g_dbg_acc = 4; g_dbg_sw = Dm;
+            *alpha_out = ap; *az_out = az;
+            return 1;
+        }
+        /* StopWatchDog: back to the stored iterate and direction; backtrack from there without the full step */
+        wd_save(W, 1);
+        S->wd_on = 0;
+        S->wd_short = 0;
+        th0 = S->wd_th; phi0 = S->wd_ph; Dm = S->wd_Dm; ap = S->wd_alpha;
+        az = ftb_dual(W, tau);
+        skip_first = 1;
+    }
     double amin;
     if (Dm < 0.0) {
         amin = fmin(g_th, g_ph * th0 / (-Dm));
@@ -1773,24 +1927,15 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double th0, double ph
         amin = g_th;
     }
     amin *= g_al;
-    const double tolc = 10.0 * DBL_EPSILON;
     double alpha = ap;
-    int accepted = rel < 1e-15, ftype = 0;
-    const int rs = W->R == M_RESTO;
-    const size_t nx_ = 6 * (size_t)(W->N + 1), nu_ = 2 * (size_t)W->N, nw_ = 8 * (size_t)W->nb, ns_ = 4 * (size_t)W->nb;
-    const size_t nr_ = (size_t)W->nrow;
-    double tht = 0.0, pht = 0.0;
+    accepted = rel < 1e-15;
     for (int ls = 0; !accepted; ++ls) {
-        set_trial(W, alpha);
-        trial_eval(W, mu, &tht, &pht);
-        const int sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
-        int ok = 0;
-        if (isfinite(pht) && tht <= S->th_max && !in_filter(&S->F, tht, pht)) {
-            if (th0 <= S->th_min && sw) { ftype = 1; ok = pht - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
-            else { ftype = 0; ok = tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
+        if (!(ls == 0 && skip_first)) {
+            set_trial(W, alpha);
+            trial_eval(W, mu, &tht, &pht);
+            if (acceptable(S, tht, pht, th0, phi0, Dm, alpha, &ftype)) { accepted = 1; break; }
         }
-        if (ok) { accepted = 1; break; }
-        if (ls == 0 && isfinite(pht) && tht >= th0) {
+        if (ls == 0 && !skip_first && isfinite(pht) && tht >= th0) {
             /* second-order corrections (IPOPT max_soc 4, kappa_soc 0.99) */
             double* o = W->sv;
             memcpy(o, W->dx, nx_ * 8); o += nx_; memcpy(o, W->du, nu_ * 8); o += nu_;
@@ -1814,12 +1959,9 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double th0, double ph
                 a_soc = ftb_primal(W, tau);
                 set_trial(W, a_soc);
                 trial_eval(W, mu, &tht, &pht);
-                int ok2 = 0;
-                if (isfinite(pht) && tht <= S->th_max && !in_filter(&S->F, tht, pht)) {
-                    if (th0 <= S->th_min && sw) { ftype = 1; ok2 = pht - (phi0 + eta_ph * alpha * Dm) <= tolc * fabs(phi0); }
-                    else { ftype = 0; ok2 = tht <= (1.0 - g_th) * th0 || pht - (phi0 - g_ph * th0) <= tolc * fabs(phi0); }
-                }
-                if (ok2) { soc_ok = 1; break; }
+                /* the acceptance test of a corrected step uses the uncorrected alpha in the Armijo term */
+                int ft2 = 0;
+                if (acceptable(S, tht, pht, th0, phi0, Dm, alpha, &ft2)) { soc_ok = 1; ftype = ft2; break; }
                 if (!isfinite(pht)) break;
             }
             if (soc_ok) {
@@ -1838,8 +1980,22 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double th0, double ph
         }
         if (alpha * 0.5 < amin) break;
         alpha *= 0.5;
+        ++nsteps;
     }
     if (accepted && !ftype) add_filter(&S->F, (1.0 - g_th) * th0, phi0 - g_ph * th0);
+    if (accepted) S->wd_short = nsteps > 0 ? S->wd_short + 1 : 0;
+    g_dbg_ap = ap; g_dbg_acc = accepted; g_dbg_sw = Dm;
+    if (getenv("TTO_DEBUG")) {
+        double c[7];
+        ftb_classes(W, tau, c);
+        fprintf(stderr, "     ftb x %.1e u %.1e w %.1e s %.1e sf %.1e p %.1e n %.1e\n", c[0], c[1], c[2], c[3], c[4], c[5], c[6]);
+    }
+    if (skip_first) {
+        /* the iterate is the watchdog's stored one: re-linearise it for the caller */
+        linearise(W);
+        *th0p = th0;
+        *phi0p = phi0;
+    }
     *alpha_out = alpha;
     *az_out = az;
     return accepted != 0;
@@ -1864,6 +2020,7 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     W->R = M_ORIG;
     W->lsq = 0;
     W->have_acc = 0;
+    W->kd = (P->opts & TTO_OPT_KAPPA_D) ? KAPPA_D : 0.0;
     const int dbg = getenv("TTO_DEBUG") != NULL;
     const int use_resto = !(P->opts & TTO_OPT_NO_RESTO), use_soft = !(P->opts & TTO_OPT_NO_SOFT_RESTO);
     /* weights, bounds (bound_relax_factor 1e-8 on every finite bound) */
@@ -2009,8 +2166,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         }
         const double mu = S->mu;
         int bad = 0;
-        const double th0 = infeas1(W, W->rc0, W->rd0, W->rf0);
-        const double phi0 = (W->R == M_RESTO ? resto_obj(W, W->x, W->u, W->w, W->pr, W->nr) : cost_eval(W, W->x, W->u)) +
+        double th0 = infeas1(W, W->rc0, W->rd0, W->rf0);
+        double phi0 = (W->R == M_RESTO ? resto_obj(W, W->x, W->u, W->w, W->pr, W->nr) : cost_eval(W, W->x, W->u)) +
                             barrier(W, W->x, W->u, W->w, W->s, W->sf, W->R == M_RESTO ? W->pr : NULL,
                                     W->R == M_RESTO ? W->nr : NULL, mu, &bad);
         double dw = 0.0, alpha = 0.0, az = 0.0;
@@ -2023,7 +2180,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         if (W->R == M_ORIG && in_soft) {
             accepted = 0; /* handled below as a soft restoration step */
         } else {
-            accepted = line_search(W, S, (W->R == M_RESTO ? iter == resto_iter0 : iter == 0), th0, phi0, &alpha, &az);
+            accepted = line_search(W, S, (W->R == M_RESTO ? iter == resto_iter0 : iter == 0), &th0, &phi0, &alpha, &az);
+            if (!accepted) oe = opt_error(W, mu); /* a stopped watchdog may have restored its stored iterate */
         }
         if (!accepted && W->R == M_ORIG && use_soft && (in_soft ? ++soft_cnt <= MAX_SOFT_RESTO : 1)) {
             /* soft restoration step (BacktrackingLineSearch::TrySoftRestoStep): primal and dual step
@@ -2098,7 +2256,7 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
             --iter; /* entering is not an iteration */
             continue;
         }
-        if (dbg) fprintf(stderr, "     alpha %.3e az %.3e dw %.2e th %.3e nf %d\n", alpha, az, dw, th0, S->F.n);
+        if (dbg) fprintf(stderr, "     alpha %.3e (ap %.3e acc %d Dm %.2e) az %.3e dw %.2e th %.3e nf %d\n", alpha, g_dbg_ap, g_dbg_acc, g_dbg_sw, az, dw, th0, S->F.n);
         take_step(W, mu, alpha, az);
     }
     if (W->R == M_RESTO) W->R = M_ORIG;

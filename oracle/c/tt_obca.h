@@ -44,6 +44,10 @@ typedef struct {
 #define TTO_OPT_NO_RESTO 1       /* no restoration phase: a failed line search takes its last trial step */
 #define TTO_OPT_NO_SOFT_RESTO 2  /* no soft restoration phase */
 #define TTO_OPT_NO_LSQ_MULT 4    /* constraint multipliers start at 0 instead of the least-squares estimate */
+/* opt-in IPOPT features restated in the oracle only (A/B on the C4 census: 57/64 converged with and without
+ * them); the GPU kernel does not run them, so GPU-vs-oracle parity uses opts without these bits */
+#define TTO_OPT_KAPPA_D 8        /* kappa_d = 1e-5 linear damping of variables / slacks with one finite bound */
+#define TTO_OPT_WATCHDOG 16      /* watchdog (trigger 10 shortened steps, 3 trial iterations) in the line search */
 
 /* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).
  * z_guess (n) or NULL (plan: _generate_initial_trajectory_guess 209-225; track: reference copy +

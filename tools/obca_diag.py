@@ -1,9 +1,11 @@
 """CPU-oracle convergence census of an OBCA bench workload (development check, no GPU).
 
     python tools/obca_diag.py c4|cobs|c4replan LO HI [max_iter] [out.npz]
+$TTO_OPTS: oracle TTO_OPT_* bits (switch IPOPT features off for A/B runs).
 Solves instances LO..HI-1 of the bench's seed-0 batch with the C oracle (8 threads) and prints status /
 iteration counts, so solver changes can be judged on the instances the bench actually runs."""
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -45,7 +47,7 @@ def main():
     max_iter = int(sys.argv[4]) if len(sys.argv) > 4 else 5000
     P, data = workload(cfg)
     prob = co.make_obca_problem(P["N"], P["params"], sc.OBCA_Q, sc.OBCA_R, *P["bnd"], P["obs"], mode=P["mode"],
-                                max_iter=max_iter)
+                                max_iter=max_iter, opts=int(os.environ.get("TTO_OPTS", "0")))
     sl = {k: v[lo:hi] for k, v in data.items()}
     t = time.time()
     z, st, it, kk = co.obca_solve_batch(prob, **sl, nthreads=8)
