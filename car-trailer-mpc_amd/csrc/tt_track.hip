@@ -1206,6 +1206,77 @@ __device__ __forceinline__ void phase_load(const Ctx<BM>& c, const TrackArgs& a,
     __syncthreads();
 }
 
+// Stage-unrolled builds with a specialised bound pattern and the reference-copy guess: the lane of a stage
+// already holds its reference row (rc0..rc7, read at kernel entry), so the guess, the bound push, z = 1 and
+// y = 0 are written straight from registers -- one global round trip before the first linearisation
+// instead of two.  Same values as phase_load + phase_init (an infeasible x_init keeps the unpushed copy).
+template <int BM>
+__device__ __forceinline__ void phase_load_init_reg(const Ctx<BM>& c, const TrackArgs& a, int b) {
+    const int lane = c.lane, N = c.N;
+    if (lane < 8) {
+        const int v = lane;
+        const double l = v < 6 ? a.xlb[v] : a.ulb[v - 6];
+        const double u = v < 6 ? a.xub[v] : a.uub[v - 6];
+        const bool hl = isfinite(l) && l > -1e19, hu = isfinite(u) && u < 1e19;
+        c.h(hLB + v) = hl ? l - 1e-8 * fmax(1.0, fabs(l)) : -INFINITY;
+        c.h(hUB + v) = hu ? u + 1e-8 * fmax(1.0, fabs(u)) : INFINITY;
+    }
+    const double* wq = a.wqwr ? a.wqwr + (size_t)b * 8 : nullptr;
+    if (lane < 36) {
+        const int i = lane / 6, j = lane % 6;
+        const double q = 0.5 * (a.Q[i * 6 + j] + a.Q[j * 6 + i]);
+        c.h(hQW + lane) = wq ? q * wq[i] * wq[j] : q;
+    } else if (lane < 40) {
+        const int e = lane - 36, i = e / 2, j = e % 2;
+        const double r = 0.5 * (a.R[i * 2 + j] + a.R[j * 2 + i]);
+        c.h(hRW + e) = wq ? r * wq[6 + i] * wq[6 + j] : r;
+    } else if (lane < 46) {
+        c.h(hXI + lane - 40) = a.x0[(size_t)b * 6 + (lane - 40)];
+    }
+    // relaxed bounds (the head's values) and the infeasibility test of the kernel, evaluated per lane
+    double lr[8], ur[8];
+    bool infeas = false;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+        const double l = v < 6 ? a.xlb[v] : a.ulb[v - 6], u = v < 6 ? a.xub[v] : a.uub[v - 6];
+        lr[v] = l - 1e-8 * fmax(1.0, fabs(l));
+        ur[v] = u + 1e-8 * fmax(1.0, fabs(u));
+        if (v < 6) {
+            const double xi = a.x0[(size_t)b * 6 + v];
+            if (!isfinite(xi) || (c.hl(v) && xi < lr[v]) || (c.hu(v) && xi > ur[v])) infeas = true;
+        }
+    }
+    const int k = c.k0(), part = c.part();
+    if (k <= N) {
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            if (c.pair && (v >> 2) != part) continue;  // lane pairs: rows 0-3 on the even lane, 4-7 on the odd
+            if (v >= 6 && k == N) continue;
+            double z = c.rcv(v);
+            if (!infeas) {
+                const double l = lr[v], u = ur[v];
+                if (c.hl(v) && c.hu(v)) {
+                    const double pl = fmin(1e-2 * fmax(1.0, fabs(l)), 1e-2 * (u - l));
+                    const double pu = fmin(1e-2 * fmax(1.0, fabs(u)), 1e-2 * (u - l));
+                    z = fmin(fmax(z, l + pl), u - pu);
+                } else if (c.hl(v)) {
+                    z = fmax(z, l + 1e-2 * fmax(1.0, fabs(l)));
+                } else if (c.hu(v)) {
+                    z = fmin(z, u - 1e-2 * fmax(1.0, fabs(u)));
+                }
+                c.r(rZL + v, k) = c.hl(v) ? 1.0 : 0.0;
+                c.r(rZU + v, k) = c.hu(v) ? 1.0 : 0.0;
+            }
+            c.r(rX + v, k) = z;
+        }
+        if (!infeas) {
+            if (!c.pair || part == 0) { c.r(rY + 0, k) = 0.0; c.r(rY + 1, k) = 0.0; c.r(rY + 2, k) = 0.0; c.r(PAD, k) = 0.0; }
+            if (!c.pair || part == 1) { c.r(rY + 3, k) = 0.0; c.r(rY + 4, k) = 0.0; c.r(rY + 5, k) = 0.0; }
+        }
+    }
+    __syncthreads();
+}
+
 // bound push (IPOPT bound_push / bound_frac = 1e-2), z_L = z_U = 1, y = 0, zero pad row
 template <int BM>
 __device__ __forceinline__ void phase_init(const Ctx<BM>& c) {
@@ -1277,7 +1348,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
     Stamps stamps;
     stamps.begin();
 #endif
-    phase_load(c, a, b);
+    const bool fused = BM >= 0 && c.regref && !a.zg;
+    if (fused) phase_load_init_reg(c, a, b);
+    else phase_load(c, a, b);
     int nbx = 0, nbu = 0;
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
@@ -1295,17 +1368,22 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
     int status = infeas ? 3 : 2, iter = 0;
     double E0 = INFINITY;
     if (!infeas) {
-        phase_init(c);
+        if (!fused) phase_init(c);
         STAMP(PH_LOAD);
         double dw_last = 0.0, th_max = 0.0, th_min = 0.0;
         int acc_count = 0, nf = 0;
+        // launch constants of the optimality-error scaling and the barrier floor: no IEEE division per iteration
+        const double inv_m = 1.0 / (double)(6 * (N + 1) + nb), inv_nb = nb ? 1.0 / (double)nb : 0.0;
+        const double mu_floor = a.tol / 10.0, mu_floor_test = mu_floor * 1.0000001;
         for (iter = 0;; ++iter) {
             const Lin e = phase_linearize(c);
             STAMP(PH_LIN);
             if (!isfinite(e.dinf) || !isfinite(e.pinf)) { status = 4; break; }
-            const double sd = fmax(100.0, (e.sy + e.sz) / (double)(6 * (N + 1) + nb)) / 100.0;
-            const double sc = nb ? fmax(100.0, e.sz / (double)nb) / 100.0 : 1.0;
-            E0 = fmax(fmax(e.dinf / sd, e.pinf), e.c0() / sc);
+            // IPOPT's s_d, s_c (s_max = 100) as reciprocals: E = max(dinf / s_d, pinf, compl / s_c)
+            const double isd = 100.0 * frcp(fmax(100.0, (e.sy + e.sz) * inv_m));
+            const double isc = nb ? 100.0 * frcp(fmax(100.0, e.sz * inv_nb)) : 1.0;
+            const double dsc = e.dinf * isd;
+            E0 = fmax(fmax(dsc, e.pinf), e.c0() * isc);
             if (E0 <= a.tol) { status = 0; break; }
             if (E0 <= a.acc_tol) {
                 if (++acc_count >= a.acc_iter) { status = 1; break; }
@@ -1316,9 +1394,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             // barrier parameter (monotone Fiacco-McCormick)
             double cmu = e.cmu(c.mu);
             for (;;) {
-                const double Emu = fmax(fmax(e.dinf / sd, e.pinf), cmu / sc);
-                if (!(Emu <= 10.0 * c.mu && c.mu > a.tol / 10.0 * 1.0000001)) break;
-                c.mu = fmax(a.tol / 10.0, fmin(0.2 * c.mu, c.mu * sqrt(c.mu)));
+                const double Emu = fmax(fmax(dsc, e.pinf), cmu * isc);
+                if (!(Emu <= 10.0 * c.mu && c.mu > mu_floor_test)) break;
+                c.mu = fmax(mu_floor, fmin(0.2 * c.mu, c.mu * sqrt(c.mu)));
                 c.tau = fmax(0.99, 1.0 - c.mu);
                 nf = 0;  // IPOPT resets the filter on every barrier update
                 cmu = e.cmu(c.mu);
