@@ -104,6 +104,7 @@ typedef struct {
     double rf0[6];
     /* factorisation */
     double *Dd, *Ed, *L, *V, *Qt, *Rt, *Pm, *G, *H, *K;
+    double* Sg;     /* signs of the block LDL' pivots: 8 of A, 4 of T per block (all +1 unless indefinite) */
     double Dsf[6], Dfe[6];
     double *Sd, *Mch, *Ptl, *ptl; /* soft dynamics rows (restoration) */
     /* rhs + step */
@@ -317,7 +318,7 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->gw, nb * 8); TAKE(W->Wd, N * 36);
     TAKE(W->Jx, nb * 16); TAKE(W->Jw, nb * 32); TAKE(W->Hxx, nb * 16); TAKE(W->Hxw, nb * 32); TAKE(W->Hww, nb * 16);
     TAKE(W->rc0, N1 * 6); TAKE(W->rd0, nb * 4);
-    TAKE(W->Dd, nb * 4); TAKE(W->Ed, nb * 4); TAKE(W->L, nb * 64); TAKE(W->V, nb * 32); TAKE(W->Qt, N1 * 36);
+    TAKE(W->Dd, nb * 4); TAKE(W->Ed, nb * 4); TAKE(W->Sg, nb * 12); TAKE(W->L, nb * 64); TAKE(W->V, nb * 32); TAKE(W->Qt, N1 * 36);
     TAKE(W->Rt, N * 4);
     TAKE(W->Pm, N1 * 36); TAKE(W->G, N * 4); TAKE(W->H, N * 12); TAKE(W->K, N * 12);
     TAKE(W->Sd, N1 * 6); TAKE(W->Mch, N1 * 36); TAKE(W->Ptl, N1 * 36); TAKE(W->ptl, N1 * 6);
@@ -510,6 +511,28 @@ static int chol(double* a, int n) { /* in-place lower Cholesky, row-major n x n;
     }
     return 0;
 }
+/* signed Cholesky A = L S L' (S = diag(+-1), L_jj = sqrt|d_j|), no pivoting; identical to chol() on a
+ * positive definite matrix (IPOPT's inertia test needs the signs, not definiteness).  Returns the number of negative pivots, -1 on a (numerically) zero pivot. */
+static int schol(double* a, int n, double* S) {
+    int neg = 0;
+    for (int j = 0; j < n; ++j) {
+        const double ajj = a[j * n + j];
+        double s = ajj;
+        for (int k = 0; k < j; ++k) s -= a[j * n + k] * a[j * n + k] * S[k];
+        /* a positive pivot is taken as chol() takes it; a negative one only when it is not numerically zero */
+        if (!(s > 0.0) && !(s < -1e-14 * fabs(ajj))) return -1;
+        S[j] = s > 0.0 ? 1.0 : -1.0;
+        neg += s < 0.0;
+        const double r = sqrt(fabs(s));
+        a[j * n + j] = r;
+        for (int i = j + 1; i < n; ++i) {
+            double t = a[i * n + j];
+            for (int k = 0; k < j; ++k) t -= a[i * n + k] * S[k] * a[j * n + k];
+            a[i * n + j] = t / (S[j] * r);
+        }
+    }
+    return neg;
+}
 static void fsub(const double* L, int n, double* b) { /* b <- L^-1 b */
     for (int i = 0; i < n; ++i) {
         double t = b[i];
@@ -614,7 +637,11 @@ static void linearise(ws_t* W) {
  * G = Y'Z - b2, the Schur complement onto dx^ is
  *     W_xx - Z'Z + G' T^-1 G
  * which never forms C' D C: with D ~ 1e10 on the near-equality range rows that product cancels
- * catastrophically, while T stays well conditioned.  Inertia: A must be positive definite. */
+ * catastrophically, while T stays well conditioned.  Inertia (IPOPT tests the whole KKT matrix): by
+ * Haynsworth In(M) = In(A) + In(-T), so the block has the correct inertia (8, 4, 0) iff T has exactly as many
+ * negative pivots as A; both are factored by the signed Cholesky A = L S_A L', T = L_T S_T L_T', and every
+ * A^-1 / T^-1 carries its sign vector.  That exact test is an opt-in (TTO_OPT_BLOCK_INERTIA); the
+ * default, which the GPU kernel runs, asks for A positive definite (S = I), a sufficient condition. */
 static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     const double *Jx = W->Jx + 16 * bi, *Jw = W->Jw + 32 * bi;
     double* D = W->Dd + 4 * bi;
@@ -637,7 +664,17 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
         Lb[e * 8 + e] += W->zw[8 * bi + e] / (W->w[8 * bi + e] + RELAX) + dw;
         if (W->R == M_RESTO) Lb[e * 8 + e] += W->zeta * W->dRw[8 * bi + e];
     }
-    if (chol(Lb, 8) != 0) return 1;
+    double* SA = W->Sg + 12 * bi;
+    double* ST = SA + 8;
+    const int inert = (W->P->opts & TTO_OPT_BLOCK_INERTIA) != 0;
+    int negA = 0;
+    if (inert) {
+        negA = schol(Lb, 8, SA);
+        if (negA < 0) return 1;
+    } else {
+        if (chol(Lb, 8) != 0) return 1;
+        for (int e = 0; e < 8; ++e) SA[e] = 1.0;
+    }
     double *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *LT = W->LT + 16 * bi, *Gm = W->Gm + 16 * bi;
     for (int r = 0; r < 4; ++r) {
         double col[8];
@@ -654,23 +691,31 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     for (int r = 0; r < 4; ++r)
         for (int c = 0; c < 4; ++c) {
             double t = (r == c) ? E[r] : 0.0, g = -Jx[r * 4 + c];
-            for (int a = 0; a < 8; ++a) { t += Yb[a * 4 + r] * Yb[a * 4 + c]; g += Yb[a * 4 + r] * Zb[a * 4 + c]; }
+            for (int a = 0; a < 8; ++a) { t += Yb[a * 4 + r] * SA[a] * Yb[a * 4 + c]; g += Yb[a * 4 + r] * SA[a] * Zb[a * 4 + c]; }
             LT[r * 4 + c] = t;
             Gm[r * 4 + c] = g;
         }
-    if (chol(LT, 4) != 0) return 1;
+    if (inert) {
+        /* inertia of the block [[A, C'], [C, -E]] = In(A) + In(-T): (8, 4, 0) iff T has as many negative
+         * pivots as A (Haynsworth); the stage Riccati then tests the Schur complement onto dx^ */
+        if (schol(LT, 4, ST) != negA) return 1;
+    } else {
+        if (chol(LT, 4) != 0) return 1;
+        for (int r = 0; r < 4; ++r) ST[r] = 1.0;
+    }
     /* Q += W_xx - Z'Z + G' T^-1 G   (T^-1 G via two triangular solves per column) */
     double TG[16];
     for (int c = 0; c < 4; ++c) {
         double col[4] = {Gm[0 * 4 + c], Gm[1 * 4 + c], Gm[2 * 4 + c], Gm[3 * 4 + c]};
         fsub(LT, 4, col);
+        for (int r = 0; r < 4; ++r) col[r] *= ST[r];
         bsub(LT, 4, col);
         for (int r = 0; r < 4; ++r) TG[r * 4 + c] = col[r];
     }
     for (int p = 0; p < 4; ++p)
         for (int q = 0; q < 4; ++q) {
             double t = W->lsq ? 0.0 : W->Hxx[16 * bi + p * 4 + q];
-            for (int a = 0; a < 8; ++a) t -= Zb[a * 4 + p] * Zb[a * 4 + q];
+            for (int a = 0; a < 8; ++a) t -= Zb[a * 4 + p] * SA[a] * Zb[a * 4 + q];
             for (int r = 0; r < 4; ++r) t += Gm[r * 4 + p] * TG[r * 4 + q];
             Q[p * 6 + q] += t;
         }
@@ -845,18 +890,20 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
                 rd[r] = dres[4 * bi + r] + bgrad_s(W, bi, r, mu) / D[r] + (rs ? W->gpn[W->nrc + 4 * bi + r] : 0.0);
             double* zf = W->vv + 8 * bi;
             for (int a = 0; a < 8; ++a) zf[a] = bgrad_w(W, 8 * bi + a, mu);
+            const double *SA = W->Sg + 12 * bi, *ST = SA + 8;
             fsub(W->L + 64 * bi, 8, zf);
             double* t = W->tv + 4 * bi;
             for (int r = 0; r < 4; ++r) {
                 double h = rd[r];
-                for (int a = 0; a < 8; ++a) h -= Yb[a * 4 + r] * zf[a];
+                for (int a = 0; a < 8; ++a) h -= Yb[a * 4 + r] * SA[a] * zf[a];
                 t[r] = h;
             }
             fsub(W->LT + 16 * bi, 4, t);
+            for (int r = 0; r < 4; ++r) t[r] *= ST[r];
             bsub(W->LT + 16 * bi, 4, t);
             for (int p = 0; p < 4; ++p) {
                 double g = 0.0;
-                for (int a = 0; a < 8; ++a) g -= Zb[a * 4 + p] * zf[a];
+                for (int a = 0; a < 8; ++a) g -= Zb[a * 4 + p] * SA[a] * zf[a];
                 for (int r = 0; r < 4; ++r) g -= Gm[r * 4 + p] * t[r];
                 q[p] += g;
             }
@@ -953,6 +1000,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             const int bi = k * W->nbk + j;
             const double *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *Gm = W->Gm + 16 * bi, *dxk = W->dx + 6 * k;
             const double* D = W->Dd + 4 * bi;
+            const double *SA = W->Sg + 12 * bi, *ST = SA + 8;
             double g4[4];
             for (int r = 0; r < 4; ++r) {
                 double t = 0.0;
@@ -960,6 +1008,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
                 g4[r] = t;
             }
             fsub(W->LT + 16 * bi, 4, g4);
+            for (int r = 0; r < 4; ++r) g4[r] *= ST[r];
             bsub(W->LT + 16 * bi, 4, g4);
             double* yp = W->ydp + 4 * bi;
             for (int r = 0; r < 4; ++r) yp[r] = W->tv[4 * bi + r] - g4[r];
@@ -968,7 +1017,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
                 double t = W->vv[8 * bi + a];
                 for (int q = 0; q < 4; ++q) t += Zb[a * 4 + q] * dxk[q];
                 for (int r = 0; r < 4; ++r) t += Yb[a * 4 + r] * yp[r];
-                t8[a] = t;
+                t8[a] = SA[a] * t;
             }
             bsub(W->L + 64 * bi, 8, t8);
             for (int a = 0; a < 8; ++a) W->dw[8 * bi + a] = -t8[a];

@@ -48,6 +48,7 @@ typedef struct {
  * them); the GPU kernel does not run them, so GPU-vs-oracle parity uses opts without these bits */
 #define TTO_OPT_KAPPA_D 8        /* kappa_d = 1e-5 linear damping of variables / slacks with one finite bound */
 #define TTO_OPT_WATCHDOG 16      /* watchdog (trigger 10 shortened steps, 3 trial iterations) in the line search */
+#define TTO_OPT_BLOCK_INERTIA 32 /* exact block inertia In(A) + In(-T) = (8, 4, 0) by signed LDL' instead of A positive definite */
 
 /* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).
  * z_guess (n) or NULL (plan: _generate_initial_trajectory_guess 209-225; track: reference copy +

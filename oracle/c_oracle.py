@@ -106,8 +106,8 @@ os.environ.setdefault("OMP_PROC_BIND", "false")
 # ------------------------------------------------------------------------------------------------
 MAXM = 16
 OBCA_PLAN, OBCA_TRACK = 0, 1
-# oracle-only opt-in IPOPT features (tt_obca.h): kappa_d damping, line-search watchdog
-OPT_KAPPA_D, OPT_WATCHDOG = 8, 16
+# oracle-only opt-in IPOPT features (tt_obca.h): kappa_d damping, line-search watchdog, exact block inertia test
+OPT_KAPPA_D, OPT_WATCHDOG, OPT_BLOCK_INERTIA = 8, 16, 32
 
 
 class TTOObcaProblem(C.Structure):
