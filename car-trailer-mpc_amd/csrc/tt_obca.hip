@@ -1199,7 +1199,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
     const int i = act ? lane / 6 : 0, j = act ? lane % 6 : 0, r = vec ? lane - 48 : 0;
     const int ii = min(i, j), jj = max(i, j), sij = sy6(ii, jj);
     const ColMask mj(j), mi(ii), mr(r);
-    __shared__ double Pt[48], Mt[48], Yt[48], Tt[48];
+    __shared__ double Pt[48], Yt[48], Tt[48];
     if (act) {
         const double q = src.QT(sij, N);
         Pt[8 * i + j] = q;
@@ -1211,25 +1211,23 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
     lds_order();
     auto stage = [&](int k, const SoftOps& cur, SoftOps& nx) __attribute__((always_inline)) {
         if (k > 0) soft_ops(src, k - 1, i, j, sij, r, vec, nx);  // next stage's operands, one stage ahead
-        // ---- soften stage k
-        if (act) Mt[8 * i + j] = (i == j ? 1.0 : 0.0) + cur.si * Pt[8 * ii + jj] * cur.sj;
-        lds_order();
+        // ---- soften stage k: M = I + S P S inverted by Gauss-Jordan in registers (lane 6i + j holds M[i][j]);
+        // each pivot arrives by v_readlane, its row and column entries by ds_bpermute, so no LDS write / read
+        // round trip sits on the six-pivot chain (same arithmetic as an LDS tile)
+        double mv = act ? (i == j ? 1.0 : 0.0) + cur.si * Pt[8 * ii + jj] * cur.sj : 0.0;
 #pragma unroll
         for (int p = 0; p < 6; ++p) {
-            const double piv = Mt[8 * p + p];
-            double nv = 0.0;
-            if (act) {
-                const double aip = Mt[8 * i + p], apj = Mt[8 * p + j], aij = Mt[8 * i + j], ip = 1.0 / piv;
-                nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : aij - aip * apj * ip;
-            }
+            const double piv = readlane_d(mv, 7 * p);
+            const double aip = __shfl(mv, 6 * i + p), apj = __shfl(mv, 6 * p + j);
+            const double ip = 1.0 / piv;
+            const double nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : mv - aip * apj * ip;
             fail = fail || !(piv > 0.0);
-            lds_order();
-            if (act) Mt[8 * i + j] = nv;
-            lds_order();
+            mv = act ? nv : 0.0;
         }
+        const double mji = __shfl(mv, 6 * j + i);
         if (act) {
             // Y = S M^-1 S from the upper entry (symmetric by construction)
-            const double y = i <= j ? cur.si * Mt[8 * i + j] * cur.sj : cur.sj * Mt[8 * j + i] * cur.si;
+            const double y = i <= j ? cur.si * mv * cur.sj : cur.sj * mji * cur.si;
             Yt[8 * i + j] = y;
             if (i <= j) c.S(S_Y + sij, k) = y;
         }
