@@ -199,6 +199,7 @@ struct Ctx {
     LArgs* a;
     gdouble* ws;
     double* lds;  // dynamic LDS for the staged sweeps, or nullptr (sweeps read the HBM workspace)
+    __attribute__((address_space(3))) double* slab;  // block-phase slabs (dynamic LDS, kSlab x T; thread t at slab + t)
     int N, NP, nbk, tid, b;
     double dt;
     double xl[6], xu[6], ul[2], uu[2];
@@ -316,7 +317,17 @@ __device__ __forceinline__ void blk_vals(LArgs& a, const double* xk, const Trig&
 }
 
 // Full block linearisation + elimination.  See the header comment and oracle/c/tt_obca.c:block_factor.
+typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: ds_read / ds_write
+
+// per-thread LDS slab of the block phases: the 48 doubles of Yl, Zl, G (field stride T, conflict-free).  Kept in
+// registers they were what the block elimination spilled to scratch, and every scratch reload waited behind
+// the factor-record stores (one in-order vmcnt); ds_ reads wait on lgkmcnt only.
+constexpr int kSlab = 48;
 struct Blk {
+    lds_double* m;                   // this thread's slab (Yl 0-15 | Zl 16-31 | G 32-47)
+    __device__ __forceinline__ lds_double& Yl(int a, int r) const { return m[(a * 4 + r) * T]; }  // L^-1 Jw_lam'  [a][r]
+    __device__ __forceinline__ lds_double& Zl(int a, int q) const { return m[(16 + a * 4 + q) * T]; }  // L^-1 W_lam x  [a][q]
+    __device__ __forceinline__ lds_double& G(int r, int q) const { return m[(32 + r * 4 + q) * T]; }  // Y_lam' Z - Jx  [r][q]
     // linearisation
     double d[4];
     double jx0[4], e2, e3, angp;     // Jx rows 0..2 (row 3 = 0)
@@ -327,10 +338,7 @@ struct Blk {
     // elimination
     double idm[4];                   // 1 / (Sigma_mu + dw) (mu block is diagonal)
     double LL[10];                   // chol of the lam block (1/L_ii on the diagonal)
-    double Yl[4][4];                 // L^-1 Jw_lam'  [a][r]
-    double Zl[4][4];                 // L^-1 W_lam x  [a][q]
     double LT[10];                   // chol of T (1/L_ii on the diagonal)
-    double G[4][4];                  // Y_lam' Z - Jx  [r][q]
     double D[4];                     // Sigma_s + dw of the 4 slacks
     double E[4];                     // E of the 4 rows: 1/D (+ 1/D_p + 1/D_n in the restoration phase)
 };
@@ -461,7 +469,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int a = 0; a < 4; ++a) col[a] = jwl(k, r, a);
         fsub4(k.LL, col);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) k.Yl[a][r] = col[a];
+        for (int a = 0; a < 4; ++a) k.Yl(a, r) = col[a];
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -470,7 +478,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int a = 0; a < 4; ++a) col[a] = k.hxl[q][a];
         fsub4(k.LL, col);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) k.Zl[a][q] = col[a];
+        for (int a = 0; a < 4; ++a) k.Zl(a, q) = col[a];
     }
     const double* idm = k.idm;
 #pragma unroll
@@ -479,7 +487,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int s = 0; s <= r; ++s) {
             double t = (r == s) ? k.E[r] : 0.0;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) t += jwm(k, r, a) * jwm(k, s, a) * idm[a] + k.Yl[a][r] * k.Yl[a][s];
+            for (int a = 0; a < 4; ++a) t += jwm(k, r, a) * jwm(k, s, a) * idm[a] + k.Yl(a, r) * k.Yl(a, s);
             k.LT[lo4(r, s)] = t;
         }
 #pragma unroll
@@ -488,14 +496,14 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int q = 0; q < 4; ++q) {
             double g = -jx(k, r, q);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) g += k.Yl[a][r] * k.Zl[a][q];
-            k.G[r][q] = g;
+            for (int a = 0; a < 4; ++a) g += k.Yl(a, r) * k.Zl(a, q);
+            k.G(r, q) = g;
         }
     if (!chol4(k.LT)) return false;
     double Wm[4][4];  // LT^-1 G
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        double col[4] = {k.G[0][q], k.G[1][q], k.G[2][q], k.G[3][q]};
+        double col[4] = {k.G(0, q), k.G(1, q), k.G(2, q), k.G(3, q)};
         fsub4(k.LT, col);
 #pragma unroll
         for (int r = 0; r < 4; ++r) Wm[r][q] = col[r];
@@ -507,7 +515,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int q = 0; q <= p; ++q) {
             double t = hxx[p][q];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) t += Wm[a][p] * Wm[a][q] - k.Zl[a][p] * k.Zl[a][q];
+            for (int a = 0; a < 4; ++a) t += Wm[a][p] * Wm[a][q] - k.Zl(a, p) * k.Zl(a, q);
             C[lo4(p, q)] += t;
         }
     return true;
@@ -527,7 +535,7 @@ __device__ __forceinline__ void blk_rhs(const Blk& k, const double* fw, const do
     for (int r = 0; r < 4; ++r) {
         double h = rd[r];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) h -= jwm(k, r, a) * zf[a] + k.Yl[a][r] * zl[a];
+        for (int a = 0; a < 4; ++a) h -= jwm(k, r, a) * zf[a] + k.Yl(a, r) * zl[a];
         t[r] = h;
     }
     fsub4(k.LT, t);
@@ -536,9 +544,9 @@ __device__ __forceinline__ void blk_rhs(const Blk& k, const double* fw, const do
     for (int p = 0; p < 4; ++p) {
         double g = 0.0;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) g -= k.Zl[a][p] * zl[a];
+        for (int a = 0; a < 4; ++a) g -= k.Zl(a, p) * zl[a];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) g -= k.G[r][p] * t[r];
+        for (int r = 0; r < 4; ++r) g -= k.G(r, p) * t[r];
         q4[p] += g;
     }
 }
@@ -551,7 +559,7 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
     for (int r = 0; r < 4; ++r) {
         double s = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s += k.G[r][q] * dxh[q];
+        for (int q = 0; q < 4; ++q) s += k.G(r, q) * dxh[q];
         g4[r] = s;
     }
     fsub4(k.LT, g4);
@@ -570,9 +578,9 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
     for (int a = 0; a < 4; ++a) {
         double s = zf[4 + a];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s += k.Zl[a][q] * dxh[q];
+        for (int q = 0; q < 4; ++q) s += k.Zl(a, q) * dxh[q];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s += k.Yl[a][r] * yp[r];
+        for (int r = 0; r < 4; ++r) s += k.Yl(a, r) * yp[r];
         v[a] = s;
     }
     bsub4(k.LL, v);
@@ -749,13 +757,14 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
         const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
+            bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4];
             if (!block_setup(c, sh, j, k, x, tr, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
             auto st = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) st(FR_G + 4 * r + q, bk.G[r][q]);
+                for (int q = 0; q < 4; ++q) st(FR_G + 4 * r + q, bk.G(r, q));
 #pragma unroll
             for (int i = 0; i < 10; ++i) { st(FR_LT + i, bk.LT[i]); st(FR_LL + i, bk.LL[i]); }
 #pragma unroll
@@ -765,7 +774,7 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
                 st(FR_T + a, t4[a]);
                 st(FR_D + a, bk.D[a]);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { st(FR_ZL + 4 * a + q, bk.Zl[a][q]); st(FR_YL + 4 * a + q, bk.Yl[a][q]); }
+                for (int q = 0; q < 4; ++q) { st(FR_ZL + 4 * a + q, bk.Zl(a, q)); st(FR_YL + 4 * a + q, bk.Yl(a, q)); }
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) st(FR_FW + e, fw[e]);
@@ -893,7 +902,6 @@ struct GSrc {
 };
 // region A per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CR 6  (47);  region B: P 21 | PV 6 | K 12 | KF 2 (41)
 constexpr int LA = 47, LB = 41;
-typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: ds_read / ds_write
 struct LSrc {
     const lds_double* A;
     lds_double* B;
@@ -1513,12 +1521,13 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
             }
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
+            bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4], yp[4], dwv[8];
             auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
 #pragma unroll
             for (int r = 0; r < 4; ++r)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) bk.G[r][q] = ld(FR_G + 4 * r + q);
+                for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
 #pragma unroll
             for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
 #pragma unroll
@@ -1528,7 +1537,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 t4[a] = ld(FR_T + a);
                 bk.D[a] = ld(FR_D + a);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { bk.Zl[a][q] = ld(FR_ZL + 4 * a + q); bk.Yl[a][q] = ld(FR_YL + 4 * a + q); }
+                for (int q = 0; q < 4; ++q) { bk.Zl(a, q) = ld(FR_ZL + 4 * a + q); bk.Yl(a, q) = ld(FR_YL + 4 * a + q); }
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
@@ -2590,6 +2599,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     Ctx c;
     c.a = &a;
     c.lds = obca_lds_bytes(a.N) <= kObcaLdsMax ? dyn_lds : nullptr;
+    c.slab = (__attribute__((address_space(3))) double*)dyn_lds;  // the sweeps' staging area is free then
     c.b = blockIdx.x;
     c.N = a.N;
     c.NP = a.N + 1;
@@ -3045,8 +3055,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
 
 hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream) {
     if (a.B <= 0) return hipSuccess;
-    const size_t need = obca_lds_bytes(a.N);
-    const int bytes = (int)(need <= kObcaLdsMax ? need : 0);
+    const size_t need = obca_lds_bytes(a.N), slab = (size_t)kSlab * T * 8;
+    const int bytes = (int)(need <= kObcaLdsMax ? (need > slab ? need : slab) : slab);
     // the >64 KB dynamic-LDS opt-in is a per-device function attribute: set it on every such launch
     if (bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)obca_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
