@@ -757,7 +757,7 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 
 # commit whose rocprofv3 PMC passes the default C2 / C3 lines quote as roofline.traffic (the kernel has not
 # changed since; re-profile with tools/gpu_track_prof.sh after a kernel change)
-TRAFFIC_COMMIT = "06e88e9"
+TRAFFIC_COMMIT = "fcd2080"
 
 
 def read_traffic(paths):
