@@ -105,6 +105,7 @@ typedef struct {
     /* factorisation */
     double *Dd, *Ed, *L, *V, *Qt, *Rt, *Pm, *G, *H, *K;
     double* Sg;     /* signs of the block LDL' pivots: 8 of A, 4 of T per block (all +1 unless indefinite) */
+    double* alt;    /* 1: the block was eliminated rows-first through M_w = A + Jw' E^-1 Jw (TTO_OPT_BLOCK_MW) */
     double Dsf[6], Dfe[6];
     double *Sd, *Mch, *Ptl, *ptl; /* soft dynamics rows (restoration) */
     /* rhs + step */
@@ -130,6 +131,12 @@ typedef struct {
     /* soft restoration / SOC save area; watchdog save area (iterate + search direction) */
     double* sv;
     double* wdv;
+    /* iterative refinement (IPOPT PDFullSpaceSolver): while ov != NULL the stationarity constants of the
+     * condensed solve come from these arrays (x u w s sf p n) instead of the barrier gradients */
+    double *ov, *ovx, *ovu, *ovw, *ovs, *ovsf, *ovp, *ovn;
+    double *rsx, *rsu, *rsw, *rss, *rssf, *rsp, *rsn, *rrc, *rrd, *rrf; /* residuals of the un-condensed rows */
+    double *sol;    /* refinement save area of the solution */
+    double dw_cur;
     double* mem;
 } ws_t;
 
@@ -318,7 +325,7 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->gw, nb * 8); TAKE(W->Wd, N * 36);
     TAKE(W->Jx, nb * 16); TAKE(W->Jw, nb * 32); TAKE(W->Hxx, nb * 16); TAKE(W->Hxw, nb * 32); TAKE(W->Hww, nb * 16);
     TAKE(W->rc0, N1 * 6); TAKE(W->rd0, nb * 4);
-    TAKE(W->Dd, nb * 4); TAKE(W->Ed, nb * 4); TAKE(W->Sg, nb * 12); TAKE(W->L, nb * 64); TAKE(W->V, nb * 32); TAKE(W->Qt, N1 * 36);
+    TAKE(W->Dd, nb * 4); TAKE(W->Ed, nb * 4); TAKE(W->Sg, nb * 12); TAKE(W->alt, nb); TAKE(W->L, nb * 64); TAKE(W->V, nb * 32); TAKE(W->Qt, N1 * 36);
     TAKE(W->Rt, N * 4);
     TAKE(W->Pm, N1 * 36); TAKE(W->G, N * 4); TAKE(W->H, N * 12); TAKE(W->K, N * 12);
     TAKE(W->Sd, N1 * 6); TAKE(W->Mch, N1 * 36); TAKE(W->Ptl, N1 * 36); TAKE(W->ptl, N1 * 6);
@@ -342,6 +349,11 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->xacc, N1 * 6); TAKE(W->uacc, N * 2); TAKE(W->wacc, nb * 8);
     TAKE(W->sv, 4 * (N1 * 6 + N * 2 + nb * 8 + nb * 4) + 2 * nr + nsv);
     TAKE(W->wdv, 2 * (N1 * 6 * 4 + N * 2 * 3 + nb * 8 * 2 + nb * 4 * 4 + 4 * nr + 24) + 64);
+    TAKE(W->ovx, N1 * 6); TAKE(W->ovu, N * 2); TAKE(W->ovw, nb * 8); TAKE(W->ovs, nb * 4); TAKE(W->ovsf, 6);
+    TAKE(W->ovp, nr); TAKE(W->ovn, nr);
+    TAKE(W->rsx, N1 * 6); TAKE(W->rsu, N * 2); TAKE(W->rsw, nb * 8); TAKE(W->rss, nb * 4); TAKE(W->rssf, 6);
+    TAKE(W->rsp, nr); TAKE(W->rsn, nr); TAKE(W->rrc, N1 * 6); TAKE(W->rrd, nb * 4); TAKE(W->rrf, 6);
+    TAKE(W->sol, N1 * 12 + N * 2 + nb * 16 + 12 + 2 * nr);
 #undef TAKE
     W->mem = (double*)calloc(tot, sizeof(double));
     if (!W->mem) return -1;
@@ -668,7 +680,44 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     double* ST = SA + 8;
     const int inert = (W->P->opts & TTO_OPT_BLOCK_INERTIA) != 0;
     int negA = 0;
-    if (inert) {
+    W->alt[bi] = 0.0;
+    if ((W->P->opts & TTO_OPT_BLOCK_MW) && !W->lsq) {
+        for (int e = 0; e < 8; ++e) SA[e] = 1.0;
+        for (int r = 0; r < 4; ++r) ST[r] = 1.0;
+        double Ab[64];
+        memcpy(Ab, Lb, sizeof(Ab));
+        if (chol(Lb, 8) != 0) {
+            /* A indefinite: the block still has IPOPT's inertia (8, 4, 0) iff M_w = A + Jw' E^-1 Jw > 0;
+             * eliminate the rows first (stable Cholesky of M_w; E^-1 moderate where this happens) */
+            for (int a = 0; a < 8; ++a)
+                for (int b = 0; b < 8; ++b) {
+                    double t = Ab[a * 8 + b];
+                    for (int r = 0; r < 4; ++r) t += Jw[r * 8 + a] * Jw[r * 8 + b] / E[r];
+                    Lb[a * 8 + b] = t;
+                }
+            if (chol(Lb, 8) != 0) return 1;
+            W->alt[bi] = 1.0;
+            double* Zb = W->V + 32 * bi;
+            for (int q = 0; q < 4; ++q) {
+                double col[8];
+                for (int a = 0; a < 8; ++a) {
+                    double t = W->Hxw[32 * bi + q * 8 + a];
+                    for (int r = 0; r < 4; ++r) t += Jw[r * 8 + a] / E[r] * Jx[r * 4 + q];
+                    col[a] = t;
+                }
+                fsub(Lb, 8, col);
+                for (int a = 0; a < 8; ++a) Zb[a * 4 + q] = col[a];
+            }
+            for (int p = 0; p < 4; ++p)
+                for (int q = 0; q < 4; ++q) {
+                    double t = W->Hxx[16 * bi + p * 4 + q];
+                    for (int r = 0; r < 4; ++r) t += Jx[r * 4 + p] / E[r] * Jx[r * 4 + q];
+                    for (int a = 0; a < 8; ++a) t -= Zb[a * 4 + p] * Zb[a * 4 + q];
+                    Q[p * 6 + q] += t;
+                }
+            return 0;
+        }
+    } else if (inert) {
         negA = schol(Lb, 8, SA);
         if (negA < 0) return 1;
     } else {
@@ -874,23 +923,37 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
     const int rs = W->R == M_RESTO;
     if (rs)
         for (int i = 0; i < W->nrow; ++i) {
-            const double gp = W->rho - (W->lsq ? W->zp[i] : mu / W->pr[i] - W->kd * mu);
-            const double gn = W->rho - (W->lsq ? W->zn[i] : mu / W->nr[i] - W->kd * mu);
+            const double gp = W->ov ? W->ovp[i] : W->rho - (W->lsq ? W->zp[i] : mu / W->pr[i] - W->kd * mu);
+            const double gn = W->ov ? W->ovn[i] : W->rho - (W->lsq ? W->zn[i] : mu / W->nr[i] - W->kd * mu);
             W->gpn[i] = gp / W->Dpr[i] - gn / W->Dnr[i];
         }
     for (int i = 0; i < W->nrc; ++i) W->rct[i] = cres[i] + (rs ? W->gpn[i] : 0.0);
     for (int k = 0; k <= N; ++k) {
         double* q = W->qt + 6 * k;
-        for (int i = 0; i < 6; ++i) q[i] = bgrad_x(W, k, i, mu);
+        for (int i = 0; i < 6; ++i) q[i] = W->ov ? W->ovx[6 * k + i] : bgrad_x(W, k, i, mu);
         for (int j = 0; j < W->nbk; ++j) {
             const int bi = k * W->nbk + j;
             const double *D = W->Dd + 4 * bi, *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *Gm = W->Gm + 16 * bi;
             double* rd = W->rd + 4 * bi;
             for (int r = 0; r < 4; ++r)
-                rd[r] = dres[4 * bi + r] + bgrad_s(W, bi, r, mu) / D[r] + (rs ? W->gpn[W->nrc + 4 * bi + r] : 0.0);
+                rd[r] = dres[4 * bi + r] + (W->ov ? W->ovs[4 * bi + r] : bgrad_s(W, bi, r, mu)) / D[r] +
+                        (rs ? W->gpn[W->nrc + 4 * bi + r] : 0.0);
             double* zf = W->vv + 8 * bi;
-            for (int a = 0; a < 8; ++a) zf[a] = bgrad_w(W, 8 * bi + a, mu);
+            for (int a = 0; a < 8; ++a) zf[a] = W->ov ? W->ovw[8 * bi + a] : bgrad_w(W, 8 * bi + a, mu);
             const double *SA = W->Sg + 12 * bi, *ST = SA + 8;
+            if (W->alt[bi] != 0.0) {
+                const double *Jx = W->Jx + 16 * bi, *Jw = W->Jw + 32 * bi, *E = W->Ed + 4 * bi;
+                for (int a = 0; a < 8; ++a)
+                    for (int r = 0; r < 4; ++r) zf[a] += Jw[r * 8 + a] / E[r] * rd[r];
+                fsub(W->L + 64 * bi, 8, zf);
+                for (int p = 0; p < 4; ++p) {
+                    double g = 0.0;
+                    for (int r = 0; r < 4; ++r) g += Jx[r * 4 + p] / E[r] * rd[r];
+                    for (int a = 0; a < 8; ++a) g -= Zb[a * 4 + p] * zf[a];
+                    q[p] += g;
+                }
+                continue;
+            }
             fsub(W->L + 64 * bi, 8, zf);
             double* t = W->tv + 4 * bi;
             for (int r = 0; r < 4; ++r) {
@@ -910,11 +973,12 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
         }
         if (k == N && W->mode == TTO_OBCA_PLAN)
             for (int i = 0; i < 6; ++i) {
-                W->rf[i] = fres[i] + bgrad_sf(W, i, mu) / W->Dsf[i] + (rs ? W->gpn[W->nrc + W->nrd + i] : 0.0);
+                W->rf[i] = fres[i] + (W->ov ? W->ovsf[i] : bgrad_sf(W, i, mu)) / W->Dsf[i] +
+                           (rs ? W->gpn[W->nrc + W->nrd + i] : 0.0);
                 q[i] += W->Dfe[i] * W->rf[i];
             }
         if (k < N)
-            for (int i = 0; i < 2; ++i) W->rt[2 * k + i] = bgrad_u(W, k, i, mu);
+            for (int i = 0; i < 2; ++i) W->rt[2 * k + i] = W->ov ? W->ovu[2 * k + i] : bgrad_u(W, k, i, mu);
     }
     /* Riccati vector pass (p~ = p - P S M^-1 S p for soft rows) */
     memcpy(W->pv + 6 * N, W->qt + 6 * N, 6 * sizeof(double));
@@ -1001,6 +1065,26 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             const double *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *Gm = W->Gm + 16 * bi, *dxk = W->dx + 6 * k;
             const double* D = W->Dd + 4 * bi;
             const double *SA = W->Sg + 12 * bi, *ST = SA + 8;
+            if (W->alt[bi] != 0.0) {
+                const double *Jx = W->Jx + 16 * bi, *Jw = W->Jw + 32 * bi, *E = W->Ed + 4 * bi;
+                double t8[8];
+                for (int a = 0; a < 8; ++a) {
+                    double t = W->vv[8 * bi + a];
+                    for (int q = 0; q < 4; ++q) t += Zb[a * 4 + q] * dxk[q];
+                    t8[a] = t;
+                }
+                bsub(W->L + 64 * bi, 8, t8);
+                for (int a = 0; a < 8; ++a) W->dw[8 * bi + a] = -t8[a];
+                double* yp = W->ydp + 4 * bi;
+                for (int r = 0; r < 4; ++r) {
+                    double t = W->rd[4 * bi + r];
+                    for (int a = 0; a < 8; ++a) t += Jw[r * 8 + a] * W->dw[8 * bi + a];
+                    for (int q = 0; q < 4; ++q) t += Jx[r * 4 + q] * dxk[q];
+                    yp[r] = t / E[r];
+                }
+                for (int r = 0; r < 4; ++r) W->ds[4 * bi + r] = (yp[r] - (W->ov ? W->ovs[4 * bi + r] : bgrad_s(W, bi, r, mu))) / D[r];
+                continue;
+            }
             double g4[4];
             for (int r = 0; r < 4; ++r) {
                 double t = 0.0;
@@ -1021,18 +1105,21 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             }
             bsub(W->L + 64 * bi, 8, t8);
             for (int a = 0; a < 8; ++a) W->dw[8 * bi + a] = -t8[a];
-            for (int r = 0; r < 4; ++r) W->ds[4 * bi + r] = (yp[r] - bgrad_s(W, bi, r, mu)) / D[r];
+            for (int r = 0; r < 4; ++r)
+                W->ds[4 * bi + r] = (yp[r] - (W->ov ? W->ovs[4 * bi + r] : bgrad_s(W, bi, r, mu))) / D[r];
         }
     if (W->mode == TTO_OBCA_PLAN)
         for (int i = 0; i < 6; ++i) {
             W->ydpf[i] = W->Dfe[i] * (W->dx[6 * N + i] + W->rf[i]);
-            W->dsf[i] = (W->ydpf[i] - bgrad_sf(W, i, mu)) / W->Dsf[i];
+            W->dsf[i] = (W->ydpf[i] - (W->ov ? W->ovsf[i] : bgrad_sf(W, i, mu))) / W->Dsf[i];
         }
     if (rs) /* elastic variables: D_p dp - y+ = -(rho - mu/p),  D_n dn + y+ = -(rho - mu/n) */
         for (int i = 0; i < W->nrow; ++i) {
             const double yp = i < W->nrc ? W->ycp[i] : i < W->nrc + W->nrd ? W->ydp[i - W->nrc] : W->ydpf[i - W->nrc - W->nrd];
-            W->dpr[i] = (yp - (W->rho - mu / W->pr[i] + W->kd * mu)) / W->Dpr[i];
-            W->dnr[i] = (-yp - (W->rho - mu / W->nr[i] + W->kd * mu)) / W->Dnr[i];
+            const double gp = W->ov ? W->ovp[i] : W->rho - mu / W->pr[i] + W->kd * mu;
+            const double gn = W->ov ? W->ovn[i] : W->rho - mu / W->nr[i] + W->kd * mu;
+            W->dpr[i] = (yp - gp) / W->Dpr[i];
+            W->dnr[i] = (-yp - gn) / W->Dnr[i];
         }
 }
 
@@ -1878,6 +1965,162 @@ static void check_newton(ws_t* W, double mu, double dw) {
     fprintf(stderr, "   check(R=%d): x %.1e u %.1e w %.1e s %.1e pn %.1e rows %.1e\n", W->R, wx, wu, ww, wsl, wpn, wrow);
 }
 
+/* residuals of the un-condensed primal-dual Newton rows at the solution in dx.. ycp ydp dsf ydpf (dp dn), with
+ * the constants of the solve (barrier gradients or the override, and cres / dres / fres); returns the max
+ * norm of all of them and of the constants in *rhs_inf */
+static double newton_resid(ws_t* W, double mu, const double* cres, const double* dres, const double* fres,
+                           double* rhs_inf) {
+    const tto_obca_problem* P = W->P;
+    const int N = W->N, rs = W->R == M_RESTO;
+    const double dw = W->dw_cur;
+    double rmax = 0.0, bmax = 0.0;
+#define CST(v) (bmax = fmax(bmax, fabs(v)), (v))
+    for (int k = 0; k <= N; ++k) {
+        const double tf = (k == N && W->mode == TTO_OBCA_PLAN) ? P->tfac : 1.0;
+        for (int i = 0; i < 6; ++i) {
+            double t = CST(W->ov ? W->ovx[6 * k + i] : bgrad_x(W, k, i, mu));
+            for (int j = 0; j < 6; ++j) {
+                double h = (k < N ? W->Wd[36 * k + i * 6 + j] : 0.0);
+                if (!rs) h += 2.0 * tf * W->Qc[i * 6 + j];
+                t += h * W->dx[6 * k + j];
+            }
+            t += (sig_x(W, k, i) + dw + (rs ? W->zeta * W->dRx[6 * k + i] : 0.0)) * W->dx[6 * k + i];
+            t += W->ycp[6 * k + i];
+            if (k < N) for (int l = 0; l < 6; ++l) t -= W->A[36 * k + l * 6 + i] * W->ycp[6 * (k + 1) + l];
+            if (k == N && W->mode == TTO_OBCA_PLAN) t += W->ydpf[i];
+            if (i < 4)
+                for (int j = 0; j < W->nbk; ++j) {
+                    const int bi = k * W->nbk + j;
+                    for (int q = 0; q < 4; ++q) t += W->Hxx[16 * bi + i * 4 + q] * W->dx[6 * k + q];
+                    for (int a = 0; a < 8; ++a) t += W->Hxw[32 * bi + i * 8 + a] * W->dw[8 * bi + a];
+                    for (int r = 0; r < 4; ++r) t += W->Jx[16 * bi + r * 4 + i] * W->ydp[4 * bi + r];
+                }
+            W->rsx[6 * k + i] = t;
+            rmax = fmax(rmax, fabs(t));
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) {
+                double t = CST(W->ov ? W->ovu[2 * k + i] : bgrad_u(W, k, i, mu));
+                if (!rs) for (int j = 0; j < 2; ++j) t += 2.0 * W->Rc[i * 2 + j] * W->du[2 * k + j];
+                t += (sig_u(W, k, i) + dw + (rs ? W->zeta * W->dRu[2 * k + i] : 0.0)) * W->du[2 * k + i];
+                t -= P->dt * W->ycp[6 * (k + 1) + (i == 0 ? 5 : 4)];
+                W->rsu[2 * k + i] = t;
+                rmax = fmax(rmax, fabs(t));
+            }
+        for (int j = 0; j < W->nbk; ++j) {
+            const int bi = k * W->nbk + j;
+            for (int a = 0; a < 8; ++a) {
+                double t = CST(W->ov ? W->ovw[8 * bi + a] : bgrad_w(W, 8 * bi + a, mu));
+                t += (W->zw[8 * bi + a] / (W->w[8 * bi + a] + RELAX) + dw + (rs ? W->zeta * W->dRw[8 * bi + a] : 0.0)) * W->dw[8 * bi + a];
+                for (int q = 0; q < 4; ++q) t += W->Hxw[32 * bi + q * 8 + a] * W->dx[6 * k + q];
+                if (a >= 4) for (int b = 0; b < 4; ++b) t += W->Hww[16 * bi + (a - 4) * 4 + b] * W->dw[8 * bi + 4 + b];
+                for (int r = 0; r < 4; ++r) t += W->Jw[32 * bi + r * 8 + a] * W->ydp[4 * bi + r];
+                W->rsw[8 * bi + a] = t;
+                rmax = fmax(rmax, fabs(t));
+            }
+            for (int r = 0; r < 4; ++r) {
+                const int v = 4 * bi + r, ro = W->nrc + v;
+                double t = CST(W->ov ? W->ovs[v] : bgrad_s(W, bi, r, mu));
+                t += (sig_s(W, bi, r) + dw) * W->ds[v] - W->ydp[v];
+                W->rss[v] = t;
+                rmax = fmax(rmax, fabs(t));
+                t = CST(dres[v]);
+                for (int q = 0; q < 4; ++q) t += W->Jx[16 * bi + r * 4 + q] * W->dx[6 * k + q];
+                for (int a = 0; a < 8; ++a) t += W->Jw[32 * bi + r * 8 + a] * W->dw[8 * bi + a];
+                t -= W->ds[v];
+                if (rs) t += -W->dpr[ro] + W->dnr[ro];
+                W->rrd[v] = t;
+                rmax = fmax(rmax, fabs(t));
+            }
+        }
+        for (int i = 0; i < 6; ++i) {
+            const int v = 6 * k + i;
+            double t = CST(cres[v]) + W->dx[v];
+            if (k > 0) {
+                for (int j = 0; j < 6; ++j) t -= W->A[36 * (k - 1) + i * 6 + j] * W->dx[6 * (k - 1) + j];
+                if (i == 5) t -= P->dt * W->du[2 * (k - 1)];
+                if (i == 4) t -= P->dt * W->du[2 * (k - 1) + 1];
+            }
+            if (rs) t += -W->dpr[v] + W->dnr[v];
+            W->rrc[v] = t;
+            rmax = fmax(rmax, fabs(t));
+        }
+    }
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) {
+            const int ro = W->nrc + W->nrd + i;
+            double t = CST(fres[i]) + W->dx[6 * N + i] - W->dsf[i];
+            if (rs) t += -W->dpr[ro] + W->dnr[ro];
+            W->rrf[i] = t;
+            rmax = fmax(rmax, fabs(t));
+            t = CST(W->ov ? W->ovsf[i] : bgrad_sf(W, i, mu));
+            t += (W->vLf[i] / (W->sf[i] - W->fL) + W->vUf[i] / (W->fU - W->sf[i]) + dw) * W->dsf[i] - W->ydpf[i];
+            W->rssf[i] = t;
+            rmax = fmax(rmax, fabs(t));
+        }
+    if (rs)
+        for (int i = 0; i < W->nrow; ++i) {
+            const double yp = i < W->nrc ? W->ycp[i] : i < W->nrc + W->nrd ? W->ydp[i - W->nrc] : W->ydpf[i - W->nrc - W->nrd];
+            double t = CST(W->ov ? W->ovp[i] : W->rho - mu / W->pr[i] + W->kd * mu);
+            t += (W->zp[i] / W->pr[i] + dw) * W->dpr[i] - yp;
+            W->rsp[i] = t;
+            rmax = fmax(rmax, fabs(t));
+            t = CST(W->ov ? W->ovn[i] : W->rho - mu / W->nr[i] + W->kd * mu);
+            t += (W->zn[i] / W->nr[i] + dw) * W->dnr[i] + yp;
+            W->rsn[i] = t;
+            rmax = fmax(rmax, fabs(t));
+        }
+#undef CST
+    if (rhs_inf) *rhs_inf = bmax;
+    return rmax;
+}
+
+/* the step solve with IPOPT's iterative refinement on the un-condensed system (min_refinement_steps 1,
+ * max_refinement_steps 10, residual_ratio_max 1e-10): correction solves reuse the factorisation with the
+ * residuals as constants (TTO_OPT_REFINE) */
+static void refined_solve(ws_t* W, double mu, double* cres, double* dres, double* fres) {
+    solve_rhs(W, mu, cres, dres, fres);
+    if (!(W->P->opts & TTO_OPT_REFINE) || W->lsq) return;
+    const int N = W->N, rs = W->R == M_RESTO;
+    const size_t N1 = (size_t)N + 1, nb = (size_t)W->nb, nr = (size_t)W->nrow;
+    double bnorm = 0.0;
+    double res = newton_resid(W, mu, cres, dres, fres, &bnorm);
+    double* cc = (double*)malloc((N1 * 6 + nb * 4 + 6) * sizeof(double));
+    for (int it = 0; it < 10; ++it) {
+        double snorm = 0.0;
+        for (size_t i = 0; i < N1 * 6; ++i) snorm = fmax(snorm, fmax(fabs(W->dx[i]), fabs(W->ycp[i])));
+        for (size_t i = 0; i < nb * 8; ++i) snorm = fmax(snorm, fabs(W->dw[i]));
+        if (it >= 1 && res <= 1e-10 * (fmin(snorm, 1e6) + bnorm)) break;
+        /* save the solution, solve for the correction with the residuals as constants, add */
+        double* o = W->sol;
+        memcpy(o, W->dx, N1 * 48); o += N1 * 6; memcpy(o, W->ycp, N1 * 48); o += N1 * 6;
+        memcpy(o, W->du, (size_t)N * 16); o += N * 2; memcpy(o, W->dw, nb * 64); o += nb * 8;
+        memcpy(o, W->ds, nb * 32); o += nb * 4; memcpy(o, W->ydp, nb * 32); o += nb * 4;
+        memcpy(o, W->dsf, 48); o += 6; memcpy(o, W->ydpf, 48); o += 6;
+        if (rs) { memcpy(o, W->dpr, nr * 8); o += nr; memcpy(o, W->dnr, nr * 8); o += nr; }
+        memcpy(W->ovx, W->rsx, N1 * 48); memcpy(W->ovu, W->rsu, (size_t)N * 16); memcpy(W->ovw, W->rsw, nb * 64);
+        memcpy(W->ovs, W->rss, nb * 32); memcpy(W->ovsf, W->rssf, 48);
+        if (rs) { memcpy(W->ovp, W->rsp, nr * 8); memcpy(W->ovn, W->rsn, nr * 8); }
+        memcpy(cc, W->rrc, N1 * 48); memcpy(cc + N1 * 6, W->rrd, nb * 32); memcpy(cc + N1 * 6 + nb * 4, W->rrf, 48);
+        W->ov = W->ovx;
+        solve_rhs(W, mu, cc, cc + N1 * 6, cc + N1 * 6 + nb * 4);
+        W->ov = NULL;
+        o = W->sol;
+#define ADD(ptr, cnt) do { for (size_t q_ = 0; q_ < (cnt); ++q_) (ptr)[q_] += o[q_]; o += (cnt); } while (0)
+        ADD(W->dx, N1 * 6); ADD(W->ycp, N1 * 6); ADD(W->du, (size_t)N * 2); ADD(W->dw, nb * 8); ADD(W->ds, nb * 4);
+        ADD(W->ydp, nb * 4); ADD(W->dsf, 6); ADD(W->ydpf, 6);
+        if (rs) { ADD(W->dpr, nr); ADD(W->dnr, nr); }
+#undef ADD
+        const double res2 = newton_resid(W, mu, cres, dres, fres, NULL);
+        if (!(res2 < res)) { /* no improvement: IPOPT stops refining (residual_improvement_factor 1) */
+            res = res2;
+            break;
+        }
+        res = res2;
+    }
+    free(cc);
+}
+
 /* Newton step with inertia correction into dx..; 0 on success */
 static int newton(ws_t* W, ipm_state_t* S, double* dw_out) {
     double dw = 0.0;
@@ -1890,9 +2133,10 @@ static int newton(ws_t* W, ipm_state_t* S, double* dw_out) {
     if (!ok) return 1;
     if (dw > 0) S->dw_last = dw;
     *dw_out = dw;
+    W->dw_cur = dw;
     memcpy(W->cr, W->rc0, (size_t)W->nrc * 8);
     memcpy(W->dr, W->rd0, (size_t)W->nrd * 8);
-    solve_rhs(W, S->mu, W->cr, W->dr, W->rf0);
+    refined_solve(W, S->mu, W->cr, W->dr, W->rf0);
     if (getenv("TTO_CHECK")) check_newton(W, S->mu, dw);
     mult_steps(W, S->mu);
     return 0;
@@ -2004,7 +2248,7 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double* th0p, double*
                 for (size_t i = 0; i < nx_; ++i) W->cr[i] = a_soc * W->cr[i] + W->ct[i];
                 for (size_t i = 0; i < ns_; ++i) W->dr[i] = a_soc * W->dr[i] + W->dtr[i];
                 if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = a_soc * frs[i] + W->dft[i];
-                solve_rhs(W, mu, W->cr, W->dr, frs);
+                refined_solve(W, mu, W->cr, W->dr, frs);
                 a_soc = ftb_primal(W, tau);
                 set_trial(W, a_soc);
                 trial_eval(W, mu, &tht, &pht);

@@ -38,7 +38,8 @@ typedef struct {
     int dual_init;                   /* 0: start from the guess's mu/lam (reference behaviour);
                                         1: replace them by the separating-axis certificate of each
                                         body/obstacle pair at the guess pose (see tt_obca.c) */
-    int opts;                        /* TTO_OPT_* bits switching IPOPT features off (diagnostics; 0 = IPOPT) */
+    int opts;                        /* TTO_OPT_* bits (diagnostics / A-B): 1-4 switch restated features off, 8-128 switch
+                                        oracle-only IPOPT features on; 0 = the kernel's algorithm */
 } tto_obca_problem;
 
 #define TTO_OPT_NO_RESTO 1       /* no restoration phase: a failed line search takes its last trial step */
@@ -48,6 +49,8 @@ typedef struct {
  * them); the GPU kernel does not run them, so GPU-vs-oracle parity uses opts without these bits */
 #define TTO_OPT_KAPPA_D 8        /* kappa_d = 1e-5 linear damping of variables / slacks with one finite bound */
 #define TTO_OPT_WATCHDOG 16      /* watchdog (trigger 10 shortened steps, 3 trial iterations) in the line search */
+#define TTO_OPT_BLOCK_MW 128     /* exact block inertia: a block with indefinite A eliminated rows-first through M_w = A + Jw' E^-1 Jw */
+#define TTO_OPT_REFINE 64        /* IPOPT's iterative refinement of every step solve on the un-condensed system */
 #define TTO_OPT_BLOCK_INERTIA 32 /* exact block inertia In(A) + In(-T) = (8, 4, 0) by signed LDL' instead of A positive definite */
 
 /* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).

@@ -106,8 +106,9 @@ os.environ.setdefault("OMP_PROC_BIND", "false")
 # ------------------------------------------------------------------------------------------------
 MAXM = 16
 OBCA_PLAN, OBCA_TRACK = 0, 1
-# oracle-only opt-in IPOPT features (tt_obca.h): kappa_d damping, line-search watchdog, exact block inertia test
-OPT_KAPPA_D, OPT_WATCHDOG, OPT_BLOCK_INERTIA = 8, 16, 32
+# oracle-only opt-in IPOPT features (tt_obca.h): kappa_d damping, line-search watchdog, exact block inertia test,
+# iterative refinement, rows-first elimination of indefinite blocks
+OPT_KAPPA_D, OPT_WATCHDOG, OPT_BLOCK_INERTIA, OPT_REFINE, OPT_BLOCK_MW = 8, 16, 32, 64, 128
 
 
 class TTOObcaProblem(C.Structure):
