@@ -699,39 +699,60 @@ __device__ __forceinline__ double grad_row(const Ctx& c, int r, double s, double
     return g;
 }
 
-// linearise + factor + rhs of one block at the current iterate; returns false if not positive definite.
-// Outputs D (Sigma_s + dw), E (row regularisation), the elimination and the block's Hessian / gradient
-// contribution to its stage.
-__device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, int j, int k, const double* x,
+// the workspace inputs of one block's factor step (restoration fields only when rs)
+struct BlkIn {
+    double w[8], zw[8], y[4], s[4], vl[4], vu[4], dr[4];
+    double drw[8], wr[8], pr[4], nr[4], zp[4], zn[4];
+};
+__device__ __forceinline__ void load_blk_in(const Ctx& c, bool rs, int j, int k, BlkIn& in) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { in.w[e] = c.B(B_W + e, j, k); in.zw[e] = c.B(B_ZW + e, j, k); }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        in.y[r] = c.B(B_YD + r, j, k);
+        in.s[r] = c.B(B_S + r, j, k); in.vl[r] = c.B(B_VL + r, j, k); in.vu[r] = c.B(B_VU + r, j, k);
+        in.dr[r] = c.B(B_DR + r, j, k);
+    }
+    if (rs) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { in.drw[e] = c.B(B_DRW + e, j, k); in.wr[e] = c.B(B_WR + e, j, k); }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            in.pr[r] = c.B(B_PR + r, j, k); in.nr[r] = c.B(B_NR + r, j, k);
+            in.zp[r] = c.B(B_ZP + r, j, k); in.zn[r] = c.B(B_ZN + r, j, k);
+        }
+    }
+}
+
+// linearise + factor + rhs of one block at the current iterate (inputs preloaded); returns false if not
+// positive definite.  Outputs D (Sigma_s + dw), E (row regularisation), the elimination and the block's
+// Hessian / gradient contribution to its stage.
+__device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, const BlkIn& in, int j, const double* x,
                                             const Trig& tr, double mu, double dw, Blk& bk, double* fw, double* zf,
                                             double* t4, double* C4, double* q4) {
     const bool rs = sh.R != 0, lsq = sh.lsq != 0;
-    double w[8], y[4], sw[8], rd[4];
+    double sw[8], rd[4];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        w[e] = c.B(B_W + e, j, k);
-        const double sl = w[e] + RELAX, zw = c.B(B_ZW + e, j, k);
+        const double sl = in.w[e] + RELAX, zw = in.zw[e];
         double gw = 0.0, hw = 0.0;
         if (rs) {
-            hw = sh.zeta * c.B(B_DRW + e, j, k);
-            gw = hw * (w[e] - c.B(B_WR + e, j, k));
+            hw = sh.zeta * in.drw[e];
+            gw = hw * (in.w[e] - in.wr[e]);
         }
         sw[e] = lsq ? 1.0 : zw / sl + hw;
         fw[e] = lsq ? gw - zw : gw - mu / sl;
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
-    blk_lin(*c.a, x, tr, j, w, y, bk);
+    blk_lin(*c.a, x, tr, j, in.w, in.y, bk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+        const double s = in.s[r], vl = in.vl[r], vu = in.vu[r];
         bk.D[r] = lsq ? 1.0 : sig_row(c, r, s, vl, vu) + dw;
         bk.E[r] = 1.0 / bk.D[r];
         const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
-        rd[r] = c.B(B_DR + r, j, k) + gs / bk.D[r];
+        rd[r] = in.dr[r] + gs / bk.D[r];
         if (rs) {
-            const PN t = pn_terms(lsq, c.B(B_PR + r, j, k), c.B(B_NR + r, j, k), c.B(B_ZP + r, j, k),
-                                  c.B(B_ZN + r, j, k), mu, dw);
+            const PN t = pn_terms(lsq, in.pr[r], in.nr[r], in.zp[r], in.zn[r], mu, dw);
             bk.E[r] += 1.0 / t.Dp + 1.0 / t.Dn;
             rd[r] += t.gp / t.Dp - t.gn / t.Dn;
         }
@@ -755,11 +776,16 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
         // the OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
         double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
         const Trig tr = stage_trig(x);
+        // software-pipelined inputs: block j+1's loads are issued before block j's factor-record stores, so
+        // waiting for them does not wait for the stores (one in-order vmcnt queue)
+        BlkIn cur;
+        load_blk_in(c, rs, 0, k, cur);
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4];
-            if (!block_setup(c, sh, j, k, x, tr, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+            if (!block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+            if (j + 1 < c.nbk) load_blk_in(c, rs, j + 1, k, cur);
             auto st = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
 #pragma unroll
             for (int r = 0; r < 4; ++r)
