@@ -1673,8 +1673,10 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
                 if (c.huu(i)) { const double sl = c.uu[i] - u[i]; ok &= sl > 0.0; ls.add(sl); }
                 if (rs) { const double e = u[i] - c.S(S_UR + i, k); prox += c.S(S_DRU + i, k) * e * e; }
             }
-        // dynamics residual c_{k+1} = x_{k+1} - F(x_k, u_k) (thread k), c_0 = x_0 - x_init
-        double ck[6] = {0, 0, 0, 0, 0, 0};
+        // dynamics residual c_{k+1} = x_{k+1} - F(x_k, u_k) (thread k), c_0 = x_0 - x_init; stored after the
+        // block loop (and each block's trial residual after the next block's loads): a store ahead of a load
+        // in the in-order vmcnt queue makes the load's wait include it
+        double ck[6] = {0, 0, 0, 0, 0, 0}, cn[6] = {0, 0, 0, 0, 0, 0};
         if (k == 0) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) ck[i] = x[i] - a.x0[6 * (size_t)c.b + i];
@@ -1691,7 +1693,7 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
                     const double n = c.S(S_NR + i, k + 1) + alpha * c.S(S_DN + 6 * buf + i, k + 1);
                     cv -= p - n;
                 }
-                c.S(S_CT + i, k + 1) = cv;
+                cn[i] = cv;
                 th += fabs(cv);
             }
         }
@@ -1708,43 +1710,67 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
             }
         if (k == 0)
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                c.S(S_CT + i, 0) = ck[i];
-                th += fabs(ck[i]);
-            }
+            for (int i = 0; i < 6; ++i) th += fabs(ck[i]);
         const Trig tr = stage_trig(x);
+        double pdt[4] = {0, 0, 0, 0};
+        int pj = -1;
         for (int j = 0; j < c.nbk; ++j) {
-            double w[8], d[4];
+            double w[8], d[4], wr[8], drw[8], sv[4], pv[4], nv[4];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 w[e] = c.B(B_W + e, j, k) + alpha * c.B(B_DW + 8 * buf + e, j, k);
+                if (rs) { wr[e] = c.B(B_WR + e, j, k); drw[e] = c.B(B_DRW + e, j, k); }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                sv[r] = c.B(B_S + r, j, k) + alpha * c.B(B_DS + 4 * buf + r, j, k);
+                if (rs) {
+                    pv[r] = c.B(B_PR + r, j, k) + alpha * c.B(B_DP + 4 * buf + r, j, k);
+                    nv[r] = c.B(B_NR + r, j, k) + alpha * c.B(B_DN + 4 * buf + r, j, k);
+                }
+            }
+            if (pj >= 0)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c.B(B_DT + r, pj, k) = pdt[r];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
                 const double sl = w[e] + RELAX;
                 ok &= sl > 0.0;
                 ls.add(sl);
-                if (rs) { const double ew = w[e] - c.B(B_WR + e, j, k); prox += c.B(B_DRW + e, j, k) * ew * ew; }
+                if (rs) { const double ew = w[e] - wr[e]; prox += drw[e] * ew * ew; }
             }
             blk_vals(a, x, tr, j, w, d);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double s = c.B(B_S + r, j, k) + alpha * c.B(B_DS + 4 * buf + r, j, k);
+                const double s = sv[r];
                 double res = d[r] - s;
                 if (rs) {
-                    const double p = c.B(B_PR + r, j, k) + alpha * c.B(B_DP + 4 * buf + r, j, k);
-                    const double n = c.B(B_NR + r, j, k) + alpha * c.B(B_DN + 4 * buf + r, j, k);
+                    const double p = pv[r];
+                    const double n = nv[r];
                     ok &= p > 0.0 && n > 0.0;
                     ls.add(p);
                     ls.add(n);
                     Fr += p + n;
                     res -= p - n;
                 }
-                c.B(B_DT + r, j, k) = res;
+                pdt[r] = res;
                 th += fabs(res);
                 const double su = c.rU(r) - s;
                 ok &= su > 0.0;
                 ls.add(su);
                 if (c.hrl(r)) { const double sl = s - c.rL(r); ok &= sl > 0.0; ls.add(sl); }
             }
+            pj = j;
         }
+        if (pj >= 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c.B(B_DT + r, pj, k) = pdt[r];
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) c.S(S_CT + i, k + 1) = cn[i];
+        if (k == 0)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) c.S(S_CT + i, 0) = ck[i];
         if (k == N && plan)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
@@ -1809,35 +1835,81 @@ __device__ __noinline__ void phase_resid(const Ctx& c, LShared& sh, bool zero) {
     }
 }
 
-// ======== phase: accept the step ========
+// inputs of one block's update (restoration pairs only when rs)
+struct UpdIn {
+    double w[8], dw[8], zw[8], s[4], ds[4], vu[4], vl[4], yd[4], yp[4];
+    double pr[4], nr[4], zp[4], zn[4], dp[4], dn[4];
+};
+__device__ __forceinline__ void load_upd_in(const Ctx& c, bool rs, int buf, int j, int k, UpdIn& in) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        in.w[e] = c.B(B_W + e, j, k); in.dw[e] = c.B(B_DW + 8 * buf + e, j, k); in.zw[e] = c.B(B_ZW + e, j, k);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        in.s[r] = c.B(B_S + r, j, k); in.ds[r] = c.B(B_DS + 4 * buf + r, j, k);
+        in.vu[r] = c.B(B_VU + r, j, k); in.vl[r] = c.hrl(r) ? (double)c.B(B_VL + r, j, k) : 0.0;
+        in.yd[r] = c.B(B_YD + r, j, k); in.yp[r] = c.B(B_YP + 4 * buf + r, j, k);
+        if (rs) {
+            in.pr[r] = c.B(B_PR + r, j, k); in.nr[r] = c.B(B_NR + r, j, k);
+            in.zp[r] = c.B(B_ZP + r, j, k); in.zn[r] = c.B(B_ZN + r, j, k);
+            in.dp[r] = c.B(B_DP + 4 * buf + r, j, k); in.dn[r] = c.B(B_DN + 4 * buf + r, j, k);
+        }
+    }
+}
+
+// ======== phase: accept the step (primal alpha, duals az, kappa_sigma safeguard) ========
+// All loads of a stage are issued before its stores, and block j+1's loads before block j's stores: the
+// workspace fields may alias as far as the compiler knows, so interleaved load / store pairs would each wait
+// for the previous stores (one in-order vmcnt queue).
 __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
     const int N = c.N;
     const bool rs = sh.R != 0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
+        double x[6], d[6], zl[6], zu[6], y[6], yp[6], pr[6], nr[6], zp[6], zn[6], dp[6], dn[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            const double x = c.S(S_X + i, k), d = c.S(S_DX + 6 * buf + i, k);
-            const double xn = x + alpha * d;
+            x[i] = c.S(S_X + i, k); d[i] = c.S(S_DX + 6 * buf + i, k);
+            zl[i] = c.hlx(i) ? (double)c.S(S_ZLX + i, k) : 0.0;
+            zu[i] = c.hux(i) ? (double)c.S(S_ZUX + i, k) : 0.0;
+            y[i] = c.S(S_YC + i, k); yp[i] = c.S(S_YCP + 6 * buf + i, k);
+            if (rs) {
+                pr[i] = c.S(S_PR + i, k); nr[i] = c.S(S_NR + i, k); zp[i] = c.S(S_ZP + i, k); zn[i] = c.S(S_ZN + i, k);
+                dp[i] = c.S(S_DP + 6 * buf + i, k); dn[i] = c.S(S_DN + 6 * buf + i, k);
+            }
+        }
+        double u[2] = {0.0, 0.0}, du[2] = {0.0, 0.0}, zlu[2] = {0.0, 0.0}, zuu[2] = {0.0, 0.0};
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                u[i] = c.S(S_U + i, k); du[i] = c.S(S_DU + 2 * buf + i, k);
+                if (c.hlu(i)) zlu[i] = c.S(S_ZLU + i, k);
+                if (c.huu(i)) zuu[i] = c.S(S_ZUU + i, k);
+            }
+        UpdIn cur;
+        if (c.nbk > 0) load_upd_in(c, rs, buf, 0, k, cur);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double xv = x[i], dv = d[i];
+            const double xn = xv + alpha * dv;
             if (c.hlx(i)) {
-                const double sl = x - c.xl[i], z = c.S(S_ZLX + i, k);
-                double zn = z + az * (mu / sl - z - z / sl * d);
-                clamp_mult(zn, xn - c.xl[i], mu);
-                c.S(S_ZLX + i, k) = zn;
+                const double sl = xv - c.xl[i], z = zl[i];
+                double zn2 = z + az * (mu / sl - z - z / sl * dv);
+                clamp_mult(zn2, xn - c.xl[i], mu);
+                c.S(S_ZLX + i, k) = zn2;
             }
             if (c.hux(i)) {
-                const double sl = c.xu[i] - x, z = c.S(S_ZUX + i, k);
-                double zn = z + az * (mu / sl - z + z / sl * d);
-                clamp_mult(zn, c.xu[i] - xn, mu);
-                c.S(S_ZUX + i, k) = zn;
+                const double sl = c.xu[i] - xv, z = zu[i];
+                double zn2 = z + az * (mu / sl - z + z / sl * dv);
+                clamp_mult(zn2, c.xu[i] - xn, mu);
+                c.S(S_ZUX + i, k) = zn2;
             }
             c.S(S_X + i, k) = xn;
-            const double y = c.S(S_YC + i, k);
-            c.S(S_YC + i, k) = y + alpha * (c.S(S_YCP + 6 * buf + i, k) - y);
+            c.S(S_YC + i, k) = y[i] + alpha * (yp[i] - y[i]);
             if (rs) {
-                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
-                const double dp = c.S(S_DP + 6 * buf + i, k), dn = c.S(S_DN + 6 * buf + i, k);
-                const double pn = p + alpha * dp, nn = n + alpha * dn;
-                double zpn = zp + az * (mu / p - zp - zp / p * dp), znn = zn + az * (mu / n - zn - zn / n * dn);
+                const double p = pr[i], n = nr[i], zpv = zp[i], znv = zn[i];
+                const double pn = p + alpha * dp[i], nn = n + alpha * dn[i];
+                double zpn = zpv + az * (mu / p - zpv - zpv / p * dp[i]), znn = znv + az * (mu / n - znv - znv / n * dn[i]);
                 clamp_mult(zpn, pn, mu);
                 clamp_mult(znn, nn, mu);
                 c.S(S_PR + i, k) = pn;
@@ -1849,60 +1921,74 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
         if (k < N)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const double u = c.S(S_U + i, k), d = c.S(S_DU + 2 * buf + i, k);
-                const double un = u + alpha * d;
+                const double uv = u[i], dv = du[i];
+                const double un = uv + alpha * dv;
                 if (c.hlu(i)) {
-                    const double sl = u - c.ul[i], z = c.S(S_ZLU + i, k);
-                    double zn = z + az * (mu / sl - z - z / sl * d);
-                    clamp_mult(zn, un - c.ul[i], mu);
-                    c.S(S_ZLU + i, k) = zn;
+                    const double sl = uv - c.ul[i], z = zlu[i];
+                    double zn2 = z + az * (mu / sl - z - z / sl * dv);
+                    clamp_mult(zn2, un - c.ul[i], mu);
+                    c.S(S_ZLU + i, k) = zn2;
                 }
                 if (c.huu(i)) {
-                    const double sl = c.uu[i] - u, z = c.S(S_ZUU + i, k);
-                    double zn = z + az * (mu / sl - z + z / sl * d);
-                    clamp_mult(zn, c.uu[i] - un, mu);
-                    c.S(S_ZUU + i, k) = zn;
+                    const double sl = c.uu[i] - uv, z = zuu[i];
+                    double zn2 = z + az * (mu / sl - z + z / sl * dv);
+                    clamp_mult(zn2, c.uu[i] - un, mu);
+                    c.S(S_ZUU + i, k) = zn2;
                 }
                 c.S(S_U + i, k) = un;
             }
         for (int j = 0; j < c.nbk; ++j) {
+            double wn[8], zwn[8], sn[4], vun[4], vln[4], ydn[4], prn[4], nrn[4], zpn[4], znn[4];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const double w = c.B(B_W + e, j, k), d = c.B(B_DW + 8 * buf + e, j, k), z = c.B(B_ZW + e, j, k);
-                const double sl = w + RELAX, wn = w + alpha * d;
-                double zn = z + az * (mu / sl - z - z / sl * d);
-                clamp_mult(zn, wn + RELAX, mu);
-                c.B(B_W + e, j, k) = wn;
-                c.B(B_ZW + e, j, k) = zn;
+                const double w = cur.w[e], dv = cur.dw[e], z = cur.zw[e];
+                const double sl = w + RELAX;
+                wn[e] = w + alpha * dv;
+                double zn2 = z + az * (mu / sl - z - z / sl * dv);
+                clamp_mult(zn2, wn[e] + RELAX, mu);
+                zwn[e] = zn2;
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double s = c.B(B_S + r, j, k), d = c.B(B_DS + 4 * buf + r, j, k), sn = s + alpha * d;
-                const double vu = c.B(B_VU + r, j, k), slu = c.rU(r) - s;
-                double vun = vu + az * (mu / slu - vu + vu / slu * d);
-                clamp_mult(vun, c.rU(r) - sn, mu);
-                c.B(B_VU + r, j, k) = vun;
+                const double sv = cur.s[r], dv = cur.ds[r];
+                sn[r] = sv + alpha * dv;
+                const double vu = cur.vu[r], slu = c.rU(r) - sv;
+                double vu2 = vu + az * (mu / slu - vu + vu / slu * dv);
+                clamp_mult(vu2, c.rU(r) - sn[r], mu);
+                vun[r] = vu2;
                 if (c.hrl(r)) {
-                    const double vl = c.B(B_VL + r, j, k), sll = s - c.rL(r);
-                    double vln = vl + az * (mu / sll - vl - vl / sll * d);
-                    clamp_mult(vln, sn - c.rL(r), mu);
-                    c.B(B_VL + r, j, k) = vln;
+                    const double vl = cur.vl[r], sll = sv - c.rL(r);
+                    double vl2 = vl + az * (mu / sll - vl - vl / sll * dv);
+                    clamp_mult(vl2, sn[r] - c.rL(r), mu);
+                    vln[r] = vl2;
                 }
-                c.B(B_S + r, j, k) = sn;
-                const double y = c.B(B_YD + r, j, k);
-                c.B(B_YD + r, j, k) = y + alpha * (c.B(B_YP + 4 * buf + r, j, k) - y);
+                ydn[r] = cur.yd[r] + alpha * (cur.yp[r] - cur.yd[r]);
                 if (rs) {
-                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k), zp = c.B(B_ZP + r, j, k),
-                                 zn = c.B(B_ZN + r, j, k);
-                    const double dp = c.B(B_DP + 4 * buf + r, j, k), dn = c.B(B_DN + 4 * buf + r, j, k);
-                    const double pn = p + alpha * dp, nn = n + alpha * dn;
-                    double zpn = zp + az * (mu / p - zp - zp / p * dp), znn = zn + az * (mu / n - zn - zn / n * dn);
-                    clamp_mult(zpn, pn, mu);
-                    clamp_mult(znn, nn, mu);
-                    c.B(B_PR + r, j, k) = pn;
-                    c.B(B_NR + r, j, k) = nn;
-                    c.B(B_ZP + r, j, k) = zpn;
-                    c.B(B_ZN + r, j, k) = znn;
+                    const double p = cur.pr[r], n = cur.nr[r], zpv = cur.zp[r], znv = cur.zn[r];
+                    prn[r] = p + alpha * cur.dp[r];
+                    nrn[r] = n + alpha * cur.dn[r];
+                    double a1 = zpv + az * (mu / p - zpv - zpv / p * cur.dp[r]);
+                    double a2 = znv + az * (mu / n - znv - znv / n * cur.dn[r]);
+                    clamp_mult(a1, prn[r], mu);
+                    clamp_mult(a2, nrn[r], mu);
+                    zpn[r] = a1;
+                    znn[r] = a2;
+                }
+            }
+            if (j + 1 < c.nbk) load_upd_in(c, rs, buf, j + 1, k, cur);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { c.B(B_W + e, j, k) = wn[e]; c.B(B_ZW + e, j, k) = zwn[e]; }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                c.B(B_VU + r, j, k) = vun[r];
+                if (c.hrl(r)) c.B(B_VL + r, j, k) = vln[r];
+                c.B(B_S + r, j, k) = sn[r];
+                c.B(B_YD + r, j, k) = ydn[r];
+                if (rs) {
+                    c.B(B_PR + r, j, k) = prn[r];
+                    c.B(B_NR + r, j, k) = nrn[r];
+                    c.B(B_ZP + r, j, k) = zpn[r];
+                    c.B(B_ZN + r, j, k) = znn[r];
                 }
             }
         }
