@@ -2054,6 +2054,10 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
     const double* xinit = a.x0 + 6 * (size_t)c.b;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0}, gl[6];
+        // this stage's outputs stay in registers until every load of the stage has been issued (a store ahead
+        // of a load in the in-order vmcnt queue makes the load's wait include it); block j's row values are
+        // stored after block j+1's loads
+        double gxs[6], gus[2] = {0.0, 0.0}, dj[9], wd[7];
         double objR = 0.0;  // restoration objective of this stage
         load_x(c, k, x);
         if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
@@ -2063,14 +2067,14 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
             for (int i = 0; i < 6; ++i) {
                 const double dr = c.S(S_DRX + i, k), e = x[i] - c.S(S_XR + i, k);
                 gl[i] = zeta * dr * e;
-                c.S(S_GX + i, k) = gl[i];
+                gxs[i] = gl[i];
                 prox += dr * e * e;
             }
             if (k < N)
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     const double dr = c.S(S_DRU + i, k), e = u[i] - c.S(S_UR + i, k);
-                    c.S(S_GU + i, k) = zeta * dr * e;
+                    gus[i] = zeta * dr * e;
                     prox += dr * e * e;
                 }
             objR += 0.5 * zeta * prox;
@@ -2083,13 +2087,13 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
                 for (int j2 = 0; j2 < 6; ++j2) g += 0.5 * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]) * (x[j2] - tg[j2]);
                 gl[i] = 2.0 * sc * g;
-                c.S(S_GX + i, k) = gl[i];
+                gxs[i] = gl[i];
             }
             if (k < N) {
                 const double r0 = u[0] - (plan ? 0.0 : c.tgt_u[2 * k]), r1 = u[1] - (plan ? 0.0 : c.tgt_u[2 * k + 1]);
                 const double R01 = 0.5 * (a.R[1] + a.R[2]);
-                c.S(S_GU, k) = 2.0 * (a.R[0] * r0 + R01 * r1);
-                c.S(S_GU + 1, k) = 2.0 * (R01 * r0 + a.R[3] * r1);
+                gus[0] = 2.0 * (a.R[0] * r0 + R01 * r1);
+                gus[1] = 2.0 * (R01 * r0 + a.R[3] * r1);
             }
         }
         double ck[6];
@@ -2106,7 +2110,6 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
         LogSum lsum, lorig;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            c.S(S_C + i, k) = ck[i];
             double res = ck[i];
             if (rs) {
                 const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
@@ -2132,12 +2135,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
         if (k < N) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) yn[i] = c.S(S_YC + i, k + 1);
-            double dj[9], wd[7];
             model_lin(a, x, yn, dj, wd);
-#pragma unroll
-            for (int i = 0; i < 9; ++i) c.S(S_AJ + i, k) = dj[i];
-#pragma unroll
-            for (int i = 0; i < 7; ++i) c.S(S_WD + i, k) = wd[i];
 #pragma unroll
             for (int i = 0; i < 6; ++i) gl[i] += yk[i] - yn[i];
             gl[2] -= dj[0] * yn[0] + dj[2] * yn[1];
@@ -2151,16 +2149,32 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
         for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
         const Trig tr = stage_trig(x);
+        double pdv[4] = {0, 0, 0, 0};
+        int pj = -1;
         for (int j = 0; j < c.nbk; ++j) {
-            double w[8], y[4], zw[8];
+            double w[8], y[4], zw[8], drw[8], wrv[8], sv[4], vlv[4], vuv[4], prv[4], nrv[4], zpv[4], znv[4];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); }
+            for (int e = 0; e < 8; ++e) {
+                w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k);
+                if (rs) { drw[e] = c.B(B_DRW + e, j, k); wrv[e] = c.B(B_WR + e, j, k); }
+            }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) y[r] = c.B(B_YD + r, j, k);
+            for (int r = 0; r < 4; ++r) {
+                y[r] = c.B(B_YD + r, j, k);
+                sv[r] = c.B(B_S + r, j, k); vlv[r] = c.B(B_VL + r, j, k); vuv[r] = c.B(B_VU + r, j, k);
+                if (rs) {
+                    prv[r] = c.B(B_PR + r, j, k); nrv[r] = c.B(B_NR + r, j, k);
+                    zpv[r] = c.B(B_ZP + r, j, k); znv[r] = c.B(B_ZN + r, j, k);
+                }
+            }
+            if (pj >= 0)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) c.B(B_D + r, pj, k) = pdv[r];
             Blk bk;
             blk_lin(a, x, tr, j, w, y, bk);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) c.B(B_D + r, j, k) = bk.d[r];
+            for (int r = 0; r < 4; ++r) pdv[r] = bk.d[r];
+            pj = j;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 double s = 0.0;
@@ -2172,7 +2186,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
             for (int e = 0; e < 8; ++e) {
                 double t = -zw[e];
                 if (rs) {
-                    const double dr = c.B(B_DRW + e, j, k), ew = w[e] - c.B(B_WR + e, j, k);
+                    const double dr = drw[e], ew = w[e] - wrv[e];
                     t += zeta * dr * ew;
                     objR += 0.5 * zeta * dr * ew * ew;
                 }
@@ -2189,15 +2203,14 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double s = c.B(B_S + r, j, k), vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+                const double s = sv[r], vl = vlv[r], vu = vuv[r];
                 const double td = -y[r] - vl + vu;
                 red[0] = fmax(red[0], fabs(td));
                 red[8] += fabs(td);
                 double res = bk.d[r] - s;
                 red[9] += fabs(res);
                 if (rs) {
-                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k), zp = c.B(B_ZP + r, j, k),
-                                 zn = c.B(B_ZN + r, j, k);
+                    const double p = prv[r], n = nrv[r], zp = zpv[r], zn = znv[r];
                     res -= p - n;
                     const double t1 = RHO - y[r] - zp, t2 = RHO + y[r] - zn;
                     red[0] = fmax(red[0], fmax(fabs(t1), fabs(t2)));
@@ -2273,12 +2286,25 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const double zl = c.S(S_ZLU + i, k), zu = c.S(S_ZUU + i, k);
-                const double t = c.S(S_GU + i, k) - a.dt * yn[i == 0 ? 5 : 4] - zl + zu;
+                const double t = gus[i] - a.dt * yn[i == 0 ? 5 : 4] - zl + zu;
                 red[0] = fmax(red[0], fabs(t));
                 red[8] += fabs(t);
                 if (c.hlu(i)) { const double sl = u[i] - c.ul[i]; red[2] = fmax(red[2], fabs(zl * sl)); red[3] += zl; red[4] += zl; lsum.add(sl); lorig.add(sl); }
                 if (c.huu(i)) { const double sl = c.uu[i] - u[i]; red[2] = fmax(red[2], fabs(zu * sl)); red[3] += zu; red[4] += zu; lsum.add(sl); lorig.add(sl); }
             }
+        if (pj >= 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c.B(B_D + r, pj, k) = pdv[r];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { c.S(S_GX + i, k) = gxs[i]; c.S(S_C + i, k) = ck[i]; }
+        if (k < N) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) c.S(S_GU + i, k) = gus[i];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) c.S(S_AJ + i, k) = dj[i];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) c.S(S_WD + i, k) = wd[i];
+        }
         const double cost = stage_cost(c, k, x, u);
         red[6] += rs ? objR : cost;
         red[7] += lsum.value();
