@@ -950,10 +950,32 @@ __host__ __device__ inline size_t obca_lds_bytes(int N) { return (size_t)(LA + L
 constexpr size_t kObcaLdsMax = 150 * 1024;  // dynamic LDS budget for the staged sweeps (+ static Shared)
 
 // all threads: copy the sweep inputs of every stage into region A (field-major reads: coalesced in k)
+// Copy F stage fields of every stage into an LDS record array A[k * F + f] (value(f, k) reads the workspace):
+// eight loads per thread are in flight before their LDS stores, instead of one load waited for per element.
+template <int F, class Val>
+__device__ __forceinline__ void stage_copy(const Ctx& c, double* A, Val value) {
+    const int NP = c.NP, tot = F * NP;
+    for (int base = threadIdx.x; base < tot; base += 8 * T) {
+        double v[8];
+        int d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int idx = base + u * T;
+            d[u] = -1;
+            v[u] = 0.0;
+            if (idx < tot) {
+                const int f = idx / NP, k = idx - f * NP;
+                d[u] = k * F + f;
+                v[u] = value(f, k);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (d[u] >= 0) A[d[u]] = v[u];
+    }
+}
 __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
-    const int NP = c.NP;
-    for (int idx = threadIdx.x; idx < LA * NP; idx += T) {
-        const int f = idx / NP, k = idx - f * NP;
+    stage_copy<LA>(c, A, [&](int f, int k) -> double {
         int g;
         if (f < 21) g = S_QT + f;
         else if (f < 27) g = S_QV + f - 21;
@@ -961,8 +983,8 @@ __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
         else if (f < 32) g = S_RV + f - 30;
         else if (f < 41) g = S_AJ + f - 32;
         else g = S_CE + f - 41;
-        A[k * LA + f] = (k < c.N || (f < 27 || f >= 41)) ? c.S(g, k) : 0.0;
-    }
+        return (k < c.N || (f < 27 || f >= 41)) ? (double)c.S(g, k) : 0.0;
+    });
 }
 
 // ======== phase: Riccati backward sweep (wave 0).  Sets sh.flag = 1 if an input block is not PD ========
@@ -1198,9 +1220,7 @@ struct SoftG {
     __device__ double SD(int i, int k) const { return c.S(S_SD + i, k); }
 };
 __device__ __noinline__ void stage_soft_inputs(const Ctx& c, double* A) {
-    const int NP = c.NP;
-    for (int idx = threadIdx.x; idx < LAS * NP; idx += T) {
-        const int f = idx / NP, k = idx - f * NP;
+    stage_copy<LAS>(c, A, [&](int f, int k) -> double {
         int g;
         if (f < 21) g = S_QT + f;
         else if (f < 27) g = S_QV + f - 21;
@@ -1209,8 +1229,8 @@ __device__ __noinline__ void stage_soft_inputs(const Ctx& c, double* A) {
         else if (f < 41) g = S_AJ + f - 32;
         else if (f < 47) g = S_CE + f - 41;
         else g = S_SD + f - 47;
-        A[k * LAS + f] = (k < c.N || f < 27 || f >= 41) ? c.S(g, k) : 0.0;
-    }
+        return (k < c.N || f < 27 || f >= 41) ? (double)c.S(g, k) : 0.0;
+    });
 }
 // operands of one soft stage: the softening of stage k (S entries of the lane) and the hard step k-1
 struct SoftOps {
@@ -1388,9 +1408,7 @@ struct SoftFG {
     __device__ double CR(int i, int k) const { return c.S(S_CE + i, k); }
 };
 __device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A) {
-    const int NP = c.NP;
-    for (int idx = threadIdx.x; idx < LFS * NP; idx += T) {
-        const int f = idx / NP, k = idx - f * NP;
+    stage_copy<LFS>(c, A, [&](int f, int k) -> double {
         int g;
         if (f < 21) g = S_P + f;
         else if (f < 27) g = S_PV + f - 21;
@@ -1399,8 +1417,8 @@ __device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A) {
         else if (f < 62) g = S_Y + f - 41;
         else if (f < 71) g = S_AJ + f - 62;
         else g = S_CE + f - 71;
-        A[k * LFS + f] = (k < c.N || f < 27 || (f >= 41 && f < 62) || f >= 71) ? c.S(g, k) : 0.0;
-    }
+        return (k < c.N || f < 27 || (f >= 41 && f < 62) || f >= 71) ? (double)c.S(g, k) : 0.0;
+    });
 }
 template <class Src>
 __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf) {
@@ -1804,13 +1822,27 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
 }
 
 // ======== phase: second-order-correction residual r <- a_soc r + r(trial) ========
+// (both residual phases load every value before the stores that would precede it in program order -- their
+// waits would include those stores, one in-order vmcnt queue -- so a block's results are stored after the
+// next block's loads)
 __device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a_soc) {
     for (int k = (int)threadIdx.x; k <= c.N; k += T) {
+        double cr[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = a_soc * c.S(S_CR + i, k) + c.S(S_CT + i, k);
-        for (int j = 0; j < c.nbk; ++j)
+        for (int i = 0; i < 6; ++i) cr[i] = a_soc * c.S(S_CR + i, k) + c.S(S_CT + i, k);
+        double dr[4], nx[4];
+        auto blk = [&](int j, double* v) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) c.B(B_DR + r, j, k) = a_soc * c.B(B_DR + r, j, k) + c.B(B_DT + r, j, k);
+            for (int r = 0; r < 4; ++r) v[r] = a_soc * c.B(B_DR + r, j, k) + c.B(B_DT + r, j, k);
+        };
+        if (c.nbk > 0) blk(0, dr);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = cr[i];
+        for (int j = 0; j < c.nbk; ++j) {
+            if (j + 1 < c.nbk) blk(j + 1, nx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { c.B(B_DR + r, j, k) = dr[r]; dr[r] = nx[r]; }
+        }
         if (k == c.N && c.plan())
 #pragma unroll
             for (int i = 0; i < 6; ++i) sh.dfr[i] = a_soc * sh.dfr[i] + sh.dft[i];
@@ -1821,14 +1853,24 @@ __device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a
 __device__ __noinline__ void phase_resid(const Ctx& c, LShared& sh, bool zero) {
     const bool rs = sh.R != 0;
     for (int k = (int)threadIdx.x; k <= c.N; k += T) {
+        double cr[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i)
-            c.S(S_CR + i, k) = zero ? 0.0 : c.S(S_C + i, k) - (rs ? c.S(S_PR + i, k) - c.S(S_NR + i, k) : 0.0);
-        for (int j = 0; j < c.nbk; ++j)
+            cr[i] = zero ? 0.0 : c.S(S_C + i, k) - (rs ? c.S(S_PR + i, k) - c.S(S_NR + i, k) : 0.0);
+        double dr[4], nx[4];
+        auto blk = [&](int j, double* v) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                c.B(B_DR + r, j, k) = zero ? 0.0 : c.B(B_D + r, j, k) - c.B(B_S + r, j, k) -
-                                                       (rs ? c.B(B_PR + r, j, k) - c.B(B_NR + r, j, k) : 0.0);
+                v[r] = zero ? 0.0 : c.B(B_D + r, j, k) - c.B(B_S + r, j, k) - (rs ? c.B(B_PR + r, j, k) - c.B(B_NR + r, j, k) : 0.0);
+        };
+        if (c.nbk > 0) blk(0, dr);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = cr[i];
+        for (int j = 0; j < c.nbk; ++j) {
+            if (j + 1 < c.nbk) blk(j + 1, nx);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { c.B(B_DR + r, j, k) = dr[r]; dr[r] = nx[r]; }
+        }
         if (k == c.N && c.plan())
 #pragma unroll
             for (int i = 0; i < 6; ++i) sh.dfr[i] = zero ? 0.0 : sh.df[i] - sh.sf[i] - (rs ? sh.pf[i] - sh.nf[i] : 0.0);
