@@ -137,6 +137,8 @@ typedef struct {
     double *rsx, *rsu, *rsw, *rss, *rssf, *rsp, *rsn, *rrc, *rrd, *rrf; /* residuals of the un-condensed rows */
     double *sol;    /* refinement save area of the solution */
     double dw_cur;
+    int dbg;        /* diagnostics, read once per solve: 1 TTO_DEBUG, 2 TTO_DEBUG2, 4 TTO_CHECK */
+    double* cc;     /* refinement row-residual constants */
     double* mem;
 } ws_t;
 
@@ -354,6 +356,7 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->rsx, N1 * 6); TAKE(W->rsu, N * 2); TAKE(W->rsw, nb * 8); TAKE(W->rss, nb * 4); TAKE(W->rssf, 6);
     TAKE(W->rsp, nr); TAKE(W->rsn, nr); TAKE(W->rrc, N1 * 6); TAKE(W->rrd, nb * 4); TAKE(W->rrf, 6);
     TAKE(W->sol, N1 * 12 + N * 2 + nb * 16 + 12 + 2 * nr);
+    TAKE(W->cc, N1 * 6 + nb * 4 + 6);
 #undef TAKE
     W->mem = (double*)calloc(tot, sizeof(double));
     if (!W->mem) return -1;
@@ -1464,7 +1467,7 @@ static opterr_t opt_error(ws_t* W, double mu) {
     o.dinf = dinf;
     o.pinf = pinf;
     o.pderr = d1 + p1 + cm1;
-    if (getenv("TTO_DEBUG2")) {
+    if (W->dbg & 2) {
         double my_ = 0, mz = 0, mzw = 0, mv = 0;
         for (int i = 0; i < W->nrc; ++i) my_ = fmax(my_, fabs(W->yc[i]));
         double myd = 0; for (int i = 0; i < W->nrd; ++i) myd = fmax(myd, fabs(W->yd[i]));
@@ -2085,7 +2088,7 @@ static void refined_solve(ws_t* W, double mu, double* cres, double* dres, double
     const size_t N1 = (size_t)N + 1, nb = (size_t)W->nb, nr = (size_t)W->nrow;
     double bnorm = 0.0;
     double res = newton_resid(W, mu, cres, dres, fres, &bnorm);
-    double* cc = (double*)malloc((N1 * 6 + nb * 4 + 6) * sizeof(double));
+    double* cc = W->cc;
     for (int it = 0; it < 10; ++it) {
         double snorm = 0.0;
         for (size_t i = 0; i < N1 * 6; ++i) snorm = fmax(snorm, fmax(fabs(W->dx[i]), fabs(W->ycp[i])));
@@ -2118,7 +2121,6 @@ static void refined_solve(ws_t* W, double mu, double* cres, double* dres, double
         }
         res = res2;
     }
-    free(cc);
 }
 
 /* Newton step with inertia correction into dx..; 0 on success */
@@ -2137,7 +2139,7 @@ static int newton(ws_t* W, ipm_state_t* S, double* dw_out) {
     memcpy(W->cr, W->rc0, (size_t)W->nrc * 8);
     memcpy(W->dr, W->rd0, (size_t)W->nrd * 8);
     refined_solve(W, S->mu, W->cr, W->dr, W->rf0);
-    if (getenv("TTO_CHECK")) check_newton(W, S->mu, dw);
+    if (W->dbg & 4) check_newton(W, S->mu, dw);
     mult_steps(W, S->mu);
     return 0;
 }
@@ -2278,7 +2280,7 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double* th0p, double*
     if (accepted && !ftype) add_filter(&S->F, (1.0 - g_th) * th0, phi0 - g_ph * th0);
     if (accepted) S->wd_short = nsteps > 0 ? S->wd_short + 1 : 0;
     g_dbg_ap = ap; g_dbg_acc = accepted; g_dbg_sw = Dm;
-    if (getenv("TTO_DEBUG")) {
+    if (W->dbg & 1) {
         double c[7];
         ftb_classes(W, tau, c);
         fprintf(stderr, "     ftb x %.1e u %.1e w %.1e s %.1e sf %.1e p %.1e n %.1e\n", c[0], c[1], c[2], c[3], c[4], c[5], c[6]);
@@ -2314,7 +2316,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     W->lsq = 0;
     W->have_acc = 0;
     W->kd = (P->opts & TTO_OPT_KAPPA_D) ? KAPPA_D : 0.0;
-    const int dbg = getenv("TTO_DEBUG") != NULL;
+    W->dbg = (getenv("TTO_DEBUG") ? 1 : 0) | (getenv("TTO_DEBUG2") ? 2 : 0) | (getenv("TTO_CHECK") ? 4 : 0);
+    const int dbg = W->dbg & 1;
     const int use_resto = !(P->opts & TTO_OPT_NO_RESTO), use_soft = !(P->opts & TTO_OPT_NO_SOFT_RESTO);
     /* weights, bounds (bound_relax_factor 1e-8 on every finite bound) */
     for (int i = 0; i < 6; ++i)
