@@ -85,8 +85,25 @@ def spawn_ranks(args):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    return next((c for c in codes if c != 0), 0)
+    # poll every rank: the first failure terminates the others (a rank left waiting in a collective or the
+    # rendezvous for a dead peer would otherwise hang until the process-group timeout)
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = next((c for c in codes if c not in (None, 0)), None)
+        if bad is not None:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad
+        if all(c == 0 for c in codes):
+            return 0
+        time.sleep(0.2)
 
 
 def cpu_baseline(cfg, B, N, seed, budget_s):

@@ -51,8 +51,11 @@ constexpr int kObcaThreads = 256;  // one workgroup (4 waves) per instance
 constexpr int kObcaMaxFilter = 64;
 enum { OBCA_PLAN = 0, OBCA_TRACK = 1 };
 
-// ObcaArgs::opts bits (diagnostics; 0 = IPOPT's algorithm): the same switches as the oracle's TTO_OPT_*
-enum { OBCA_OPT_NO_RESTO = 1, OBCA_OPT_NO_SOFT_RESTO = 2, OBCA_OPT_NO_LSQ_MULT = 4 };
+// ObcaArgs::opts bits (diagnostics / A-B builds; 0 = IPOPT's algorithm): the same switches as the oracle's TTO_OPT_*
+// (PD_BLOCKS: round 2's positive-definite block test instead of the exact block inertia; NO_REFINE: no iterative
+// refinement)
+enum { OBCA_OPT_NO_RESTO = 1, OBCA_OPT_NO_SOFT_RESTO = 2, OBCA_OPT_NO_LSQ_MULT = 4, OBCA_OPT_PD_BLOCKS = 32,
+       OBCA_OPT_NO_REFINE = 64 };
 
 struct ObcaArgs {
     int N, M, B, mode, max_iter, acc_iter, dual_init, opts;
@@ -74,12 +77,12 @@ struct ObcaArgs {
     double* ws;                     // per-instance workspace, obca_ws_doubles(N, M) each
     unsigned long long* stamps;     // [B][kObcaPhases] cycle sums (diagnostics), or nullptr
 };
-enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_TOTAL,
+enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_REFINE, OPH_TOTAL,
        kObcaPhases };
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
-constexpr int kObcaStageFields = 339;
-constexpr int kObcaBlockFields = 276;
+constexpr int kObcaStageFields = 353;
+constexpr int kObcaBlockFields = 288;
 __host__ __device__ inline size_t obca_ws_doubles(int N, int M) {
     return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
 }

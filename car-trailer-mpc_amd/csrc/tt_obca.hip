@@ -48,15 +48,19 @@ constexpr int MAX_SOFT_RESTO = 10;             // max_soft_resto_iters
 enum : int {
     S_X = 0, S_U = 6, S_ZLX = 8, S_ZUX = 14, S_ZLU = 20, S_ZUU = 22, S_YC = 24,
     S_GX = 30, S_GU = 36, S_C = 38, S_AJ = 44, S_WD = 53, S_QT = 60, S_QV = 81, S_RT = 87, S_RV = 90,
-    S_P = 92, S_PV = 113, S_K = 119, S_KF = 131, S_GI = 133, S_H = 136, S_DX = 148, S_DU = 160, S_YCP = 164,
-    S_CT = 176, S_CR = 182,
+    S_P = 92, S_PV = 113, S_K = 119, S_KF = 131, S_GI = 133,
+    // iterative refinement: the elastic-pair constants of the correction solve (dynamics rows; restoration phase)
+    S_OP = 136, S_ON = 142,
+    // step buffers: 0 the Newton step, 1 the second-order correction, 2 (dx, du, y+ only) a refinement correction
+    S_DX = 148, S_DU = 166, S_YCP = 172,
+    S_CT = 190, S_CR = 196,
     // restoration phase: elastic pairs of the 6 dynamics rows of the stage (and their steps, 2 buffers),
     // S = sqrt(E) of those rows, Y = S M^-1 S of the soft Riccati, the effective row residual, the
     // reference point and D_R^2, the saved original bound multipliers, the stored acceptable point and the
     // soft-restoration snapshot (x u zLx zUx zLu zUu yc)
-    S_PR = 188, S_NR = 194, S_ZP = 200, S_ZN = 206, S_DP = 212, S_DN = 224, S_SD = 236, S_Y = 242,
-    S_CE = 263, S_XR = 269, S_UR = 275, S_DRX = 277, S_DRU = 283, S_SZ = 285, S_XACC = 301, S_UACC = 307,
-    S_SNAP = 309, S_END = 339
+    S_PR = 202, S_NR = 208, S_ZP = 214, S_ZN = 220, S_DP = 226, S_DN = 238, S_SD = 250, S_Y = 256,
+    S_CE = 277, S_XR = 283, S_UR = 289, S_DRX = 291, S_DRU = 297, S_SZ = 299, S_XACC = 315, S_UACC = 321,
+    S_SNAP = 323, S_END = 353
 };
 static_assert(S_END == kObcaStageFields, "stage field count");
 enum : int {
@@ -66,9 +70,12 @@ enum : int {
     // D_R^2, saved multipliers, acceptable point, soft-restoration snapshot (w zw s vL vU yd)
     B_PR = 76, B_NR = 80, B_ZP = 84, B_ZN = 88, B_DP = 92, B_DN = 100, B_WR = 108, B_DRW = 116, B_SR = 124,
     B_SZW = 128, B_SVL = 136, B_SVU = 140, B_WACC = 144, B_SNAP = 152,
+    // iterative refinement: slack and elastic-pair constants of the correction solve (read by its recovery)
+    B_OS = 184, B_OP = 188, B_ON = 192,
     // the block's elimination as phase_factor left it (read back by phase_recover instead of refactoring):
     // G 16 | LT 10 | LL 10 | 1/dm 4 | zf_lam 4 | t 4 | Zl 16 | Yl 16 | fw 8 | D 4
-    B_FR = 184, B_END = 276
+    // (LL and LT keep S_j / L_jj on their diagonals: the signs of the signed LDL' pivots)
+    B_FR = 196, B_END = 288
 };
 enum : int { FR_G = 0, FR_LT = 16, FR_LL = 26, FR_IDM = 36, FR_ZFL = 40, FR_T = 44, FR_ZL = 48, FR_YL = 64, FR_FW = 80,
              FR_D = 88, FR_END = 92 };
@@ -123,6 +130,8 @@ struct Shared {
     double sf[6], vLf[6], vUf[6], ydf[6], df[6], dsf[2][6], ydpf[2][6], dft[6], dfr[6], Dsf[6], Dfe[6], rf[6];
     // their restoration-phase elastic pairs, saved multipliers and the soft-restoration snapshot
     double pf[6], nf[6], zpf[6], znf[6], dpf[2][6], dnf[2][6], sfR[6], svLf[6], svUf[6], snapf[24];
+    // iterative refinement: the final rows' slack / elastic-pair constants of the correction solve
+    double osf[6], opf[6], onf[6];
     // filters: [0] original problem, [1] restoration problem
     double fth[2][kObcaMaxFilter], fph[2][kObcaMaxFilter];
     int nfl[2];
@@ -201,6 +210,8 @@ struct Ctx {
     double* lds;  // dynamic LDS for the staged sweeps, or nullptr (sweeps read the HBM workspace)
     __attribute__((address_space(3))) double* slab;  // block-phase slabs (dynamic LDS, kSlab x T; thread t at slab + t)
     int N, NP, nbk, tid, b;
+    bool pd;                // round 2's positive-definite block test instead of the exact block inertia (A/B)
+    bool refine;            // IPOPT's iterative refinement of every step solve
     double dt;
     double xl[6], xu[6], ul[2], uu[2];
     int hx, hu;             // bit i: finite lower (i) / upper (8+i) bound
@@ -343,42 +354,60 @@ struct Blk {
     double E[4];                     // E of the 4 rows: 1/D (+ 1/D_p + 1/D_n in the restoration phase)
 };
 
-__device__ __forceinline__ bool chol4(double* L) {
+// Signed LDL' of a packed lower 4x4, A = L S L' (S = diag(+-1), |L_jj| = sqrt|d_j|, no pivoting; the oracle's
+// schol).  The diagonal keeps S_j / L_jj: the solves multiply by its magnitude and read S_j from its sign.  Returns
+// the number of negative pivots, or -1 on a (numerically) zero pivot; with pd a negative pivot fails too (round 2's
+// positive-definite test).  On a positive definite matrix every operation is the plain Cholesky's (S = 1 exactly).
+__device__ __forceinline__ double sgn(double d) { return copysign(1.0, d); }
+__device__ __forceinline__ int schol4(double* L, bool pd) {
+    int neg = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        double s = L[lo4(j, j)];
+        const double ajj = L[lo4(j, j)];
+        double s = ajj;
 #pragma unroll
-        for (int k = 0; k < j; ++k) s -= L[lo4(j, k)] * L[lo4(j, k)];
-        if (!(s > 0.0)) return false;
-        const double ir = frcp(sqrt(s));
-        L[lo4(j, j)] = ir;  // the factor keeps 1/L_jj on its diagonal: the solves multiply
+        for (int k = 0; k < j; ++k) s = fma(-(L[lo4(j, k)] * sgn(L[lo4(k, k)])), L[lo4(j, k)], s);
+        if (!(s > 0.0) && (pd || !(s < -1e-14 * fabs(ajj)))) return -1;
+        const double sj = s > 0.0 ? 1.0 : -1.0;
+        neg += s < 0.0 ? 1 : 0;
+        const double ir = frcp(sqrt(fabs(s)));
+        L[lo4(j, j)] = sj * ir;
 #pragma unroll
         for (int i = j + 1; i < 4; ++i) {
             double t = L[lo4(i, j)];
 #pragma unroll
-            for (int k = 0; k < j; ++k) t -= L[lo4(i, k)] * L[lo4(j, k)];
-            L[lo4(i, j)] = t * ir;
+            for (int k = 0; k < j; ++k) t = fma(-(L[lo4(i, k)] * sgn(L[lo4(k, k)])), L[lo4(j, k)], t);
+            L[lo4(i, j)] = (t * ir) * sj;
         }
     }
-    return true;
+    return neg;
 }
+// b <- L^-1 b
 __device__ __forceinline__ void fsub4(const double* L, double* b) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         double t = b[i];
 #pragma unroll
         for (int k = 0; k < i; ++k) t -= L[lo4(i, k)] * b[k];
-        b[i] = t * L[lo4(i, i)];
+        b[i] = t * fabs(L[lo4(i, i)]);
     }
 }
+// b <- L^-T b
 __device__ __forceinline__ void bsub4(const double* L, double* b) {
 #pragma unroll
     for (int i = 3; i >= 0; --i) {
         double t = b[i];
 #pragma unroll
         for (int k = i + 1; k < 4; ++k) t -= L[lo4(k, i)] * b[k];
-        b[i] = t * L[lo4(i, i)];
+        b[i] = t * fabs(L[lo4(i, i)]);
     }
+}
+// b <- (L S L')^-1 b
+__device__ __forceinline__ void ssolve4(const double* L, double* b) {
+    fsub4(L, b);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] *= sgn(L[lo4(i, i)]);
+    bsub4(L, b);
 }
 
 __device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& tr, int j, const double* w, const double* y,
@@ -451,17 +480,24 @@ __device__ __forceinline__ double jwm(const Blk& k, int r, int a) {
     return 0.0;
 }
 
-// elimination of a linearised block: returns false when the lam block is not positive definite.
+// elimination of a linearised block.  Inertia (IPOPT tests the whole KKT matrix; oracle/c/tt_obca.c:block_factor):
+// by Haynsworth the block [[A, Jw'], [Jw, -E]] has the inertia (8, 4, 0) iff T = E + Jw A^-1 Jw' has as many
+// negative pivots as A; the mu part of A is a positive diagonal, so A's negative pivots are those of the lam block
+// LL.  Returns false when the test fails (with pd: when LL or T is not positive definite, round 2's test).
 // sig_w: diagonal Hessian of the 8 duals (Sigma_w, plus zeta D_R^2 in the restoration phase); E: the rows'
-// dual regularisation (1/D, plus 1/D_p + 1/D_n in the restoration phase).  Adds the Schur complement into the
-// stage Hessian contribution C (10 packed lower entries over X,Y,theta,psi).
-__device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double dw, double* C) {
+// dual regularisation (1/D, plus 1/D_p + 1/D_n in the restoration phase).  Adds the Schur complement
+// W_xx - Z' S_A Z + G' T^-1 G into the stage Hessian contribution C (10 packed lower entries over X,Y,theta,psi).
+__device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double dw, double* C, bool pd) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         k.idm[i] = frcp(sig_w[i] + dw);
         k.LL[lo4(i, i)] += sig_w[4 + i] + dw;
     }
-    if (!chol4(k.LL)) return false;
+    const int negA = schol4(k.LL, pd);
+    if (negA < 0) return false;
+    double SA[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) SA[a] = sgn(k.LL[lo4(a, a)]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         double col[4];
@@ -487,7 +523,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int s = 0; s <= r; ++s) {
             double t = (r == s) ? k.E[r] : 0.0;
 #pragma unroll
-            for (int a = 0; a < 4; ++a) t += jwm(k, r, a) * jwm(k, s, a) * idm[a] + k.Yl(a, r) * k.Yl(a, s);
+            for (int a = 0; a < 4; ++a) t += jwm(k, r, a) * jwm(k, s, a) * idm[a] + (k.Yl(a, r) * SA[a]) * k.Yl(a, s);
             k.LT[lo4(r, s)] = t;
         }
 #pragma unroll
@@ -496,10 +532,10 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int q = 0; q < 4; ++q) {
             double g = -jx(k, r, q);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) g += k.Yl(a, r) * k.Zl(a, q);
+            for (int a = 0; a < 4; ++a) g += (k.Yl(a, r) * SA[a]) * k.Zl(a, q);
             k.G(r, q) = g;
         }
-    if (!chol4(k.LT)) return false;
+    if (schol4(k.LT, pd) != negA) return false;
     double Wm[4][4];  // LT^-1 G
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -515,15 +551,16 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
         for (int q = 0; q <= p; ++q) {
             double t = hxx[p][q];
 #pragma unroll
-            for (int a = 0; a < 4; ++a) t += Wm[a][p] * Wm[a][q] - k.Zl(a, p) * k.Zl(a, q);
+            for (int a = 0; a < 4; ++a)
+                t += (Wm[a][p] * sgn(k.LT[lo4(a, a)])) * Wm[a][q] - (k.Zl(a, p) * SA[a]) * k.Zl(a, q);
             C[lo4(p, q)] += t;
         }
     return true;
 }
 
-// right-hand side of a factored block.  fw: barrier gradient of the 8 duals; rd: row residual
-// (d - s) + D^-1 grad phi_s.  Returns zf (L^-1-scaled dual gradient: mu part fw/dm, lam part LL^-1 fw),
-// t = T^-1 h, and adds the gradient contribution into q4.
+// right-hand side of a factored block.  fw: gradient constants of the 8 duals; rd: row constant
+// (d - s) + D^-1 grad phi_s.  Returns zf (mu part fw/dm, lam part LL^-1 fw), t = T^-1 h, and adds the gradient
+// contribution -(Z' S_A zl + G' t) into q4.
 __device__ __forceinline__ void blk_rhs(const Blk& k, const double* fw, const double* rd, double* zf, double* t, double* q4) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) zf[a] = fw[a] * k.idm[a];
@@ -531,27 +568,29 @@ __device__ __forceinline__ void blk_rhs(const Blk& k, const double* fw, const do
     fsub4(k.LL, zl);
 #pragma unroll
     for (int a = 0; a < 4; ++a) zf[4 + a] = zl[a];
+    double szl[4];  // S_A zl
+#pragma unroll
+    for (int a = 0; a < 4; ++a) szl[a] = zl[a] * sgn(k.LL[lo4(a, a)]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         double h = rd[r];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) h -= jwm(k, r, a) * zf[a] + k.Yl(a, r) * zl[a];
+        for (int a = 0; a < 4; ++a) h -= jwm(k, r, a) * zf[a] + k.Yl(a, r) * szl[a];
         t[r] = h;
     }
-    fsub4(k.LT, t);
-    bsub4(k.LT, t);
+    ssolve4(k.LT, t);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         double g = 0.0;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) g -= k.Zl(a, p) * zl[a];
+        for (int a = 0; a < 4; ++a) g -= k.Zl(a, p) * szl[a];
 #pragma unroll
         for (int r = 0; r < 4; ++r) g -= k.G(r, p) * t[r];
         q4[p] += g;
     }
 }
 
-// recovery: y+ = t - T^-1 G dx^, dw_mu = -(fw_mu + Jw_mu' y+)/dm, dw_lam = -L^-T (zl + Z dx^ + Y y+)
+// recovery: y+ = t - T^-1 G dx^, dw_mu = -(fw_mu + Jw_mu' y+)/dm, dw_lam = -L^-T S_A (zl + Z dx^ + Y y+)
 __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, const double* zf, const double* t,
                                             const double* dxh, double* yp, double* dwv) {
     double g4[4];
@@ -562,8 +601,7 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
         for (int q = 0; q < 4; ++q) s += k.G(r, q) * dxh[q];
         g4[r] = s;
     }
-    fsub4(k.LT, g4);
-    bsub4(k.LT, g4);
+    ssolve4(k.LT, g4);
 #pragma unroll
     for (int r = 0; r < 4; ++r) yp[r] = t[r] - g4[r];
 #pragma unroll
@@ -581,7 +619,7 @@ __device__ __forceinline__ void blk_recover(const Blk& k, const double* fw, cons
         for (int q = 0; q < 4; ++q) s += k.Zl(a, q) * dxh[q];
 #pragma unroll
         for (int r = 0; r < 4; ++r) s += k.Yl(a, r) * yp[r];
-        v[a] = s;
+        v[a] = s * sgn(k.LL[lo4(a, a)]);
     }
     bsub4(k.LL, v);
 #pragma unroll
@@ -757,7 +795,7 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, con
             rd[r] += t.gp / t.Dp - t.gn / t.Dn;
         }
     }
-    if (!blk_factor(bk, sw, dw, C4)) return false;
+    if (!blk_factor(bk, sw, dw, C4, c.pd)) return false;
     blk_rhs(bk, fw, rd, zf, t4, q4);
     return true;
 }
@@ -910,6 +948,7 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
 // staged by all four waves before the sweep (LSrc: region A = sweep inputs, region B = its outputs).
 // CR is the effective dynamics-row residual S_CE.
 struct GSrc {
+    static constexpr bool kLds = false;
     const Ctx& c;
     __device__ double QT(int i, int k) const { return c.S(S_QT + i, k); }
     __device__ double QV(int i, int k) const { return c.S(S_QV + i, k); }
@@ -929,6 +968,7 @@ struct GSrc {
 // region A per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CR 6  (47);  region B: P 21 | PV 6 | K 12 | KF 2 (41)
 constexpr int LA = 47, LB = 41;
 struct LSrc {
+    static constexpr bool kLds = true;
     const lds_double* A;
     lds_double* B;
     __device__ double QT(int i, int k) const { return A[k * LA + i]; }
@@ -1042,10 +1082,13 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
     // the two tiles as LDS-addressed arrays (ds_read / ds_write, not flat accesses through `sh`)
     __shared__ __attribute__((aligned(16))) double P[48];   // P_{k+1}, row-major, row stride 8
     __shared__ __attribute__((aligned(16))) double PT[48];  // PA transposed: PT[8 j + r] = PA[r][j]
+    // with refinement the factorisation (P, K, G^-1) also goes to the HBM workspace: the correction solves reuse it
+    const bool keep = Src::kLds && c.refine;
     if (act) {
         const double q = src.QT(sij, N);
         P[8 * i + j] = q;
         if (i <= j) src.setP(sij, N, q);
+        if (keep && i <= j) c.S(S_P + sij, N) = q;
     }
     double pv = vec ? src.QV(r, N) : 0.0;
     if (vec) src.setPV(r, N, pv);
@@ -1106,16 +1149,20 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
         if (act) {
             P[8 * i + j] = Pk;
             if (i <= j) src.setP(sij, k, Pk);
+            if (keep && i <= j) c.S(S_P + sij, k) = Pk;
         }
         if (vec) {
             const double H0 = dt * hi.y, H1 = dt * hi.x;
-            src.setK(r, k, -fma(Gi00, H0, Gi01 * H1));
-            src.setK(6 + r, k, -fma(Gi01, H0, Gi11 * H1));
+            const double K0 = -fma(Gi00, H0, Gi01 * H1), K1 = -fma(Gi01, H0, Gi11 * H1);
+            src.setK(r, k, K0);
+            src.setK(6 + r, k, K1);
             src.setPV(r, k, pnew);
+            if (keep) { c.S(S_K + r, k) = K0; c.S(S_K + 6 + r, k) = K1; }
         }
         if (lane == 0) {
             src.setKF(0, k, kf0);
             src.setKF(1, k, kf1);
+            if (c.refine) { c.S(S_GI, k) = Gi00; c.S(S_GI + 1, k) = Gi01; c.S(S_GI + 2, k) = Gi11; }
         }
         pv = pnew;
         asm volatile("" ::: "memory");
@@ -1363,6 +1410,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         if (lane == 0) {
             out.setKF(0, kk, kf0);
             out.setKF(1, kk, kf1);
+            if (c.refine) { c.S(S_GI, kk) = Gi00; c.S(S_GI + 1, kk) = Gi01; c.S(S_GI + 2, kk) = Gi11; }
         }
         if (act && i <= j) out.setP(sij, kk, Pk);
         lds_order();
@@ -1407,8 +1455,9 @@ struct SoftFG {
     __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
     __device__ double CR(int i, int k) const { return c.S(S_CE + i, k); }
 };
-__device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A) {
+__device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A, bool soft = true) {
     stage_copy<LFS>(c, A, [&](int f, int k) -> double {
+        if (!soft && f >= 41 && f < 62) return 0.0;  // hard rows: Y unused
         int g;
         if (f < 21) g = S_P + f;
         else if (f < 27) g = S_PV + f - 21;
@@ -2464,6 +2513,612 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
     return true;
 }
 
+// ================= IPOPT's iterative refinement (PDFullSpaceSolver; oracle/c/tt_obca.c:refined_solve) =================
+// Every step solve is followed by at least one refinement step on the un-condensed primal-dual system: the residual
+// r of every Newton row at the computed step (phase_nres), a correction solve K e = -r through the same
+// factorisation (the block record, P, K, G^-1, Y), step += e; stop when max|r| <= 1e-10 (min(|sol|, 1e6) + |rhs|)
+// after the first step, when r stops decreasing (residual_improvement_factor 1) or after 10 steps.
+
+// ---- correction solve, backward: vector-only Riccati sweep over the stored factorisation (wave 0) ----
+// Per stage k = N..1 (A = I + D, B = dt [e5 e4]):
+//   s = p_k - P_k c_k,  p' = s - P_k Y_k s  (= p~_k - P~_k c_k of the soft sweep; Y = 0 outside the restoration phase),
+//   g = r_{k-1} + B'p',  kf_{k-1} = -G^-1 g,  p_{k-1} = q_{k-1} + A'p' + K'g   (K'g = H' kf)
+// P_k c_k and P_k Y_k do not depend on the recursion: all four waves stage them per stage (record LV) before the
+// sweep, so the serial chain is one 6x6 product (restoration only) plus the sparse A' and K' products, carried
+// redundantly by every lane; lanes 0..5 / lane 0 store p / kf for the forward sweep.
+constexpr int LV = 74;  // W = P c 6 | PY 36 | QV 6 | RV 2 | GI 3 | K 12 | AJ 9
+struct VecL {
+    const lds_double* A;
+    __device__ double W(int i, int k) const { return A[k * LV + i]; }
+    __device__ double PY(int i, int j, int k) const { return A[k * LV + 6 + 6 * i + j]; }
+    __device__ double QV(int i, int k) const { return A[k * LV + 42 + i]; }
+    __device__ double RV(int i, int k) const { return A[k * LV + 48 + i]; }
+    __device__ double GI(int i, int k) const { return A[k * LV + 50 + i]; }
+    __device__ double K(int i, int k) const { return A[k * LV + 53 + i]; }
+    __device__ double AJ(int i, int k) const { return A[k * LV + 65 + i]; }
+};
+// the same operands straight from the HBM workspace (horizons whose records do not fit the LDS budget)
+struct VecG {
+    const Ctx& c;
+    __device__ double W(int i, int k) const {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) t = fma((double)c.S(S_P + sy6(i, l), k), (double)c.S(S_CE + l, k), t);
+        return t;
+    }
+    __device__ double PY(int i, int j, int k) const {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < 6; ++l) t = fma((double)c.S(S_P + sy6(i, l), k), (double)c.S(S_Y + sy6(l, j), k), t);
+        return t;
+    }
+    __device__ double QV(int i, int k) const { return c.S(S_QV + i, k); }
+    __device__ double RV(int i, int k) const { return c.S(S_RV + i, k); }
+    __device__ double GI(int i, int k) const { return c.S(S_GI + i, k); }
+    __device__ double K(int i, int k) const { return c.S(S_K + i, k); }
+    __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
+};
+__device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft) {
+    for (int k = (int)threadIdx.x; k <= c.N; k += T) {
+        lds_double* r = (lds_double*)A + (size_t)k * LV;
+        double P[21], e[6];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) P[i] = c.S(S_P + i, k);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) e[i] = c.S(S_CE + i, k);
+        double q[6], rv[2] = {0.0, 0.0}, gi[3] = {0.0, 0.0, 0.0}, kk[12], aj[9];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) q[i] = c.S(S_QV + i, k);
+        const bool st = k < c.N;
+#pragma unroll
+        for (int i = 0; i < 12; ++i) kk[i] = st ? (double)c.S(S_K + i, k) : 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) aj[i] = st ? (double)c.S(S_AJ + i, k) : 0.0;
+        if (st) {
+            rv[0] = c.S(S_RV, k); rv[1] = c.S(S_RV + 1, k);
+            gi[0] = c.S(S_GI, k); gi[1] = c.S(S_GI + 1, k); gi[2] = c.S(S_GI + 2, k);
+        }
+        double Y[21];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) Y[i] = soft ? (double)c.S(S_Y + i, k) : 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(P[sy6(i, l)], e[l], t);
+            r[i] = t;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double t = 0.0;
+                if (soft)
+#pragma unroll
+                    for (int l = 0; l < 6; ++l) t = fma(P[sy6(i, l)], Y[sy6(l, j)], t);
+                r[6 + 6 * i + j] = t;
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) r[42 + i] = q[i];
+        r[48] = rv[0]; r[49] = rv[1];
+        r[50] = gi[0]; r[51] = gi[1]; r[52] = gi[2];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) r[53 + i] = kk[i];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) r[65 + i] = aj[i];
+    }
+}
+template <class Src>
+__device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft) {
+    const int lane = threadIdx.x, N = c.N;
+    const double dt = c.dt;
+    const int r = lane < 6 ? lane : 0;
+    auto pick = [&](const double* v) {
+        double t = v[0];
+#pragma unroll
+        for (int q = 1; q < 6; ++q) t = r == q ? v[q] : t;
+        return t;
+    };
+    double p[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) p[q] = src.QV(q, N);
+    if (lane < 6) c.S(S_PV + r, N) = pick(p);
+    for (int k = N; k >= 1; --k) {
+        const int km = k - 1;
+        double sv[6], pp[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) sv[q] = p[q] - src.W(q, k);
+        if (soft) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                double t = sv[i];
+#pragma unroll
+                for (int l = 0; l < 6; ++l) t = fma(-src.PY(i, l, k), sv[l], t);
+                pp[i] = t;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) pp[q] = sv[q];
+        }
+        const double g0 = fma(dt, pp[5], src.RV(0, km)), g1 = fma(dt, pp[4], src.RV(1, km));
+        const double gi0 = src.GI(0, km), gi1 = src.GI(1, km), gi2 = src.GI(2, km);
+        const double kf0 = -fma(gi0, g0, gi1 * g1), kf1 = -fma(gi1, g0, gi2 * g1);
+        double dj[9], kk[12];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) dj[q] = src.AJ(q, km);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) kk[q] = src.K(q, km);
+        double np[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) np[q] = src.QV(q, km) + pp[q] + fma(kk[q], g0, kk[6 + q] * g1);
+        // D' p' (D: 0:(0,2) 1:(0,5) 2:(1,2) 3:(1,5) 4:(2,4) 5:(2,5) 6:(3,3) 7:(3,4) 8:(3,5))
+        np[2] += fma(dj[0], pp[0], dj[2] * pp[1]);
+        np[3] += dj[6] * pp[3];
+        np[4] += fma(dj[4], pp[2], dj[7] * pp[3]);
+        np[5] += fma(dj[1], pp[0], fma(dj[3], pp[1], fma(dj[5], pp[2], dj[8] * pp[3])));
+        if (lane < 6) c.S(S_PV + r, km) = pick(np);
+        if (lane == 0) { c.S(S_KF, km) = kf0; c.S(S_KF + 1, km) = kf1; }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) p[q] = np[q];
+    }
+}
+
+// ---- residuals of the un-condensed Newton rows at the step in buffer buf (+ the correction's right-hand side) ----
+// (oracle/c/tt_obca.c:newton_resid, and solve_rhs in override mode)  Rows and their constants: the stationarity of
+// x, u, the duals w, the slacks s, sf and the elastic pairs p, n (the barrier gradients), the linearised dynamics /
+// OBCA / final rows (the row residuals S_CR / B_DR / dfr of the solve).  With prep, the right-hand side of the
+// correction solve (phase_factor's rhs with the residuals as the constants): QV, RV, CE, the factor record's
+// fw / zf_lam / t, and the constants the recovery needs (B_OS, B_OP / B_ON, S_OP / S_ON, osf / opf / onf).
+// out: [0] max |residual| [1] max |constant| [2] max |dx, y+_c, dw| (the oracle's solution norm)
+//      [3] alpha_primal [4] alpha_dual [5] grad phi' d [6] max relative step  (of the step in buf: the line search's)
+__device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, bool prep,
+                                        double (&out)[7]) {
+    LArgs& a = *c.a;
+    const int N = c.N;
+    const bool plan = c.plan(), rs = sh.R != 0;
+    const double zeta = sh.zeta, dt = c.dt;
+    double rmax = 0.0, bmax = 0.0, snorm = 0.0, ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
+    auto R = [&](double v) { rmax = fmax(rmax, fabs(v)); return v; };
+    auto Bc = [&](double v) { bmax = fmax(bmax, fabs(v)); return v; };
+    auto dual = [&](double z, double dz) { if (dz < 0.0) az = fmin(az, -tau * z / dz); };
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+        const bool st = k < N;
+        double x[6], dx[6], yp[6], ypn[6] = {0, 0, 0, 0, 0, 0}, dj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, wd[7] = {0, 0, 0, 0, 0, 0, 0};
+        double u[2] = {0.0, 0.0}, du[2] = {0.0, 0.0};
+        load_x(c, k, x);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { dx[i] = c.S(S_DX + 6 * buf + i, k); yp[i] = c.S(S_YCP + 6 * buf + i, k); }
+        if (st) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ypn[i] = c.S(S_YCP + 6 * buf + i, k + 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) dj[i] = c.S(S_AJ + i, k);
+#pragma unroll
+            for (int i = 0; i < 7; ++i) wd[i] = c.S(S_WD + i, k);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { u[i] = c.S(S_U + i, k); du[i] = c.S(S_DU + 2 * buf + i, k); }
+        }
+        // ---- x rows (without the block terms, added below) ----
+        double rx[6];
+        const double sc = (k == N && plan) ? a.tfac : 1.0;
+        double Hd[21];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j2 = i; j2 < 6; ++j2) Hd[sy6(i, j2)] = rs ? 0.0 : sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
+        Hd[sy6(2, 2)] += wd[0]; Hd[sy6(2, 5)] += wd[1]; Hd[sy6(3, 3)] += wd[2]; Hd[sy6(3, 4)] += wd[3];
+        Hd[sy6(3, 5)] += wd[4]; Hd[sy6(4, 4)] += wd[5]; Hd[sy6(4, 5)] += wd[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double xv = x[i], d = dx[i];
+            double g = c.S(S_GX + i, k), sg = dw + (rs ? zeta * c.S(S_DRX + i, k) : 0.0);
+            rel = fmax(rel, fabs(d) / (1.0 + fabs(xv)));
+            if (c.hlx(i)) {
+                const double sl = xv - c.xl[i], z = c.S(S_ZLX + i, k);
+                g -= mu / sl;
+                sg += z / sl;
+                ftb_lo(xv, c.xl[i], d, tau, ap);
+                dual(z, mu / sl - z - z / sl * d);
+            }
+            if (c.hux(i)) {
+                const double sl = c.xu[i] - xv, z = c.S(S_ZUX + i, k);
+                g += mu / sl;
+                sg += z / sl;
+                ftb_hi(xv, c.xu[i], d, tau, ap);
+                dual(z, mu / sl - z + z / sl * d);
+            }
+            Dm += g * d;
+            double t = Bc(g) + sg * d + yp[i] - ypn[i];
+#pragma unroll
+            for (int j2 = 0; j2 < 6; ++j2) t += Hd[sy6(i, j2)] * dx[j2];
+            rx[i] = t;
+            snorm = fmax(snorm, fmax(fabs(d), fabs(yp[i])));
+        }
+        // -A'y+_{k+1}: the D' part
+        rx[2] -= dj[0] * ypn[0] + dj[2] * ypn[1];
+        rx[3] -= dj[6] * ypn[3];
+        rx[4] -= dj[4] * ypn[2] + dj[7] * ypn[3];
+        rx[5] -= dj[1] * ypn[0] + dj[3] * ypn[1] + dj[5] * ypn[2] + dj[8] * ypn[3];
+        // ---- u rows ----
+        double ru[2] = {0.0, 0.0};
+        if (st)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double uv = u[i], d = du[i];
+                double g = c.S(S_GU + i, k), sg = dw + (rs ? zeta * c.S(S_DRU + i, k) : 0.0);
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(uv)));
+                if (c.hlu(i)) {
+                    const double sl = uv - c.ul[i], z = c.S(S_ZLU + i, k);
+                    g -= mu / sl;
+                    sg += z / sl;
+                    ftb_lo(uv, c.ul[i], d, tau, ap);
+                    dual(z, mu / sl - z - z / sl * d);
+                }
+                if (c.huu(i)) {
+                    const double sl = c.uu[i] - uv, z = c.S(S_ZUU + i, k);
+                    g += mu / sl;
+                    sg += z / sl;
+                    ftb_hi(uv, c.uu[i], d, tau, ap);
+                    dual(z, mu / sl - z + z / sl * d);
+                }
+                Dm += g * d;
+                double t = Bc(g) + sg * d - dt * ypn[i == 0 ? 5 : 4];
+                if (!rs) t += (i == 0 ? 2.0 * a.R[0] * du[0] + (a.R[1] + a.R[2]) * du[1]
+                                      : (a.R[1] + a.R[2]) * du[0] + 2.0 * a.R[3] * du[1]);
+                ru[i] = R(t);
+            }
+        // ---- dynamics rows of stage k: c_k + dx_k - A_{k-1} dx_{k-1} - B du_{k-1} (- dp + dn) ----
+        double rc[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) rc[i] = Bc(c.S(S_CR + i, k)) + dx[i];
+        if (k > 0) {
+            double dxp[6], ajp[9];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dxp[i] = c.S(S_DX + 6 * buf + i, k - 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) ajp[i] = c.S(S_AJ + i, k - 1);
+            const double dup0 = c.S(S_DU + 2 * buf, k - 1), dup1 = c.S(S_DU + 2 * buf + 1, k - 1);
+            rc[0] -= dxp[0] + fma(ajp[0], dxp[2], ajp[1] * dxp[5]);
+            rc[1] -= dxp[1] + fma(ajp[2], dxp[2], ajp[3] * dxp[5]);
+            rc[2] -= dxp[2] + fma(ajp[4], dxp[4], ajp[5] * dxp[5]);
+            rc[3] -= dxp[3] + fma(ajp[6], dxp[3], fma(ajp[7], dxp[4], ajp[8] * dxp[5]));
+            rc[4] -= dxp[4] + dt * dup1;
+            rc[5] -= dxp[5] + dt * dup0;
+        }
+        double rpc[6] = {0, 0, 0, 0, 0, 0}, rnc[6] = {0, 0, 0, 0, 0, 0}, gpnc[6] = {0, 0, 0, 0, 0, 0};
+        if (rs)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
+                const double dp = c.S(S_DP + 6 * buf + i, k), dn = c.S(S_DN + 6 * buf + i, k);
+                rc[i] += -dp + dn;
+                const double Dp = zp / p + dw, Dn = zn / n + dw, gp = RHO - mu / p, gn = RHO - mu / n;
+                rpc[i] = R(Bc(gp) + Dp * dp - yp[i]);
+                rnc[i] = R(Bc(gn) + Dn * dn + yp[i]);
+                gpnc[i] = rpc[i] / Dp - rnc[i] / Dn;
+                ftb_lo(p, 0.0, dp, tau, ap);
+                ftb_lo(n, 0.0, dn, tau, ap);
+                dual(zp, mu / p - zp - zp / p * dp);
+                dual(zn, mu / n - zn - zn / n * dn);
+                Dm += gp * dp + gn * dn;
+                rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) R(rc[i]);
+        // ---- OBCA blocks ----
+        double q4[4] = {0, 0, 0, 0};
+        const Trig tr = stage_trig(x);
+        for (int j = 0; j < c.nbk; ++j) {
+            double w[8], zw[8], yd[4], sv[4], vl[4], vu[4], dres[4], dwv[8], ds[4], ydp[4];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); dwv[e] = c.B(B_DW + 8 * buf + e, j, k); }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                yd[r] = c.B(B_YD + r, j, k); sv[r] = c.B(B_S + r, j, k); vl[r] = c.B(B_VL + r, j, k);
+                vu[r] = c.B(B_VU + r, j, k); dres[r] = c.B(B_DR + r, j, k); ds[r] = c.B(B_DS + 4 * buf + r, j, k);
+                ydp[r] = c.B(B_YP + 4 * buf + r, j, k);
+            }
+            Blk bk;
+            bk.m = c.slab + threadIdx.x;
+            blk_lin(a, x, tr, j, w, yd, bk);
+            // x rows: W_xx dx + W_x lam dw_lam + Jx' y+
+            rx[2] += bk.hxx22 * dx[2] + bk.hxx23 * dx[3];
+            rx[3] += bk.hxx23 * dx[2] + bk.hxx33 * dx[3];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                double t = 0.0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t += bk.hxl[q][e] * dwv[4 + e];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) t += jx(bk, r, q) * ydp[r];
+                rx[q] += t;
+            }
+            // w rows
+            double rw[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const double sl = w[e] + RELAX, d = dwv[e];
+                double hw = 0.0, gw = -mu / sl;
+                if (rs) {
+                    hw = zeta * c.B(B_DRW + e, j, k);
+                    gw += hw * (w[e] - c.B(B_WR + e, j, k));
+                }
+                double t = Bc(gw) + (zw[e] / sl + dw + hw) * d;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * ydp[r];
+                if (e >= 4) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) t += bk.hxl[q][e - 4] * dx[q];
+#pragma unroll
+                    for (int b2 = 0; b2 < 4; ++b2) t += bk.LL[lo4(max(e - 4, b2), min(e - 4, b2))] * dwv[4 + b2];
+                }
+                rw[e] = R(t);
+                Dm += gw * d;
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(w[e])));
+                snorm = fmax(snorm, fabs(d));
+                ftb_lo(w[e], -RELAX, d, tau, ap);
+                dual(zw[e], mu / sl - zw[e] - zw[e] / sl * d);
+            }
+            // slack, row and elastic-pair rows
+            double rsl[4], rdv[4], rpv[4] = {0, 0, 0, 0}, rnv[4] = {0, 0, 0, 0}, Dpv[4] = {1, 1, 1, 1}, Dnv[4] = {1, 1, 1, 1};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double s = sv[r], d = ds[r];
+                const double gs = grad_row(c, r, s, mu);
+                rsl[r] = R(Bc(gs) + (sig_row(c, r, s, vl[r], vu[r]) + dw) * d - ydp[r]);
+                double t = Bc(dres[r]) - d;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) t += jx(bk, r, q) * dx[q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t += jwm(bk, r, e) * dwv[e] + jwl(bk, r, e) * dwv[4 + e];
+                if (rs) {
+                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k);
+                    const double zp = c.B(B_ZP + r, j, k), zn = c.B(B_ZN + r, j, k);
+                    const double dp = c.B(B_DP + 4 * buf + r, j, k), dn = c.B(B_DN + 4 * buf + r, j, k);
+                    t += -dp + dn;
+                    Dpv[r] = zp / p + dw;
+                    Dnv[r] = zn / n + dw;
+                    const double gp = RHO - mu / p, gn = RHO - mu / n;
+                    rpv[r] = R(Bc(gp) + Dpv[r] * dp - ydp[r]);
+                    rnv[r] = R(Bc(gn) + Dnv[r] * dn + ydp[r]);
+                    ftb_lo(p, 0.0, dp, tau, ap);
+                    ftb_lo(n, 0.0, dn, tau, ap);
+                    dual(zp, mu / p - zp - zp / p * dp);
+                    dual(zn, mu / n - zn - zn / n * dn);
+                    Dm += gp * dp + gn * dn;
+                    rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+                }
+                rdv[r] = R(t);
+                Dm += gs * d;
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(s)));
+                const double slu = c.rU(r) - s;
+                ftb_hi(s, c.rU(r), d, tau, ap);
+                dual(vu[r], mu / slu - vu[r] + vu[r] / slu * d);
+                if (c.hrl(r)) {
+                    const double sll = s - c.rL(r);
+                    ftb_lo(s, c.rL(r), d, tau, ap);
+                    dual(vl[r], mu / sll - vl[r] - vl[r] / sll * d);
+                }
+            }
+            if (prep) {
+                auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
+#pragma unroll
+                for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
+                double Dv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bk.idm[e] = ld(FR_IDM + e);
+                    Dv[e] = ld(FR_D + e);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) { bk.Zl(e, q) = ld(FR_ZL + 4 * e + q); bk.Yl(e, q) = ld(FR_YL + 4 * e + q); }
+                }
+                double rdc[4], zf[8], t4[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / Dv[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
+                blk_rhs(bk, rw, rdc, zf, t4, q4);
+                auto stf = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
+#pragma unroll
+                for (int e = 0; e < 8; ++e) stf(FR_FW + e, rw[e]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { stf(FR_ZFL + e, zf[4 + e]); stf(FR_T + e, t4[e]); }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    c.B(B_OS + r, j, k) = rsl[r];
+                    if (rs) { c.B(B_OP + r, j, k) = rpv[r]; c.B(B_ON + r, j, k) = rnv[r]; }
+                }
+            }
+        }
+        // ---- final rows (plan mode, stage N) ----
+        double qf[6] = {0, 0, 0, 0, 0, 0};
+        if (k == N && plan)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double s = sh.sf[i], d = sh.dsf[buf][i], ypf = sh.ydpf[buf][i];
+                rx[i] += ypf;
+                const double sl = s - c.fL, su = c.fU - s;
+                const double gs = -mu / sl + mu / su;
+                double rf = Bc(sh.dfr[i]) + dx[i] - d;
+                const double rsf = R(Bc(gs) + (sh.vLf[i] / sl + sh.vUf[i] / su + dw) * d - ypf);
+                double gpn = 0.0;
+                if (rs) {
+                    const double p = sh.pf[i], n = sh.nf[i], zp = sh.zpf[i], zn = sh.znf[i];
+                    const double dp = sh.dpf[buf][i], dn = sh.dnf[buf][i];
+                    rf += -dp + dn;
+                    const double Dp = zp / p + dw, Dn = zn / n + dw, gp = RHO - mu / p, gn = RHO - mu / n;
+                    const double rp = R(Bc(gp) + Dp * dp - ypf), rn = R(Bc(gn) + Dn * dn + ypf);
+                    gpn = rp / Dp - rn / Dn;
+                    if (prep) { sh.opf[i] = rp; sh.onf[i] = rn; }
+                    ftb_lo(p, 0.0, dp, tau, ap);
+                    ftb_lo(n, 0.0, dn, tau, ap);
+                    dual(zp, mu / p - zp - zp / p * dp);
+                    dual(zn, mu / n - zn - zn / n * dn);
+                    Dm += gp * dp + gn * dn;
+                    rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+                }
+                R(rf);
+                Dm += gs * d;
+                rel = fmax(rel, fabs(d) / (1.0 + fabs(s)));
+                ftb_lo(s, c.fL, d, tau, ap);
+                ftb_hi(s, c.fU, d, tau, ap);
+                dual(sh.vLf[i], mu / sl - sh.vLf[i] - sh.vLf[i] / sl * d);
+                dual(sh.vUf[i], mu / su - sh.vUf[i] + sh.vUf[i] / su * d);
+                if (prep) {
+                    const double rfp = rf + rsf / sh.Dsf[i] + gpn;
+                    sh.rf[i] = rfp;
+                    sh.osf[i] = rsf;
+                    qf[i] = sh.Dfe[i] * rfp;
+                }
+            }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) R(rx[i]);
+        if (prep) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                c.S(S_QV + i, k) = rx[i] + (i < 4 ? q4[i] : 0.0) + qf[i];
+                c.S(S_CE + i, k) = rc[i] + (rs ? gpnc[i] : 0.0);
+                if (rs) { c.S(S_OP + i, k) = rpc[i]; c.S(S_ON + i, k) = rnc[i]; }
+            }
+            if (st) { c.S(S_RV, k) = ru[0]; c.S(S_RV + 1, k) = ru[1]; }
+        }
+    }
+    out[0] = rmax; out[1] = bmax; out[2] = snorm; out[3] = ap; out[4] = az; out[5] = Dm; out[6] = rel;
+    const int ops[7] = {R_MAX, R_MAX, R_MAX, R_MIN, R_MIN, R_SUM, R_MAX};
+    wg_reduce(sh, out, ops);
+}
+
+// ---- correction solve, recovery: the blocks' y+, dw, ds (and the elastic-pair steps) of the correction in buffer 2,
+// with the constants phase_nres prepared; every component is added into the step in buffer buf ----
+__device__ __noinline__ void phase_recover_corr(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
+    const int N = c.N;
+    const bool plan = c.plan(), rs = sh.R != 0;
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+        double dx[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dx[i] = c.S(S_DX + 12 + i, k);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double ypc = c.S(S_YCP + 12 + i, k);
+            c.S(S_DX + 6 * buf + i, k) += dx[i];
+            c.S(S_YCP + 6 * buf + i, k) += ypc;
+            if (rs) {
+                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
+                c.S(S_DP + 6 * buf + i, k) += (ypc - c.S(S_OP + i, k)) / (zp / p + dw);
+                c.S(S_DN + 6 * buf + i, k) += (-ypc - c.S(S_ON + i, k)) / (zn / n + dw);
+            }
+        }
+        if (k < N) {
+            c.S(S_DU + 2 * buf, k) += c.S(S_DU + 4, k);
+            c.S(S_DU + 2 * buf + 1, k) += c.S(S_DU + 5, k);
+        }
+        for (int j = 0; j < c.nbk; ++j) {
+            Blk bk;
+            bk.m = c.slab + threadIdx.x;
+            double fw[8], zf[8], t4[4], yp[4], dwv[8], Dv[4];
+            auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
+#pragma unroll
+            for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                bk.idm[e] = ld(FR_IDM + e);
+                zf[4 + e] = ld(FR_ZFL + e);
+                t4[e] = ld(FR_T + e);
+                Dv[e] = ld(FR_D + e);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { bk.Zl(e, q) = ld(FR_ZL + 4 * e + q); bk.Yl(e, q) = ld(FR_YL + 4 * e + q); }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
+            const bool trailer = (j & 1) != 0;
+            bk.jw0[0] = bk.jw0[2] = 0.5 * (trailer ? c.a->L2 : c.a->L1);
+            bk.jw0[1] = bk.jw0[3] = 0.5 * (trailer ? c.a->W2 : c.a->W1);
+            blk_recover(bk, fw, zf, t4, dx, yp, dwv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) c.B(B_DW + 8 * buf + e, j, k) += dwv[e];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                c.B(B_YP + 4 * buf + r, j, k) += yp[r];
+                c.B(B_DS + 4 * buf + r, j, k) += (yp[r] - c.B(B_OS + r, j, k)) / Dv[r];
+                if (rs) {
+                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k);
+                    const double zp = c.B(B_ZP + r, j, k), zn = c.B(B_ZN + r, j, k);
+                    c.B(B_DP + 4 * buf + r, j, k) += (yp[r] - c.B(B_OP + r, j, k)) / (zp / p + dw);
+                    c.B(B_DN + 4 * buf + r, j, k) += (-yp[r] - c.B(B_ON + r, j, k)) / (zn / n + dw);
+                }
+            }
+        }
+        if (k == N && plan)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double ypf = sh.Dfe[i] * (dx[i] + sh.rf[i]);
+                sh.ydpf[buf][i] += ypf;
+                sh.dsf[buf][i] += (ypf - sh.osf[i]) / sh.Dsf[i];
+                if (rs) {
+                    sh.dpf[buf][i] += (ypf - sh.opf[i]) / (sh.zpf[i] / sh.pf[i] + dw);
+                    sh.dnf[buf][i] += (-ypf - sh.onf[i]) / (sh.znf[i] / sh.nf[i] + dw);
+                }
+            }
+    }
+}
+
+// the correction solve of one refinement step: right-hand side prepared by phase_nres (prep), vector-only sweeps
+// through the stored factorisation into buffer 2, recovery added into buffer buf
+__device__ __noinline__ void correction_solve(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
+    const bool soft = sh.R != 0;
+    if (c.lds) {
+        stage_vec_inputs(c, c.lds, soft);
+        __syncthreads();
+        if (threadIdx.x < 64) riccati_vec(c, VecL{(const lds_double*)c.lds}, soft);
+        __syncthreads();
+        stage_soft_forward(c, c.lds, soft);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            if (soft) forward_soft(c, SoftF{(const lds_double*)c.lds}, 2);
+            else forward(c, SoftF{(const lds_double*)c.lds}, 2);
+        }
+    } else {
+        if (threadIdx.x < 64) riccati_vec(c, VecG{c}, soft);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            if (soft) forward_soft(c, SoftFG{c}, 2);
+            else forward(c, SoftFG{c}, 2);
+        }
+    }
+    __syncthreads();
+    phase_recover_corr(c, sh, mu, dw, buf);
+    __syncthreads();
+}
+
+// iterative refinement of the step in buffer buf (factorisation and block recovery done).  rec: the line-search
+// quantities of the refined step (alpha_primal, alpha_dual, grad phi' d, max relative step), as phase_recover's
+__device__ __noinline__ void refine(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, double (&rec)[5]) {
+    const bool on = c.a->stamps != nullptr;
+    double q[7];
+    phase_nres(c, sh, mu, dw, tau, buf, true, q);
+    stamp(sh, on, OPH_REFINE);
+    double res = q[0];
+    const double bnorm = q[1];
+    for (int it = 0; it < 10; ++it) {
+        if (it >= 1 && res <= 1e-10 * (fmin(q[2], 1e6) + bnorm)) break;
+        __syncthreads();
+        correction_solve(c, sh, mu, dw, buf);
+        phase_nres(c, sh, mu, dw, tau, buf, true, q);
+        stamp(sh, on, OPH_REFINE);
+        const double res2 = q[0];
+        if (!(res2 < res)) { res = res2; break; }  // no improvement: IPOPT stops refining
+        res = res2;
+    }
+    __syncthreads();
+    rec[0] = q[3]; rec[1] = q[4]; rec[2] = q[5]; rec[3] = q[6];
+}
+
 // ======== restoration / soft-restoration / acceptable-point bookkeeping (all stage-parallel) ========
 // snapshot of the iterate (save = true) or its restore (soft restoration trial)
 __device__ __noinline__ void phase_snapshot(const Ctx& c, LShared& sh, bool save) {
@@ -2787,6 +3442,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     c.tid = threadIdx.x;
     c.ws = (gdouble*)(a.ws + (size_t)c.b * obca_ws_doubles(a.N, a.M));
     c.dt = a.dt;
+    c.pd = (a.opts & OBCA_OPT_PD_BLOCKS) != 0;
+    c.refine = (a.opts & OBCA_OPT_NO_REFINE) == 0;
     const int N = c.N, NBK = c.nbk, tid = c.tid;
     const bool plan = a.mode == OBCA_PLAN;
     c.tgt_x = plan ? a.xgoal + 6 * (size_t)c.b : a.xref + (size_t)c.b * 6 * (N + 1);
@@ -3036,6 +3693,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     double rec[5];
                     phase_recover(cs, sh, mu, dw, stt.tau, 0, rec);
                     stamp(sh, ston, OPH_REC);
+                    if (cs.refine) refine(cs, sh, mu, dw, stt.tau, 0, rec);
                     const double ap = rec[0], Dm = rec[2], rel = rec[3];
                     double az = rec[1], alpha = ap;
                     int buf = 0;
@@ -3080,6 +3738,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                                     double rs[5];
                                     phase_recover(cs, sh, mu, dw, stt.tau, 1, rs);
                                     stamp(sh, ston, OPH_REC);
+                                    if (cs.refine) refine(cs, sh, mu, dw, stt.tau, 1, rs);
                                     a_soc = rs[0];
                                     double t2[3];
                                     phase_trial(cs, sh, mu, a_soc, 1, t2);

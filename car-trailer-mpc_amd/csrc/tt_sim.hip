@@ -207,8 +207,10 @@ __global__ void __launch_bounds__(64) collision_kernel(int B, int K, long long s
 }
 
 // ---- disturbed plant: update(q, u, params, DISTURBANCE_PARAMS), simulation.py:167-199 ------------------
-// one instance in place: q (6) <- update(q, (a, om)); (a, om) before friction/slippage scaling
-__device__ __forceinline__ void plant_apply(const tt_plant& p, double* q, double a, double om) {
+// one instance in place: q (6) <- update(q, (a, om)); (a, om) before friction/slippage scaling.  sn: the NMPC /
+// fuzzy drivers' in-plant process noise (simulation_nmpc.py:94-105, simulation_fuzzy.py: q_ += state_noise * dt
+// after the Euler step), or nullptr (simulation.py's update has none)
+__device__ __forceinline__ void plant_apply(const tt_plant& p, double* q, double a, double om, const double* sn) {
 #pragma clang fp contract(off)
     if (p.enable) { a *= p.friction_coeff; om *= p.slippage_coeff; }                     // apply_disturbances 66-80
     const double th = q[2], ps = q[3], ph = q[4], v = q[5];
@@ -226,6 +228,9 @@ __device__ __forceinline__ void plant_apply(const tt_plant& p, double* q, double
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) q[i] = q[i] + qd[i] * p.dt;
+    if (sn)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) q[i] = q[i] + sn[i] * p.dt;
     if (p.enable) {                                                                      // lateral slip 117-149
         const double mag = p.lateral_slip_gain * fabs(v) * fabs(ph);
         q[0] += mag * cos(th + M_PI / 2) * p.dt;
@@ -236,7 +241,7 @@ __device__ __forceinline__ void plant_apply(const tt_plant& p, double* q, double
 __global__ void __launch_bounds__(kThreads) plant_kernel(int B, tt_plant p, double* __restrict__ state,
                                                          const double* __restrict__ u, long long u_stride,
                                                          const int* __restrict__ status, int zero_on_fail,
-                                                         double* __restrict__ u_applied) {
+                                                         const double* __restrict__ noise, double* __restrict__ u_applied) {
     const int b = blockIdx.x * kThreads + threadIdx.x;
     if (b >= B) return;
     double q[6];
@@ -245,7 +250,7 @@ __global__ void __launch_bounds__(kThreads) plant_kernel(int B, tt_plant p, doub
     double a = u[b * u_stride], om = u[b * u_stride + 1];
     if (zero_on_fail && status && status[b] > TT_ACCEPTABLE) { a = 0.0; om = 0.0; }   // simulation_nmpc.py:208-214
     if (u_applied) { u_applied[(size_t)b * 2] = a; u_applied[(size_t)b * 2 + 1] = om; }
-    plant_apply(p, q, a, om);
+    plant_apply(p, q, a, om, noise ? noise + (size_t)b * 6 : nullptr);
 #pragma unroll
     for (int i = 0; i < 6; ++i) state[(size_t)b * 6 + i] = q[i];
 }
@@ -261,7 +266,8 @@ __global__ void __launch_bounds__(kThreads) policy_plant_kernel(int B, tt_plant 
                                                                 const double* __restrict__ u, long long u_stride,
                                                                 const int* __restrict__ status, double* __restrict__ u_last,
                                                                 int* __restrict__ consec, int* __restrict__ fails,
-                                                                int* __restrict__ active, double* __restrict__ u_applied) {
+                                                                int* __restrict__ active, const double* __restrict__ noise,
+                                                                double* __restrict__ u_applied) {
     const int b = blockIdx.x * kThreads + threadIdx.x;
     if (b >= B) return;
     double a = 0.0, om = 0.0;
@@ -297,7 +303,7 @@ __global__ void __launch_bounds__(kThreads) policy_plant_kernel(int B, tt_plant 
     double q[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) q[i] = state[(size_t)b * 6 + i];
-    plant_apply(p, q, a, om);
+    plant_apply(p, q, a, om, noise ? noise + (size_t)b * 6 : nullptr);
 #pragma unroll
     for (int i = 0; i < 6; ++i) state[(size_t)b * 6 + i] = q[i];
 }
@@ -458,25 +464,38 @@ int tt_collision_device(int B, int K, const double* poses, long long stride_b, i
     return launched("collision_kernel");
 }
 
-int tt_plant_update_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
-                           const int* status, int zero_on_fail, double* u_applied, void* stream) {
+int tt_plant_update_noise_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
+                                 const int* status, int zero_on_fail, const double* state_noise, double* u_applied,
+                                 void* stream) {
     if (B < 0 || !p || !state || !u || u_stride < 2) return -EINVAL;
     if (B == 0) return 0;
     hipLaunchKernelGGL(plant_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, *p, state, u,
-                       u_stride, status, zero_on_fail, u_applied);
+                       u_stride, status, zero_on_fail, state_noise, u_applied);
     return launched("plant_kernel");
 }
 
-int tt_policy_plant_device(int B, const tt_plant* p, int policy, double* state, const double* u, long long u_stride,
-                           const int* status, double* u_last, int* consecutive, int* failures, int* active,
-                           double* u_applied, void* stream) {
+int tt_plant_update_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
+                           const int* status, int zero_on_fail, double* u_applied, void* stream) {
+    return tt_plant_update_noise_device(B, p, state, u, u_stride, status, zero_on_fail, nullptr, u_applied, stream);
+}
+
+int tt_policy_plant_noise_device(int B, const tt_plant* p, int policy, double* state, const double* u,
+                                 long long u_stride, const int* status, double* u_last, int* consecutive, int* failures,
+                                 int* active, const double* state_noise, double* u_applied, void* stream) {
     if (B < 0 || !p || !state || !u || u_stride < 2 || !status || !u_last || !consecutive || !failures || !active ||
         policy < TT_POLICY_TRACK || policy > TT_POLICY_FUZZY)
         return -EINVAL;
     if (B == 0) return 0;
     hipLaunchKernelGGL(policy_plant_kernel, dim3(grid_for(B)), dim3(kThreads), 0, (hipStream_t)stream, B, *p, policy,
-                       state, u, u_stride, status, u_last, consecutive, failures, active, u_applied);
+                       state, u, u_stride, status, u_last, consecutive, failures, active, state_noise, u_applied);
     return launched("policy_plant_kernel");
+}
+
+int tt_policy_plant_device(int B, const tt_plant* p, int policy, double* state, const double* u, long long u_stride,
+                           const int* status, double* u_last, int* consecutive, int* failures, int* active,
+                           double* u_applied, void* stream) {
+    return tt_policy_plant_noise_device(B, p, policy, state, u, u_stride, status, u_last, consecutive, failures, active,
+                                        nullptr, u_applied, stream);
 }
 
 int tt_fuzzy_weights_device(int B, int N, const double* x, const double* xref, double* wq_wr, void* stream) {

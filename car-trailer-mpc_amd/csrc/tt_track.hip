@@ -1544,9 +1544,16 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 31 with the 117-double
     // stage record); at N = 40 four waves share a CU and the occupancy build's spills would be pure cost.
     const bool occ_room = 5 * lds_bytes(a.N) <= kMaxLdsBytes;
-    if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
-    // the BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds
+    // The BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds.  At N = 20 the large-batch
+    // occupancy build is the same stage-unrolled code, so an instance's result never depends on B (or on the
+    // sharded path's chunk size): only the build's register budget differs, not one operation.
+#ifndef TT_N20_OCC  // A/B builds only: 1 = round 2's generic occupancy build at N = 20, 2 = no occupancy build
+#define TT_N20_OCC 0
+#endif
+    if (m == kMaskMPC && d && a.N == 20 && a.B > 4096 && TT_N20_OCC == 0) return launch<kMaskMPC | kDiagBit, 2, 20>(a, stream);
+    if (m == kMaskMPC && d && a.N == 20 && a.B > 4096 && TT_N20_OCC == 1) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
+    if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
     if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);

@@ -109,6 +109,8 @@ def lib():
            "tt_sim_window_indexed_device": [i, i, vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp],
            "tt_sim_log_advance_device": [i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
            "tt_policy_plant_device": [i, C.POINTER(TTPlant), i, vp, vp, ll, vp, vp, vp, vp, vp, vp, vp],
+           "tt_plant_update_noise_device": [i, C.POINTER(TTPlant), vp, vp, ll, vp, i, vp, vp, vp],
+           "tt_policy_plant_noise_device": [i, C.POINTER(TTPlant), i, vp, vp, ll, vp, vp, vp, vp, vp, vp, vp, vp],
            "tt_fuzzy_weights_device": [i, i, vp, vp, vp, vp]}
     for name, args in sim.items():
         if os.environ.get("TTMPC_LIB") and not hasattr(L, name):

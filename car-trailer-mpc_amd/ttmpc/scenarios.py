@@ -265,6 +265,8 @@ def obca_case_batch(cases, B: int, N: int, M: int, seed: int = 0, pos_sigma=0.5,
                 hi[0] = float(np.clip(hi[0] + rng.normal(0.0, ang_sigma), -0.5, 0.5))
                 if not blocked(pos, hd, hi):
                     break
+            else:  # every redraw blocked: the exact (collision-free) case start keeps the promise
+                pos, hd, hi = base
         x0[b] = [pos[0, 0], pos[0, 1], hd[0], hi[0], 0.0, 0.0]
         xg[b] = [pos[1, 0], pos[1, 1], hd[1], hi[1], 0.0, 0.0]
         zg[b] = obca_guess(pos, hd, hi, N, M, complete=complete)
@@ -368,6 +370,11 @@ def mpc_obs_batch(state_traj, input_traj, B: int, horizon: int, seed: int = 0, d
             x0[b] = np.clip(Xr[:, 0] + pert, lo, hi)
             if obstacles is None or sat_gap(x0[b, :4], PARAMS, obstacles).min() >= min_gap:
                 break
+        else:  # every redraw too close: fall back to the window's own (plan) start and say so
+            x0[b] = np.clip(Xr[:, 0], lo, hi)
+            import warnings
+            warnings.warn(f"mpc_obs_batch: instance {b}: no perturbed start at >= {min_gap} from the obstacles in "
+                          "1000 draws; using the unperturbed window start", RuntimeWarning, stacklevel=2)
     return x0, xref, uref
 
 

@@ -107,24 +107,32 @@ def collision_flags(poses, obstacles, params, flag=None, stream=None):
 
 
 def plant_update(state, u, params, disturbance_params=None, status=None, zero_on_fail=False, u_applied=None,
-                 stream=None):
+                 stream=None, state_noise=None):
     """update(q, u, params, disturbance_params) (simulation.py:167-199) in place on state (B,6); u is
-    (B,2) or a solve's U (B,N,2) (applies U[:, 0])."""
+    (B,2) or a solve's U (B,N,2) (applies U[:, 0]).  state_noise (B,6): the NMPC / fuzzy drivers' update
+    (simulation_nmpc.py:94-105), which adds state_noise * dt right after the Euler step."""
     dev = state.device
     p = plant(params, disturbance_params)
     stride = u.stride(0)
-    _check(lib().tt_plant_update_device(state.shape[0], C.byref(p), state.data_ptr(), u.data_ptr(), stride,
-                                        None if status is None else status.data_ptr(), int(bool(zero_on_fail)),
-                                        None if u_applied is None else u_applied.data_ptr(), _stream(stream, dev)),
-           "tt_plant_update_device")
+    if state_noise is not None and (state_noise.shape != state.shape or not state_noise.is_contiguous()):
+        raise ValueError("state_noise must be a contiguous (B, 6) tensor")
+    _check(lib().tt_plant_update_noise_device(state.shape[0], C.byref(p), state.data_ptr(), u.data_ptr(), stride,
+                                              None if status is None else status.data_ptr(), int(bool(zero_on_fail)),
+                                              None if state_noise is None else state_noise.data_ptr(),
+                                              None if u_applied is None else u_applied.data_ptr(), _stream(stream, dev)),
+           "tt_plant_update_noise_device")
     return state
 
 
-def update(q, u, params, disturbance_params=None, device=0):
-    """Host convenience with the reference's signature (simulation.py:167): one state, numpy in / out."""
+def update(q, u, params, disturbance_params=None, device=0, state_noise=None):
+    """Host convenience with the reference's signature (simulation.py:167): one state, numpy in / out.
+    state_noise (6,): simulation_nmpc.py / simulation_fuzzy.py's update, with the process noise the reference
+    draws inside apply_disturbances given explicitly."""
     dev = torch.device("cuda", device)
     s = _dev(np.asarray(q, dtype=np.float64).reshape(1, 6), dev)
-    plant_update(s, _dev(np.asarray(u, dtype=np.float64).reshape(1, 2), dev), params, disturbance_params)
+    sn = None if state_noise is None else _dev(np.asarray(state_noise, dtype=np.float64).reshape(1, 6), dev)
+    plant_update(s, _dev(np.asarray(u, dtype=np.float64).reshape(1, 2), dev), params, disturbance_params,
+                 state_noise=sn)
     return s.cpu().numpy()[0]
 
 
@@ -164,11 +172,17 @@ class ClosedLoop:
       failures, stops after 30.  Default: "fuzzy" for a TT_VARIANT_FUZZY solver, "nmpc" when
       zero_on_fail=True, else "track".  A TT_VARIANT_FUZZY solver gets per-instance fuzzy weights each step
       (tt_fuzzy_weights_device, mpc_control_fuzzy.py:90-119) and its failed instances are re-solved once
-      with unit weights from the same guess (145-159)."""
+      with unit weights from the same guess (145-159).
+
+    noise_in_plant=True is the NMPC / fuzzy drivers' disturbance model (simulation_nmpc.py:94-105,
+    simulation_fuzzy.py): the solver sees the exact state and, with disturbances on, the process noise
+    N(0, process_noise_std) enters the plant as q_ += noise * dt (tt_policy_plant_noise_device); the default is
+    simulation.py's (noise on the measured state, simulation.py:509-513).  Default: True for the "nmpc" and
+    "fuzzy" policies."""
 
     def __init__(self, solver, plan_x, plan_u, params, disturbance_params=None, measurement_noise=None,
                  obstacles=None, check_collision=True, switch_solver=None, warm_start=False, bug_compatible=True,
-                 zero_on_fail=False, device=None, seed=0, policy=None):
+                 zero_on_fail=False, device=None, seed=0, policy=None, noise_in_plant=None):
         self.solver = solver
         self.N = solver.N
         self.dev = torch.device("cuda", solver.device if device is None else device)
@@ -191,6 +205,11 @@ class ClosedLoop:
         if policy not in POLICIES:
             raise ValueError(f"policy must be one of {sorted(POLICIES)}")
         self.policy = policy
+        self.noise_in_plant = (policy in ("nmpc", "fuzzy")) if noise_in_plant is None else bool(noise_in_plant)
+        if self.noise_in_plant and measurement_noise:
+            raise ValueError("noise_in_plant: the NMPC / fuzzy drivers measure the exact state")
+        if self.noise_in_plant:
+            self.measurement_noise = False
         self.gen = torch.Generator(device=self.dev)
         self.gen.manual_seed(int(seed))
         self.stream = torch.cuda.Stream(self.dev)
@@ -226,13 +245,16 @@ class ClosedLoop:
         self._alloc(x.shape[0])
         self.state.copy_(_dev(x, self.dev))
         self.first = True
+        # the buffers were allocated and filled on the current stream; step() works on self.stream
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
 
     def step(self, k, noise=None):
-        """Enqueue one closed-loop step at window index k (noise: (B,6) device tensor or None)."""
+        """Enqueue one closed-loop step at window index k (noise: (B,6) device tensor or None: the measurement
+        noise, or with noise_in_plant the plant's process noise before its dt factor)."""
         L, s, B, N = lib(), self.stream, self.B, self.N
         sp = C.c_void_p(s.cuda_stream)
         with torch.cuda.stream(s):
-            if self.measurement_noise and noise is None and self.dist is not None:
+            if (self.measurement_noise or self.noise_in_plant) and noise is None and self.dist is not None:
                 noise = torch.randn((B, 6), generator=self.gen, dtype=torch.float64, device=self.dev)
                 noise.mul_(float(self.dist.get("process_noise_std", 0.0)))
             window(self.plan_x, self.plan_u, k, N, self.state, noise if self.measurement_noise else None,
@@ -261,16 +283,21 @@ class ClosedLoop:
                 _check(L.tt_record_solution_device(B, N, self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(),
                                                    self.last.data_ptr(), self.have.data_ptr(), sp),
                        "tt_record_solution_device")
-            self._policy_plant(sp)
+            self._policy_plant(sp, noise if self.noise_in_plant else None)
         self.first = False
 
-    def _policy_plant(self, sp):
+    def _policy_plant(self, sp, state_noise=None):
         p = plant(self.params, self.dist)
-        _check(lib().tt_policy_plant_device(self.B, C.byref(p), POLICIES[self.policy], self.state.data_ptr(),
-                                            self.U.data_ptr(), self.U.stride(0), self.st.data_ptr(),
-                                            self.u_last.data_ptr(), self.consec.data_ptr(), self.fails.data_ptr(),
-                                            self.active.data_ptr(), self.u_applied.data_ptr(), sp),
-               "tt_policy_plant_device")
+        sn = None
+        if state_noise is not None:
+            state_noise = state_noise.contiguous()
+            self._sn = state_noise    # keep it alive until the stream has consumed it
+            sn = state_noise.data_ptr()
+        _check(lib().tt_policy_plant_noise_device(self.B, C.byref(p), POLICIES[self.policy], self.state.data_ptr(),
+                                                  self.U.data_ptr(), self.U.stride(0), self.st.data_ptr(),
+                                                  self.u_last.data_ptr(), self.consec.data_ptr(), self.fails.data_ptr(),
+                                                  self.active.data_ptr(), sn, self.u_applied.data_ptr(), sp),
+               "tt_policy_plant_noise_device")
 
     def _fuzzy_retry(self, s):
         """mpc_control_fuzzy.py:145-159: failed instances re-solve once with unit weights, same guess."""
@@ -300,9 +327,10 @@ class ClosedLoop:
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         Np = self.plan_u.shape[-2]
         per = int(self.plan_x.shape[0] != 1)
+        meas_all = None if self.noise_in_plant else noise_all
         _check(L.tt_sim_window_indexed_device(B, N, d_ks.data_ptr(), d_step.data_ptr(), int(Np),
                                               self.plan_x.data_ptr(), self.plan_u.data_ptr(), per,
-                                              self.state.data_ptr(), ptr(noise_all), self.x_meas.data_ptr(),
+                                              self.state.data_ptr(), ptr(meas_all), self.x_meas.data_ptr(),
                                               self.xref.data_ptr(), self.uref.data_ptr(), sp),
                "tt_sim_window_indexed_device")
         if self.check_collision:
@@ -320,7 +348,11 @@ class ClosedLoop:
             _check(L.tt_record_solution_device(B, N, self.X.data_ptr(), self.U.data_ptr(), self.st.data_ptr(),
                                                self.last.data_ptr(), self.have.data_ptr(), sp),
                    "tt_record_solution_device")
-        self._policy_plant(sp)
+        sn = None
+        if self.noise_in_plant and noise_all is not None:  # this step's process noise, selected on the device
+            sn = self._sn_buf
+            sn.copy_(torch.index_select(noise_all, 0, d_step.long()).view(B, 6))
+        self._policy_plant(sp, sn)
         S, Ua, Ss, Si, Sc = logs
         _check(L.tt_sim_log_advance_device(B, d_step.data_ptr(), self.state.data_ptr(), self.u_applied.data_ptr(),
                                            self.st.data_ptr(), self.it.data_ptr(),
@@ -343,7 +375,8 @@ class ClosedLoop:
         d_ks = torch.tensor(ks, dtype=torch.int32, device=d)
         d_step = torch.zeros(1, dtype=torch.int32, device=d)
         noise_all = None
-        if self.measurement_noise and self.dist is not None:
+        self._sn_buf = torch.empty((B, 6), dtype=torch.float64, device=d)
+        if (self.measurement_noise or self.noise_in_plant) and self.dist is not None:
             if noise is None:
                 noise_all = torch.randn((K, B, 6), generator=self.gen, dtype=torch.float64, device=d)
                 noise_all.mul_(float(self.dist.get("process_noise_std", 0.0)))
@@ -388,7 +421,8 @@ class ClosedLoop:
         self.X[idx], self.U[idx], self.st[idx], self.it[idx], self.kkt[idx] = X, U, st, it, kk
 
     def run(self, x_init, T_sim, noise=None, record=True):
-        """Run the reference's loop to T_sim.  noise: optional (steps, B, 6) measurement-noise draws.
+        """Run the reference's loop to T_sim.  noise: optional (steps, B, 6) measurement-noise draws (with
+        noise_in_plant: the plant's process-noise draws).
         Returns numpy logs: states (steps+1,B,6), controls (steps,B,2) as applied, status / iters /
         collide (steps,B), and the step indices k."""
         ks = step_indices(T_sim, float(self.params["dt"]))

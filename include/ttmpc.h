@@ -167,6 +167,17 @@ enum { TT_POLICY_TRACK = 0, TT_POLICY_NMPC = 1, TT_POLICY_FUZZY = 2 };
 int tt_policy_plant_device(int B, const tt_plant* p, int policy, double* state, const double* u, long long u_stride,
                            const int* status, double* u_last, int* consecutive, int* failures, int* active,
                            double* u_applied, void* stream);
+/* The NMPC and fuzzy drivers' plant (simulation_nmpc.py:94-105, simulation_fuzzy.py:94-105): the same update plus
+ * the process noise inside the plant, q_ += state_noise * dt right after the Euler step (before the lateral slip);
+ * those drivers solve from the exact state (no measurement noise).  state_noise [B][6] device, drawn by the caller
+ * (the reference draws N(0, process_noise_std) in apply_disturbances), or NULL = none (then identical to the
+ * functions above). */
+int tt_plant_update_noise_device(int B, const tt_plant* p, double* state, const double* u, long long u_stride,
+                                 const int* status, int zero_on_fail, const double* state_noise, double* u_applied,
+                                 void* stream);
+int tt_policy_plant_noise_device(int B, const tt_plant* p, int policy, double* state, const double* u,
+                                 long long u_stride, const int* status, double* u_last, int* consecutive, int* failures,
+                                 int* active, const double* state_noise, double* u_applied, void* stream);
 /* _compute_fuzzy_weights (mpc_control_fuzzy.py:90-119) per instance from the measured state x [B][6]
  * and the window's reference xref [B][N+1][6] (speed of stage 0): wq_wr [B][8] = (q0..q5, r0, r1), the
  * per-instance weights of a TT_VARIANT_FUZZY solve. */

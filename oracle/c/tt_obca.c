@@ -18,7 +18,8 @@
  *     slack-bound multipliers v_L, v_U): tol 1e-8, acceptable 1e-6 x 15, monotone mu from 0.1,
  *     bound_relax_factor 1e-8 on variable AND constraint bounds, bound_push/frac 1e-2, kappa_sigma 1e10;
  *   * initial constraint multipliers by least squares (constr_mult_init_max 1000: discarded if larger);
- *   * inertia correction with IPOPT's delta_w schedule (1e-4 / x100 / x8 / /3, cap 1e20);
+ *   * inertia correction with IPOPT's delta_w schedule (1e-4 / x100 / x8 / /3, cap 1e20) and iterative
+ *     refinement of every step (PDFullSpaceSolver: min 1, max 10 steps, residual ratio 1e-10);
  *   * filter line search (Waechter & Biegler 2006) with up to four second-order corrections;
  *   * the soft restoration phase (soft_resto_pderror_reduction_factor 0.9999, max_soft_resto_iters 10);
  *   * the feasibility restoration phase MinC_1Nrm: the restoration NLP
@@ -37,11 +38,12 @@
  *   D ds - y_d+ = -grad phi_s,  J_c dx - E_c y_c+ = -r_c,  J_d dx - ds - E_p y_d+ = -(d - s)
  * (E = 0 outside the restoration phase; inside it the eliminated p/n give E = 1/D_p + 1/D_n per row.)
  * Slacks and y_d are eliminated; every OBCA block (8 duals mu/lam, 4 rows) couples only to
- * (X, Y, theta, psi) of its stage, so its 8x8 block K = W_ww + Sigma_w + dw + Jw' E^-1 Jw is
- * Cholesky-factorised and Schur-eliminated into the 6x6 stage Hessian; the remaining stage-wise LQ
+ * (X, Y, theta, psi) of its stage: its dual Hessian A = W_ww + Sigma_w + dw and T = E + Jw A^-1 Jw' are factored
+ * by signed LDL' and the block is Schur-eliminated into the 6x6 stage Hessian; the remaining stage-wise LQ
  * problem is solved by a Riccati recursion (soft dynamics rows inside the restoration phase:
- * P~ = P - P S M^-1 S P, M = I + S P S, S = E_c^1/2).  Inertia test: every K, every M and every Riccati
- * input block R~ + B'P~B must be positive definite.
+ * P~ = P - P S M^-1 S P, M = I + S P S, S = E_c^1/2).  Inertia test (IPOPT's (n, m, 0) of the whole KKT matrix,
+ * restated by blocks): every block In(A) + In(-T) = (8, 4, 0), every M and every Riccati input block R~ + B'P~B
+ * positive definite.  Every step solve is followed by IPOPT's iterative refinement on the un-condensed system.
  * IPOPT's gradient-based NLP scaling is not applied: it is the identity at the bench workloads' starting
  * points (all gradients < 100; DESIGN.md §1, tests/test_obca_oracle.py).
  */
@@ -108,6 +110,8 @@ typedef struct {
     double* alt;    /* 1: the block was eliminated rows-first through M_w = A + Jw' E^-1 Jw (TTO_OPT_BLOCK_MW) */
     double Dsf[6], Dfe[6];
     double *Sd, *Mch, *Ptl, *ptl; /* soft dynamics rows (restoration) */
+    double *Gsg, *Msg; /* signs of the LDL' pivots of every G_k (2) and M_k (6) (all +1 unless indefinite) */
+    int negx;      /* global inertia test: negative pivots beyond IPOPT's (n, m, 0) count, summed over the factorisation */
     /* rhs + step */
     double *qt, *rt, *vv, *rd, *pv, *kf, *Yb, *LT, *Gm, *tv, *rct;
     double rf[6];
@@ -331,6 +335,7 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->Rt, N * 4);
     TAKE(W->Pm, N1 * 36); TAKE(W->G, N * 4); TAKE(W->H, N * 12); TAKE(W->K, N * 12);
     TAKE(W->Sd, N1 * 6); TAKE(W->Mch, N1 * 36); TAKE(W->Ptl, N1 * 36); TAKE(W->ptl, N1 * 6);
+    TAKE(W->Gsg, N * 2); TAKE(W->Msg, N1 * 6);
     TAKE(W->qt, N1 * 6); TAKE(W->rt, N * 2); TAKE(W->vv, nb * 8); TAKE(W->rd, nb * 4); TAKE(W->pv, N1 * 6);
     TAKE(W->kf, N * 2); TAKE(W->rct, N1 * 6);
     TAKE(W->dx, N1 * 6); TAKE(W->du, N * 2); TAKE(W->dw, nb * 8); TAKE(W->ds, nb * 4); TAKE(W->ycp, N1 * 6);
@@ -563,6 +568,13 @@ static void bsub(const double* L, int n, double* b) { /* b <- L^-T b */
     }
 }
 
+/* b <- (L S L')^-1 b */
+static void ssolve(const double* L, const double* S, int n, double* b) {
+    fsub(L, n, b);
+    for (int i = 0; i < n; ++i) b[i] *= S[i];
+    bsub(L, n, b);
+}
+
 /* ------------------------------------------------------------------ Newton system */
 static double sig_x(const ws_t* W, int k, int i) {
     const double v = W->x[6 * k + i];
@@ -655,8 +667,9 @@ static void linearise(ws_t* W) {
  * catastrophically, while T stays well conditioned.  Inertia (IPOPT tests the whole KKT matrix): by
  * Haynsworth In(M) = In(A) + In(-T), so the block has the correct inertia (8, 4, 0) iff T has exactly as many
  * negative pivots as A; both are factored by the signed Cholesky A = L S_A L', T = L_T S_T L_T', and every
- * A^-1 / T^-1 carries its sign vector.  That exact test is an opt-in (TTO_OPT_BLOCK_INERTIA); the
- * default, which the GPU kernel runs, asks for A positive definite (S = I), a sufficient condition. */
+ * A^-1 / T^-1 carries its sign vector.  That exact test is the default (the GPU kernel runs it too); TTO_OPT_PD_BLOCKS
+ * switches back to round 2's sufficient condition A positive definite (S = I), which raises delta_w where IPOPT
+ * would not. */
 static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     const double *Jx = W->Jx + 16 * bi, *Jw = W->Jw + 32 * bi;
     double* D = W->Dd + 4 * bi;
@@ -681,7 +694,7 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
     }
     double* SA = W->Sg + 12 * bi;
     double* ST = SA + 8;
-    const int inert = (W->P->opts & TTO_OPT_BLOCK_INERTIA) != 0;
+    const int inert = !(W->P->opts & TTO_OPT_PD_BLOCKS);
     int negA = 0;
     W->alt[bi] = 0.0;
     if ((W->P->opts & TTO_OPT_BLOCK_MW) && !W->lsq) {
@@ -749,8 +762,13 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
         }
     if (inert) {
         /* inertia of the block [[A, C'], [C, -E]] = In(A) + In(-T): (8, 4, 0) iff T has as many negative
-         * pivots as A (Haynsworth); the stage Riccati then tests the Schur complement onto dx^ */
-        if (schol(LT, 4, ST) != negA) return 1;
+         * pivots as A (Haynsworth); the stage Riccati then tests the Schur complement onto dx^.  Global test
+         * (IPOPT counts the negative eigenvalues of the whole KKT matrix): the block's surplus of negative
+         * pivots negA - negT is summed with the Riccati's and must vanish overall */
+        const int negT = schol(LT, 4, ST);
+        if (negT < 0) return 1;
+        if (W->P->opts & TTO_OPT_GLOBAL_INERTIA) W->negx += negA - negT;
+        else if (negT != negA) return 1;
     } else {
         if (chol(LT, 4) != 0) return 1;
         for (int r = 0; r < 4; ++r) ST[r] = 1.0;
@@ -783,14 +801,23 @@ static int soften(ws_t* W, int k) {
     double* Mk = W->Mch + 36 * k;
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) Mk[i * 6 + j] = (i == j ? 1.0 : 0.0) + S[i] * Pk[i * 6 + j] * S[j];
-    if (chol(Mk, 6) != 0) return 1;
+    double* Ms = W->Msg + 6 * k;
+    if (W->P->opts & TTO_OPT_GLOBAL_INERTIA) {
+        /* the soft row pair [[P, -I], [-I, -E]] has inertia (6, 6) iff M > 0; each negative pivot of M is one
+         * surplus negative eigenvalue of the KKT matrix */
+        const int negM = schol(Mk, 6, Ms);
+        if (negM < 0) return 1;
+        W->negx += negM;
+    } else {
+        if (chol(Mk, 6) != 0) return 1;
+        for (int i = 0; i < 6; ++i) Ms[i] = 1.0;
+    }
     /* X = M^-1 S P (column by column), P~ = P - (P S) X */
     double X[36];
     for (int j = 0; j < 6; ++j) {
         double col[6];
         for (int i = 0; i < 6; ++i) col[i] = S[i] * Pk[i * 6 + j];
-        fsub(Mk, 6, col);
-        bsub(Mk, 6, col);
+        ssolve(Mk, Ms, 6, col);
         for (int i = 0; i < 6; ++i) X[i * 6 + j] = col[i];
     }
     for (int i = 0; i < 6; ++i)
@@ -808,8 +835,7 @@ static void soft_apply(const ws_t* W, int k, const double* b, double* v) {
     const double* S = W->Sd + 6 * k;
     double t[6];
     for (int i = 0; i < 6; ++i) t[i] = S[i] * b[i];
-    fsub(W->Mch + 36 * k, 6, t);
-    bsub(W->Mch + 36 * k, 6, t);
+    ssolve(W->Mch + 36 * k, W->Msg + 6 * k, 6, t);
     for (int i = 0; i < 6; ++i) v[i] -= S[i] * t[i];
 }
 
@@ -819,6 +845,7 @@ static int factor(ws_t* W, double dw) {
     const int N = W->N;
     const double dt = P->dt;
     int fail = 0;
+    W->negx = 0;
     if (W->R == M_RESTO)
         for (int i = 0; i < W->nrow; ++i) {
             W->Dpr[i] = W->lsq ? 1.0 : W->zp[i] / W->pr[i] + dw;
@@ -885,12 +912,20 @@ static int factor(ws_t* W, double dw) {
             H[6 + j] = dt * h1;
         }
         G[1] = G[2] = 0.5 * (G[1] + G[2]);
-        if (chol(G, 2) != 0) return 1;
+        double* Gs = W->Gsg + 2 * kk;
+        if (P->opts & TTO_OPT_GLOBAL_INERTIA) {
+            /* each negative pivot of the reduced input Hessian is one surplus negative eigenvalue */
+            const int negG = schol(G, 2, Gs);
+            if (negG < 0) return 1;
+            W->negx += negG;
+        } else {
+            if (chol(G, 2) != 0) return 1;
+            Gs[0] = Gs[1] = 1.0;
+        }
         double* Kk = W->K + 12 * kk;
         for (int j = 0; j < 6; ++j) {
             double col[2] = {H[j], H[6 + j]};
-            fsub(G, 2, col);
-            bsub(G, 2, col);
+            ssolve(G, Gs, 2, col);
             Kk[j] = -col[0];
             Kk[6 + j] = -col[1];
         }
@@ -913,7 +948,7 @@ static int factor(ws_t* W, double dw) {
             for (int j = 0; j < i; ++j) Pk[i * 6 + j] = Pk[j * 6 + i] = 0.5 * (Pk[i * 6 + j] + Pk[j * 6 + i]);
     }
     if (soften(W, 0) != 0) return 1;
-    return 0;
+    return W->negx != 0; /* global inertia test: IPOPT's (n, m, 0) (W->negx stays 0 in the other modes) */
 }
 
 /* right-hand side + back-substitution.  cres: dynamics residual rows ((N+1)*6), dres: OBCA residual rows
@@ -995,8 +1030,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             const double* S = W->Sd + 6 * k;
             double t[6];
             for (int i = 0; i < 6; ++i) t[i] = S[i] * Pp[i];
-            fsub(W->Mch + 36 * k, 6, t);
-            bsub(W->Mch + 36 * k, 6, t);
+            ssolve(W->Mch + 36 * k, W->Msg + 6 * k, 6, t);
             for (int i = 0; i < 6; ++i) {
                 double a = 0.0;
                 for (int l = 0; l < 6; ++l) a += W->Pm[36 * k + i * 6 + l] * S[l] * t[l];
@@ -1015,8 +1049,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
             pp[i] = t;
         }
         double g[2] = {W->rt[2 * kk] + dt * pp[5], W->rt[2 * kk + 1] + dt * pp[4]};
-        fsub(W->G + 4 * kk, 2, g);
-        bsub(W->G + 4 * kk, 2, g);
+        ssolve(W->G + 4 * kk, W->Gsg + 2 * kk, 2, g);
         W->kf[2 * kk] = -g[0];
         W->kf[2 * kk + 1] = -g[1];
         const double* H = W->H + 12 * kk;
@@ -2080,10 +2113,10 @@ static double newton_resid(ws_t* W, double mu, const double* cres, const double*
 
 /* the step solve with IPOPT's iterative refinement on the un-condensed system (min_refinement_steps 1,
  * max_refinement_steps 10, residual_ratio_max 1e-10): correction solves reuse the factorisation with the
- * residuals as constants (TTO_OPT_REFINE) */
+ * residuals as constants (default; TTO_OPT_NO_REFINE switches it off) */
 static void refined_solve(ws_t* W, double mu, double* cres, double* dres, double* fres) {
     solve_rhs(W, mu, cres, dres, fres);
-    if (!(W->P->opts & TTO_OPT_REFINE) || W->lsq) return;
+    if ((W->P->opts & TTO_OPT_NO_REFINE) || W->lsq) return;
     const int N = W->N, rs = W->R == M_RESTO;
     const size_t N1 = (size_t)N + 1, nb = (size_t)W->nb, nr = (size_t)W->nrow;
     double bnorm = 0.0;

@@ -38,20 +38,26 @@ typedef struct {
     int dual_init;                   /* 0: start from the guess's mu/lam (reference behaviour);
                                         1: replace them by the separating-axis certificate of each
                                         body/obstacle pair at the guess pose (see tt_obca.c) */
-    int opts;                        /* TTO_OPT_* bits (diagnostics / A-B): 1-4 switch restated features off, 8-128 switch
-                                        oracle-only IPOPT features on; 0 = the kernel's algorithm */
+    int opts;                        /* TTO_OPT_* bits (diagnostics / A-B): 1, 2, 4, 32, 64 switch restated features off,
+                                        8, 16, 128 switch oracle-only IPOPT features on; 0 = the kernel's algorithm */
 } tto_obca_problem;
 
 #define TTO_OPT_NO_RESTO 1       /* no restoration phase: a failed line search takes its last trial step */
 #define TTO_OPT_NO_SOFT_RESTO 2  /* no soft restoration phase */
 #define TTO_OPT_NO_LSQ_MULT 4    /* constraint multipliers start at 0 instead of the least-squares estimate */
-/* opt-in IPOPT features restated in the oracle only (A/B on the C4 census: 57/64 converged with and without
- * them); the GPU kernel does not run them, so GPU-vs-oracle parity uses opts without these bits */
+/* IPOPT defaults the GPU kernel also runs (switched OFF by these bits, for A/B runs):
+ *   exact block inertia: IPOPT perturbs delta_w until the whole KKT matrix has inertia (n, m, 0); per OBCA block
+ *   that is In(A) + In(-T) = (8, 4, 0) (Haynsworth), tested by signed LDL' (DESIGN.md 5);
+ *   iterative refinement of every step solve on the un-condensed system (min_refinement_steps 1,
+ *   max_refinement_steps 10, residual_ratio_max 1e-10, residual_improvement_factor 1). */
+#define TTO_OPT_PD_BLOCKS 32     /* round-2 sufficient test instead: every block's A positive definite */
+#define TTO_OPT_NO_REFINE 64     /* no iterative refinement */
+/* opt-in IPOPT features restated in the oracle only (A/B on the C4 census); the GPU kernel does not
+ * run them, so GPU-vs-oracle parity uses opts without these bits */
 #define TTO_OPT_KAPPA_D 8        /* kappa_d = 1e-5 linear damping of variables / slacks with one finite bound */
 #define TTO_OPT_WATCHDOG 16      /* watchdog (trigger 10 shortened steps, 3 trial iterations) in the line search */
-#define TTO_OPT_BLOCK_MW 128     /* exact block inertia: a block with indefinite A eliminated rows-first through M_w = A + Jw' E^-1 Jw */
-#define TTO_OPT_REFINE 64        /* IPOPT's iterative refinement of every step solve on the un-condensed system */
-#define TTO_OPT_BLOCK_INERTIA 32 /* exact block inertia In(A) + In(-T) = (8, 4, 0) by signed LDL' instead of A positive definite */
+#define TTO_OPT_BLOCK_MW 128     /* a block with indefinite A eliminated rows-first through M_w = A + Jw' E^-1 Jw */
+#define TTO_OPT_GLOBAL_INERTIA 256 /* inertia counted over the whole factorisation (blocks, Riccati G_k, soft M_k) */
 
 /* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).
  * z_guess (n) or NULL (plan: _generate_initial_trajectory_guess 209-225; track: reference copy +

@@ -106,9 +106,10 @@ os.environ.setdefault("OMP_PROC_BIND", "false")
 # ------------------------------------------------------------------------------------------------
 MAXM = 16
 OBCA_PLAN, OBCA_TRACK = 0, 1
-# oracle-only opt-in IPOPT features (tt_obca.h): kappa_d damping, line-search watchdog, exact block inertia test,
-# iterative refinement, rows-first elimination of indefinite blocks
-OPT_KAPPA_D, OPT_WATCHDOG, OPT_BLOCK_INERTIA, OPT_REFINE, OPT_BLOCK_MW = 8, 16, 32, 64, 128
+# tt_obca.h switches: IPOPT defaults off (round 2's PD block test, no iterative refinement) and oracle-only opt-in
+# IPOPT features (kappa_d damping, line-search watchdog, rows-first elimination of indefinite blocks)
+OPT_PD_BLOCKS, OPT_NO_REFINE = 32, 64
+OPT_KAPPA_D, OPT_WATCHDOG, OPT_BLOCK_MW, OPT_GLOBAL_INERTIA = 8, 16, 128, 256
 
 
 class TTOObcaProblem(C.Structure):

@@ -398,10 +398,12 @@ DISTURBANCE_PARAMS = {"friction_coeff": 0.9, "slippage_coeff": 0.9, "process_noi
                       "lateral_slip_gain": 0.01, "slip_angle_max": 0.0}
 
 
-def plant_update(q, u, p, dist=None):
+def plant_update(q, u, p, dist=None, state_noise=None):
     """update(q, u, params, disturbance_params) of simulation.py:167-199, vectorised over leading axes:
     apply_disturbances (50-87: u scaled by friction / slippage; its noise draw is discarded),
-    f_dyn (34-48), apply_slippage_to_dynamics (89-115), Euler step, apply_lateral_slip (117-149)."""
+    f_dyn (34-48), apply_slippage_to_dynamics (89-115), Euler step, apply_lateral_slip (117-149).
+    state_noise: the NMPC / fuzzy drivers' update (simulation_nmpc.py:94-105, simulation_fuzzy.py:94-105), which
+    keeps apply_disturbances' draw and adds state_noise * dt right after the Euler step."""
     q = np.asarray(q, dtype=np.float64)
     u = np.array(u, dtype=np.float64)
     if dist is not None:
@@ -413,6 +415,8 @@ def plant_update(q, u, p, dist=None):
         qd[..., 2] = qd[..., 2] * slip
         qd[..., 3] = qd[..., 3] * slip
     nq = q + qd * p["dt"]
+    if state_noise is not None:
+        nq = nq + np.asarray(state_noise, dtype=np.float64) * p["dt"]
     if dist is not None and "lateral_slip_gain" in dist:
         mag = dist["lateral_slip_gain"] * np.abs(q[..., 5]) * np.abs(q[..., 4])
         nq[..., 0] = nq[..., 0] + mag * np.cos(q[..., 2] + np.pi / 2) * p["dt"]
@@ -430,10 +434,11 @@ def step_indices(T_sim, dt):
 
 
 def closed_loop(solve, x_init, plan_x, plan_u, horizon, T_sim, p, dist=None, noise=None, zero_on_fail=False,
-                policy=None, fuzzy=False):
+                policy=None, fuzzy=False, plant_noise=None):
     """The reference loop for B instances sharing one plan (plan_x (6,Np+1), plan_u (2,Np)).
     solve(x_meas (B,6), Xr (B,N+1,6), Ur (B,N,2)[, w (B,8)]) -> (X (B,N+1,6), U (B,N,2), status (B,)).
     noise: (steps, B, 6) measurement noise (simulation.py:509-513) or None.
+    plant_noise: (steps, B, 6) process noise inside the plant (simulation_nmpc.py:94-105) or None.
     policy: what follows a failed solve (status > 1) -- "track" (simulation.py:519-527: the returned
     inputs), "nmpc" (simulation_nmpc.py:206-216: zero control, stop after 20 consecutive failures),
     "fuzzy" (simulation_fuzzy.py:207-221: last successful control, zero after 15, stop after 30).  A
@@ -494,7 +499,7 @@ def closed_loop(solve, x_init, plan_x, plan_u, horizon, T_sim, p, dist=None, noi
                     u0[b] = 0.0
             else:
                 u0[b] = U[b, 0]
-        xn = plant_update(x, u0, p, dist)
+        xn = plant_update(x, u0, p, dist, None if plant_noise is None else plant_noise[j])
         x = np.where(active[:, None], xn, x)
         S.append(x.copy())
         Ua.append(u0)

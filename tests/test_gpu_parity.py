@@ -299,24 +299,21 @@ def test_c5_full_batch_through_the_sharded_path():
     assert np.array_equal(X, X2) and np.array_equal(U, U2) and np.array_equal(st, st2)
 
 
-def test_occupancy_build_matches_the_latency_build():
-    """Large batches (B > 4096, reference box, diagonal weights, N <= 31) launch the two-waves-per-SIMD
-    build of track_kernel; small N = 20 batches launch the stage-unrolled NS = 20 build, whose lane pairs
-    split each stage's variables over two lanes.  The per-stage arithmetic is identical; only the wave sums
-    (merit, constraint violation, slope) add the same terms in a different order, so a filter decision on
-    a last, ~1e-14 step can go the other way (tools/build_diff.py: 1 of 4608 instances, |dX| 1.4e-14).
-    Status, iteration count and KKT error must be identical; the plans equal to 1e-12."""
+def test_occupancy_build_is_bitwise_the_latency_build():
+    """Large batches (B > 4096, reference box, diagonal weights, N = 20) launch the two-waves-per-SIMD build of
+    the stage-unrolled NS = 20 kernel, small ones its one-wave build: the same code under a different register
+    budget, so every instance's result is bitwise independent of the batch size (and of the sharded path's chunk
+    size).  Two seeds, 4608 instances each, against 1152-instance batches."""
     from ttmpc.scenarios import synthetic_batch
     N, B = 20, 4608
-    x0, xr, ur = synthetic_batch(B, N, seed=77, psi_range=0.6)
     s = _gpu_solver(N)
-    big = s.solve(x0, xr, ur)
-    for lo in range(0, B, 1152):
-        small = s.solve(x0[lo:lo + 1152], xr[lo:lo + 1152], ur[lo:lo + 1152])
-        for a, b in zip(big[:2], small[:2]):
-            assert np.max(np.abs(a[lo:lo + 1152] - b)) <= 1e-12
-        for a, b in zip(big[2:], small[2:]):
-            assert np.array_equal(a[lo:lo + 1152], b)
+    for seed in (77, 78):
+        x0, xr, ur = synthetic_batch(B, N, seed=seed, psi_range=0.6)
+        big = s.solve(x0, xr, ur)
+        for lo in range(0, B, 1152):
+            small = s.solve(x0[lo:lo + 1152], xr[lo:lo + 1152], ur[lo:lo + 1152])
+            for a, b in zip(big, small):
+                assert np.array_equal(a[lo:lo + 1152], b), seed
 
 
 def test_occupancy_build_boundary_n31_n32():

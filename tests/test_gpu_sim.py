@@ -109,6 +109,26 @@ def test_plant_kernel_matches_reference_update(golden_ref):
     assert np.max(np.abs(s.cpu().numpy() - to.plant_update(golden_ref["q"], golden_ref["u"], P, d))) <= 1e-13
 
 
+def test_plant_kernel_with_in_plant_noise_matches_nmpc_update():
+    """tt_plant_update_noise_device against the NMPC / fuzzy drivers' update executed by the reference
+    (tests/golden/nmpc_plant.npz: simulation_nmpc.py / simulation_fuzzy.py:94-105 with recorded noise draws)."""
+    from conftest import GOLDEN
+    from ttmpc import simulation as sim
+    g = np.load(GOLDEN / "nmpc_plant.npz")
+    keys = ("friction_coeff", "slippage_coeff", "process_noise_std", "lateral_slip_gain", "slip_angle_max")
+    for tag in ("nmpc", "fuzzy"):
+        for which in ("own", "full"):
+            dist = {k: float(g[f"{which}_{k}"]) for k in keys}
+            s = _t(g["q"])
+            sim.plant_update(s, _t(g["u"]), P, dist, state_noise=_t(g[f"{tag}_{which}_noise"]))
+            torch.cuda.synchronize()
+            assert np.max(np.abs(s.cpu().numpy() - g[f"{tag}_{which}_next"])) <= 1e-13, (tag, which)
+    # host convenience with the reference signature + explicit draw
+    q1 = sim.update(g["q"][3], g["u"][3], P, {k: float(g[f"full_{k}"]) for k in keys},
+                    state_noise=g["nmpc_full_noise"][3])
+    assert np.max(np.abs(q1 - g["nmpc_full_next"][3])) <= 1e-13
+
+
 def test_plant_kernel_applies_first_input_and_zero_on_failure(golden_ref):
     from oracle import ttmpc_oracle as to
     from ttmpc import simulation as sim
@@ -250,7 +270,8 @@ def test_obca_plans_feed_tracking_batch_on_device(golden_ref):
 @pytest.mark.parametrize("warm", [False, True])
 def test_graph_replay_equals_eager_loop(plan, golden_ref, warm):
     """run_graph (one captured step replayed through a hipGraph, step index on the device) reproduces the
-    eager run() bit for bit, disturbances, noise, collision checks and the NMPC warm start included."""
+    eager run() bit for bit, disturbances, noise, collision checks and the NMPC warm start included (the NMPC
+    policy puts the noise into the plant, simulation_nmpc.py:94-105: the device-selected draw of the step)."""
     import ttmpc
     from oracle import ttmpc_oracle as to
     from ttmpc import simulation as sim
@@ -284,6 +305,40 @@ def _oracle_solver_cfg(N, tol, acc_tol, max_iter, acc_iter):
         X, Uo = layout.unpack(z, N)
         return X, Uo, st
     return solve
+
+
+@pytest.mark.parametrize("policy, variant", [("nmpc", "NMPC"), ("fuzzy", "FUZZY")])
+def test_disturbed_nmpc_fuzzy_loops_match_oracle_loop(plan, policy, variant):
+    """simulation_nmpc.py / simulation_fuzzy.py with ENABLE_DISTURBANCES: the solver sees the exact state and the
+    process noise enters the plant (q_ += noise * dt, 94-105; tt_policy_plant_noise_device), against the oracle
+    loop with the same draws.  The modules' own IPOPT options (tol 1e-3, acceptable 1e-2 x 5, max_iter 2000)."""
+    import ttmpc
+    from oracle import ttmpc_oracle as to
+    from ttmpc import simulation as sim
+    S, U = plan
+    N, B, T = 20, 6, 1.5
+    rng = np.random.default_rng(31)
+    x0 = S[:, 0][None] + rng.normal(scale=[0.3, 0.3, 0.02, 0.02, 0.0, 0.0], size=(B, 6))
+    K = len(to.step_indices(T, 0.05))
+    dist = {"friction_coeff": 1, "slippage_coeff": 1, "process_noise_std": 0.02, "lateral_slip_gain": 0.0,
+            "slip_angle_max": 0.0}                  # simulation_nmpc.py:20-26 / simulation_fuzzy.py:20-26
+    noise = rng.normal(scale=dist["process_noise_std"], size=(K, B, 6))
+    tol, acc, mi, ai = 1e-3, 1e-2, 2000, 5
+    solver = ttmpc.BatchSolver(N, P, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XLB, to.MPC_XUB, to.MPC_ULB, to.MPC_UUB,
+                               variant=getattr(ttmpc, f"TT_VARIANT_{variant}"), tol=tol, acc_tol=acc, max_iter=mi,
+                               acc_iter=ai)
+    cl = sim.ClosedLoop(solver, S, U, P, dist, policy=policy)
+    assert cl.noise_in_plant and not cl.measurement_noise
+    out = cl.run(x0, T, noise=noise)
+    ref_S, ref_u, ref_st, pol = to.closed_loop(_oracle_solver_cfg(N, tol, acc, mi, ai), x0, S, U, N, T, P, dist,
+                                               policy=policy, fuzzy=variant == "FUZZY", plant_noise=noise)
+    assert np.array_equal(out["status"], ref_st)
+    assert np.max(np.abs(out["controls"] - ref_u)) <= 1e-6
+    assert np.max(np.abs(out["states"] - ref_S)) <= 1e-6
+    # the plant noise moved the states: the noise-free loop ends elsewhere
+    calm = to.closed_loop(_oracle_solver_cfg(N, tol, acc, mi, ai), x0, S, U, N, T, P, dist, policy=policy,
+                          fuzzy=variant == "FUZZY")[0]
+    assert np.max(np.abs(calm[-1] - ref_S[-1])) > 1e-4
 
 
 @pytest.mark.parametrize("policy, variant", [("nmpc", "NMPC"), ("fuzzy", "FUZZY")])
