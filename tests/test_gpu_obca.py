@@ -164,6 +164,27 @@ def test_c4_full_batch_properties_and_determinism():
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
 
 
+def test_reference_default_plan_matches_oracle():
+    """The reference's own default OBCA call (trajectory_animation.py:43-52, 77-83, 109): N = 200, dt = 0.1, all 11
+    obstacles of obstacles.json, the Hybrid-A*-shaped 8-waypoint guess of tests/golden/make_golden_default_plan.py,
+    max_iter 5000.  The kernel reaches the oracle's optimum (the committed fixture): same status, the same primal
+    solution to 1e-6, cost 64,914, collision-free with d_min active."""
+    from oracle import c_oracle as co
+    from ttmpc import collision
+    g = np.load(GOLDEN / "reference_default_plan.npz")
+    ob = np.load(GOLDEN / "reference_numpy.npz")["obstacles"].reshape(-1, 4)
+    N, M = 200, ob.shape[0]
+    X, U, Z, st, it, kk = _solver(N, ob).solve(g["x_init"], g["x_goal"], z_guess=g["z_guess"])
+    assert st[0] == int(g["status"][0]) == 0, (st, it, kk)
+    Xc, Uc, _, _ = co.obca_split(g["z"], N, M)
+    assert np.abs(X - Xc).max() <= 1e-6 and np.abs(U - Uc).max() <= 1e-6
+    d = X[0] - g["x_goal"][0]
+    cost = float((d[:-1] ** 2).sum() + 100.0 * (d[-1] ** 2).sum() + 10.0 * (U[0] ** 2).sum())
+    assert abs(cost - float(g["cost"])) <= 1e-6 * float(g["cost"])
+    gap = collision.sat_gap(X[0], P6, ob).min()
+    assert 0.199 < gap <= 0.2 + 1e-6
+
+
 def _f(X, U):
     L1, L2, M = P6["L1"], P6["L2"], P6["M"]
     th, psi, phi, v = X[..., 2], X[..., 3], X[..., 4], X[..., 5]
