@@ -77,7 +77,7 @@ struct ObcaArgs {
     double* ws;                     // per-instance workspace, obca_ws_doubles(N, M) each
     unsigned long long* stamps;     // [B][kObcaPhases] cycle sums (diagnostics), or nullptr
 };
-enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_REFINE, OPH_TOTAL,
+enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_REF_SWEEP, OPH_REF_REC, OPH_TOTAL,
        kObcaPhases };
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N

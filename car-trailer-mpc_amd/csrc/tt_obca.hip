@@ -2671,8 +2671,13 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
 // fw / zf_lam / t, and the constants the recovery needs (B_OS, B_OP / B_ON, S_OP / S_ON, osf / opf / onf).
 // out: [0] max |residual| [1] max |constant| [2] max |dx, y+_c, dw| (the oracle's solution norm)
 //      [3] alpha_primal [4] alpha_dual [5] grad phi' d [6] max relative step  (of the step in buf: the line search's)
+// mode: NR_STEP the step in buf is complete; NR_MAIN the forward sweep's dx, du, y+_c are in buf and the blocks' and
+// elastic pairs' parts are recovered here first from the factor record (phase_recover's work, fused: one pass over
+// the blocks instead of two); NR_CORR a correction's dx is in buffer 2, the stage parts are already added into buf
+// (phase_stage_add), and the blocks' correction is recovered here (with the constants prep left) and added.
+enum { NR_STEP = 0, NR_MAIN = 1, NR_CORR = 2 };
 __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, bool prep,
-                                        double (&out)[7]) {
+                                        int mode, double (&out)[7]) {
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0;
@@ -2790,9 +2795,18 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
-                const double dp = c.S(S_DP + 6 * buf + i, k), dn = c.S(S_DN + 6 * buf + i, k);
-                rc[i] += -dp + dn;
                 const double Dp = zp / p + dw, Dn = zn / n + dw, gp = RHO - mu / p, gn = RHO - mu / n;
+                double dp, dn;
+                if (mode == NR_MAIN) {  // the pair's step from the new multiplier (phase_recover's pn_step)
+                    dp = (yp[i] - gp) / Dp;
+                    dn = (-yp[i] - gn) / Dn;
+                    c.S(S_DP + 6 * buf + i, k) = dp;
+                    c.S(S_DN + 6 * buf + i, k) = dn;
+                } else {
+                    dp = c.S(S_DP + 6 * buf + i, k);
+                    dn = c.S(S_DN + 6 * buf + i, k);
+                }
+                rc[i] += -dp + dn;
                 rpc[i] = R(Bc(gp) + Dp * dp - yp[i]);
                 rnc[i] = R(Bc(gn) + Dn * dn + yp[i]);
                 gpnc[i] = rpc[i] / Dp - rnc[i] / Dn;
@@ -2811,15 +2825,72 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         for (int j = 0; j < c.nbk; ++j) {
             double w[8], zw[8], yd[4], sv[4], vl[4], vu[4], dres[4], dwv[8], ds[4], ydp[4];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); dwv[e] = c.B(B_DW + 8 * buf + e, j, k); }
+            for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 yd[r] = c.B(B_YD + r, j, k); sv[r] = c.B(B_S + r, j, k); vl[r] = c.B(B_VL + r, j, k);
-                vu[r] = c.B(B_VU + r, j, k); dres[r] = c.B(B_DR + r, j, k); ds[r] = c.B(B_DS + 4 * buf + r, j, k);
-                ydp[r] = c.B(B_YP + 4 * buf + r, j, k);
+                vu[r] = c.B(B_VU + r, j, k); dres[r] = c.B(B_DR + r, j, k);
             }
             Blk bk;
             bk.m = c.slab + threadIdx.x;
+            if (mode == NR_STEP) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) dwv[e] = c.B(B_DW + 8 * buf + e, j, k);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { ds[r] = c.B(B_DS + 4 * buf + r, j, k); ydp[r] = c.B(B_YP + 4 * buf + r, j, k); }
+            } else {
+                // ---- the block's part of the step (NR_MAIN) or of the correction (NR_CORR) from the factor record ----
+                auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
+                double fw[8], zf[8], t4[4], Dv[4], ypr[4], dwr[8];
+#pragma unroll
+                for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bk.idm[e] = ld(FR_IDM + e);
+                    zf[4 + e] = ld(FR_ZFL + e);
+                    t4[e] = ld(FR_T + e);
+                    Dv[e] = ld(FR_D + e);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) { bk.Zl(e, q) = ld(FR_ZL + 4 * e + q); bk.Yl(e, q) = ld(FR_YL + 4 * e + q); }
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
+                const bool trailer = (j & 1) != 0;
+                bk.jw0[0] = bk.jw0[2] = 0.5 * (trailer ? a.L2 : a.L1);
+                bk.jw0[1] = bk.jw0[3] = 0.5 * (trailer ? a.W2 : a.W1);
+                double dxr[6];
+#pragma unroll
+                for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)c.S(S_DX + 12 + i, k);
+                blk_recover(bk, fw, zf, t4, dxr, ypr, dwr);
+                const bool add = mode == NR_CORR;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    dwv[e] = add ? (double)c.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
+                    c.B(B_DW + 8 * buf + e, j, k) = dwv[e];
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double gs = add ? (double)c.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
+                    const double dsr = (ypr[r] - gs) / Dv[r];
+                    ydp[r] = add ? (double)c.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
+                    ds[r] = add ? (double)c.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
+                    c.B(B_YP + 4 * buf + r, j, k) = ydp[r];
+                    c.B(B_DS + 4 * buf + r, j, k) = ds[r];
+                    if (rs) {
+                        const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k);
+                        const double zp = c.B(B_ZP + r, j, k), zn = c.B(B_ZN + r, j, k);
+                        const double gp = add ? (double)c.B(B_OP + r, j, k) : RHO - mu / p;
+                        const double gn = add ? (double)c.B(B_ON + r, j, k) : RHO - mu / n;
+                        const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
+                        c.B(B_DP + 4 * buf + r, j, k) = add ? (double)c.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
+                        c.B(B_DN + 4 * buf + r, j, k) = add ? (double)c.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
+                    }
+                }
+            }
             blk_lin(a, x, tr, j, w, yd, bk);
             // x rows: W_xx dx + W_x lam dw_lam + Jx' y+
             rx[2] += bk.hxx22 * dx[2] + bk.hxx23 * dx[3];
@@ -2937,6 +3008,16 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         if (k == N && plan)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
+                if (mode == NR_MAIN) {  // the final rows' part of the step (phase_recover's)
+                    const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
+                    const double ypm = sh.Dfe[i] * (dx[i] + sh.rf[i]);
+                    sh.ydpf[buf][i] = ypm;
+                    sh.dsf[buf][i] = (ypm - (-mu / sl + mu / su)) / sh.Dsf[i];
+                    if (rs) {
+                        sh.dpf[buf][i] = (ypm - (RHO - mu / sh.pf[i])) / (sh.zpf[i] / sh.pf[i] + dw);
+                        sh.dnf[buf][i] = (-ypm - (RHO - mu / sh.nf[i])) / (sh.znf[i] / sh.nf[i] + dw);
+                    }
+                }
                 const double s = sh.sf[i], d = sh.dsf[buf][i], ypf = sh.ydpf[buf][i];
                 rx[i] += ypf;
                 const double sl = s - c.fL, su = c.fU - s;
@@ -2990,74 +3071,42 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
     wg_reduce(sh, out, ops);
 }
 
-// ---- correction solve, recovery: the blocks' y+, dw, ds (and the elastic-pair steps) of the correction in buffer 2,
-// with the constants phase_nres prepared; every component is added into the step in buffer buf ----
-__device__ __noinline__ void phase_recover_corr(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
+// ---- correction solve: its stage parts (dx, du, y+_c, the dynamics rows' elastic-pair steps, the final rows)
+// added into the step in buffer buf; the blocks' parts follow in phase_nres (NR_CORR), which reads the summed
+// stage fields of neighbouring stages (hence a pass of its own) ----
+__device__ __noinline__ void phase_stage_add(const Ctx& c, LShared& sh, double dw, int buf) {
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
-        double dx[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) dx[i] = c.S(S_DX + 12 + i, k);
+        double dxc[6], ypc[6], sdx[6], syp[6], sdp[6] = {0, 0, 0, 0, 0, 0}, sdn[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            const double ypc = c.S(S_YCP + 12 + i, k);
-            c.S(S_DX + 6 * buf + i, k) += dx[i];
-            c.S(S_YCP + 6 * buf + i, k) += ypc;
-            if (rs) {
+            dxc[i] = c.S(S_DX + 12 + i, k); ypc[i] = c.S(S_YCP + 12 + i, k);
+            sdx[i] = c.S(S_DX + 6 * buf + i, k); syp[i] = c.S(S_YCP + 6 * buf + i, k);
+        }
+        if (rs)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
                 const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
-                c.S(S_DP + 6 * buf + i, k) += (ypc - c.S(S_OP + i, k)) / (zp / p + dw);
-                c.S(S_DN + 6 * buf + i, k) += (-ypc - c.S(S_ON + i, k)) / (zn / n + dw);
+                sdp[i] = c.S(S_DP + 6 * buf + i, k) + (ypc[i] - c.S(S_OP + i, k)) / (zp / p + dw);
+                sdn[i] = c.S(S_DN + 6 * buf + i, k) + (-ypc[i] - c.S(S_ON + i, k)) / (zn / n + dw);
             }
-        }
+        double du0 = 0.0, du1 = 0.0;
         if (k < N) {
-            c.S(S_DU + 2 * buf, k) += c.S(S_DU + 4, k);
-            c.S(S_DU + 2 * buf + 1, k) += c.S(S_DU + 5, k);
+            du0 = c.S(S_DU + 2 * buf, k) + c.S(S_DU + 4, k);
+            du1 = c.S(S_DU + 2 * buf + 1, k) + c.S(S_DU + 5, k);
         }
-        for (int j = 0; j < c.nbk; ++j) {
-            Blk bk;
-            bk.m = c.slab + threadIdx.x;
-            double fw[8], zf[8], t4[4], yp[4], dwv[8], Dv[4];
-            auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
-#pragma unroll
-            for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                bk.idm[e] = ld(FR_IDM + e);
-                zf[4 + e] = ld(FR_ZFL + e);
-                t4[e] = ld(FR_T + e);
-                Dv[e] = ld(FR_D + e);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) { bk.Zl(e, q) = ld(FR_ZL + 4 * e + q); bk.Yl(e, q) = ld(FR_YL + 4 * e + q); }
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
-            const bool trailer = (j & 1) != 0;
-            bk.jw0[0] = bk.jw0[2] = 0.5 * (trailer ? c.a->L2 : c.a->L1);
-            bk.jw0[1] = bk.jw0[3] = 0.5 * (trailer ? c.a->W2 : c.a->W1);
-            blk_recover(bk, fw, zf, t4, dx, yp, dwv);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) c.B(B_DW + 8 * buf + e, j, k) += dwv[e];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                c.B(B_YP + 4 * buf + r, j, k) += yp[r];
-                c.B(B_DS + 4 * buf + r, j, k) += (yp[r] - c.B(B_OS + r, j, k)) / Dv[r];
-                if (rs) {
-                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k);
-                    const double zp = c.B(B_ZP + r, j, k), zn = c.B(B_ZN + r, j, k);
-                    c.B(B_DP + 4 * buf + r, j, k) += (yp[r] - c.B(B_OP + r, j, k)) / (zp / p + dw);
-                    c.B(B_DN + 4 * buf + r, j, k) += (-yp[r] - c.B(B_ON + r, j, k)) / (zn / n + dw);
-                }
-            }
+        for (int i = 0; i < 6; ++i) {
+            c.S(S_DX + 6 * buf + i, k) = sdx[i] + dxc[i];
+            c.S(S_YCP + 6 * buf + i, k) = syp[i] + ypc[i];
+            if (rs) { c.S(S_DP + 6 * buf + i, k) = sdp[i]; c.S(S_DN + 6 * buf + i, k) = sdn[i]; }
         }
+        if (k < N) { c.S(S_DU + 2 * buf, k) = du0; c.S(S_DU + 2 * buf + 1, k) = du1; }
         if (k == N && plan)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const double ypf = sh.Dfe[i] * (dx[i] + sh.rf[i]);
+                const double ypf = sh.Dfe[i] * (dxc[i] + sh.rf[i]);
                 sh.ydpf[buf][i] += ypf;
                 sh.dsf[buf][i] += (ypf - sh.osf[i]) / sh.Dsf[i];
                 if (rs) {
@@ -3069,9 +3118,10 @@ __device__ __noinline__ void phase_recover_corr(const Ctx& c, LShared& sh, doubl
 }
 
 // the correction solve of one refinement step: right-hand side prepared by phase_nres (prep), vector-only sweeps
-// through the stored factorisation into buffer 2, recovery added into buffer buf
+// through the stored factorisation into buffer 2, its stage parts added into buffer buf (the blocks' parts: the
+// next phase_nres, NR_CORR)
 __device__ __noinline__ void correction_solve(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
-    const bool soft = sh.R != 0;
+    const bool soft = sh.R != 0, on = c.a->stamps != nullptr;
     if (c.lds) {
         stage_vec_inputs(c, c.lds, soft);
         __syncthreads();
@@ -3092,28 +3142,30 @@ __device__ __noinline__ void correction_solve(const Ctx& c, LShared& sh, double 
         }
     }
     __syncthreads();
-    phase_recover_corr(c, sh, mu, dw, buf);
+    stamp(sh, on, OPH_REF_SWEEP);
+    phase_stage_add(c, sh, dw, buf);
     __syncthreads();
 }
 
-// iterative refinement of the step in buffer buf (factorisation and block recovery done).  rec: the line-search
-// quantities of the refined step (alpha_primal, alpha_dual, grad phi' d, max relative step), as phase_recover's
+// the step solve's recovery + IPOPT's iterative refinement for the step in buffer buf (factorisation, sweeps and
+// forward sweep done; the blocks' recovery is fused into the first residual pass).  rec: the line-search quantities
+// of the refined step (alpha_primal, alpha_dual, grad phi' d, max relative step), as phase_recover's
 __device__ __noinline__ void refine(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, double (&rec)[5]) {
     const bool on = c.a->stamps != nullptr;
     double q[7];
-    phase_nres(c, sh, mu, dw, tau, buf, true, q);
-    stamp(sh, on, OPH_REFINE);
+    phase_nres(c, sh, mu, dw, tau, buf, true, NR_MAIN, q);
+    stamp(sh, on, OPH_REC);
     double res = q[0];
     const double bnorm = q[1];
     for (int it = 0; it < 10; ++it) {
         if (it >= 1 && res <= 1e-10 * (fmin(q[2], 1e6) + bnorm)) break;
         // one correction is the rule (the oracle's census: > 99.9 % of the solves), so the check after it runs
         // without the correction's right-hand side; a second correction re-runs the residual pass with it
-        if (it >= 1) phase_nres(c, sh, mu, dw, tau, buf, true, q);
+        if (it >= 1) phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
         __syncthreads();
         correction_solve(c, sh, mu, dw, buf);
-        phase_nres(c, sh, mu, dw, tau, buf, false, q);
-        stamp(sh, on, OPH_REFINE);
+        phase_nres(c, sh, mu, dw, tau, buf, false, NR_CORR, q);
+        stamp(sh, on, OPH_REF_REC);
         const double res2 = q[0];
         if (!(res2 < res)) { res = res2; break; }  // no improvement: IPOPT stops refining
         res = res2;
@@ -3694,9 +3746,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 } else {
                     if (dw > 0) stt.dw_last = dw;
                     double rec[5];
-                    phase_recover(cs, sh, mu, dw, stt.tau, 0, rec);
-                    stamp(sh, ston, OPH_REC);
-                    if (cs.refine) refine(cs, sh, mu, dw, stt.tau, 0, rec);
+                    if (cs.refine) {
+                        refine(cs, sh, mu, dw, stt.tau, 0, rec);
+                    } else {
+                        phase_recover(cs, sh, mu, dw, stt.tau, 0, rec);
+                        stamp(sh, ston, OPH_REC);
+                    }
                     const double ap = rec[0], Dm = rec[2], rel = rec[3];
                     double az = rec[1], alpha = ap;
                     int buf = 0;
@@ -3739,9 +3794,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                                     __syncthreads();
                                     if (!newton_solve(cs, sh, mu, dw, 1)) break;
                                     double rs[5];
-                                    phase_recover(cs, sh, mu, dw, stt.tau, 1, rs);
-                                    stamp(sh, ston, OPH_REC);
-                                    if (cs.refine) refine(cs, sh, mu, dw, stt.tau, 1, rs);
+                                    if (cs.refine) {
+                                        refine(cs, sh, mu, dw, stt.tau, 1, rs);
+                                    } else {
+                                        phase_recover(cs, sh, mu, dw, stt.tau, 1, rs);
+                                        stamp(sh, ston, OPH_REC);
+                                    }
                                     a_soc = rs[0];
                                     double t2[3];
                                     phase_trial(cs, sh, mu, a_soc, 1, t2);
@@ -3801,6 +3859,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                         }
                     }
                     if (!accepted) {
+                        if (R && th0 <= 1e-2 * a.tol) {  // failed at an almost feasible point of the restoration
+                            status = 3;                    // NLP: IPOPT's RESTORATION_FAILED (oracle: same test)
+                            done = true;
+                            break;
+                        }
                         if (R) {  // restoration of the restoration phase: elastic pairs back to their closed form
                             phase_setpn(cs, sh, mu);
                             __syncthreads();

@@ -2545,6 +2545,14 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         }
         if (!accepted) {
             if (W->R == M_RESTO) {
+                if (th0 <= 1e-2 * P->tol) {
+                    /* the restoration NLP's own line search failed at one of its almost feasible points: IPOPT
+                     * (BacktrackingLineSearch, inside the restoration algorithm) tries to restore an acceptable
+                     * point of that NLP and otherwise throws RESTORATION_FAILED, which ends the solve
+                     * (Restoration_Failed; status 3 here) instead of resetting p/n forever */
+                    status = 3;
+                    break;
+                }
                 /* restoration of the restoration phase: elastic variables back to their closed form */
                 set_pn(W, mu);
                 S->F.n = 0;

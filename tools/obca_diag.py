@@ -1,6 +1,6 @@
 """CPU-oracle convergence census of an OBCA bench workload (development check, no GPU).
 
-    python tools/obca_diag.py c4|cobs|c4replan LO HI [max_iter] [out.npz]
+    python tools/obca_diag.py c4|c4all|cobs|c4replan LO HI [max_iter] [out.npz]
 $TTO_OPTS: oracle TTO_OPT_* bits (switch IPOPT features off for A/B runs).
 Solves instances LO..HI-1 of the bench's seed-0 batch with the C oracle (8 threads) and prints status /
 iteration counts, so solver changes can be judged on the instances the bench actually runs."""
@@ -23,12 +23,13 @@ G = REPO / "tests" / "golden"
 def workload(cfg, B=256):
     obs_all = sc.obstacles_array(sc.load_obstacles(G / "obstacles.json"))
     g = np.load(G / "reference_numpy.npz")
-    if cfg in ("c4", "c4replan"):
+    if cfg in ("c4", "c4all", "c4replan"):
         N, M = 200, 6
         obs = obs_all[:M]
-        if cfg == "c4":
+        if cfg in ("c4", "c4all"):
             cases = json.loads((G / "test_cases.json").read_text())["cases"]
-            x0, xg, zg = sc.obca_case_batch(cases, B, N, M, seed=0, obstacles=obs, params=sc.OBCA_PARAMS)
+            x0, xg, zg = sc.obca_case_batch(cases, B, N, M, seed=0, obstacles=obs if cfg == "c4" else None,
+                                            params=sc.OBCA_PARAMS)
         else:
             x0, xg, zg = sc.obca_replan_batch(g["state_traj"], B, N, M, seed=0)
         P = dict(N=N, params=sc.OBCA_PARAMS, bnd=(sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB), obs=obs,

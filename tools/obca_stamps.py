@@ -46,8 +46,8 @@ X, U, Z, st, it, kk = run()
 torch.cuda.synchronize()
 L.ttx_obca_set_stamps(s._h, None)
 cyc = d.cpu().numpy().astype(np.float64)
-names = ["lin", "compl", "factor", "riccati", "forward", "recover", "trial", "update/other", "riccati_soft",
-         "forward_soft", "refine", "TOTAL"]
+names = ["lin", "compl", "factor", "riccati", "forward", "recover(+resid)", "trial", "update/other", "riccati_soft",
+         "forward_soft", "ref_sweeps", "ref_recover_resid", "TOTAL"]
 per_it = cyc / np.maximum(it, 1)[:, None]
 print(f"{wl} B={B} iters mean {it.mean():.1f} max {it.max()}  status {np.bincount(st, minlength=6).tolist()}")
 for i, n in enumerate(names):
