@@ -2134,14 +2134,15 @@ __device__ __forceinline__ void add_filter(LShared& sh, int f, double th, double
 // ======== phase: linearisation at the iterate + optimality-error ingredients of the current NLP ========
 // out: [0] dual inf (max) [1] primal inf (max) [2] complementarity (max) [3] sum |y| + sum z [4] sum z
 //      [5] theta (l1 of the residual rows) [6] objective [7] sum log slacks [8] sum |dual residuals|
-//      [9] original theta [10] original cost [11] original sum log slacks (restoration: no p, n)
-__device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[12]) {
+//      [9] original theta [10] original cost [11] original sum log slacks [12] original primal inf (max)
+//      (restoration: the original problem's rows without p, n)
+__device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[13]) {
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0;
     const double zeta = sh.zeta;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) red[i] = 0.0;
+    for (int i = 0; i < 13; ++i) red[i] = 0.0;
     const double* xinit = a.x0 + 6 * (size_t)c.b;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0}, gl[6];
@@ -2219,6 +2220,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
             red[1] = fmax(red[1], fabs(res));
             red[5] += fabs(res);
             red[9] += fabs(ck[i]);
+            red[12] = fmax(red[12], fabs(ck[i]));
         }
         double yk[6], yn[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -2300,6 +2302,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
                 red[8] += fabs(td);
                 double res = bk.d[r] - s;
                 red[9] += fabs(res);
+                red[12] = fmax(red[12], fabs(res));
                 if (rs) {
                     const double p = prv[r], n = nrv[r], zp = zpv[r], zn = znv[r];
                     res -= p - n;
@@ -2340,6 +2343,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
                 red[8] += fabs(td);
                 double res = dfi - sh.sf[i];
                 red[9] += fabs(res);
+                red[12] = fmax(red[12], fabs(res));
                 if (rs) {
                     const double p = sh.pf[i], n = sh.nf[i], zp = sh.zpf[i], zn = sh.znf[i];
                     res -= p - n;
@@ -2403,7 +2407,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
         red[11] += lorig.value();
         if (!isfinite(red[0]) || !isfinite(red[1])) red[0] = INFINITY;
     }
-    const int ops[12] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM};
+    const int ops[13] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_MAX};
     wg_reduce(sh, red, ops);
 }
 
@@ -3443,7 +3447,7 @@ __device__ __noinline__ void phase_leave_resto(const Ctx& c, LShared& sh, double
 __device__ __noinline__ void ls_multipliers(const Ctx& c, LShared& sh) {
     if (threadIdx.x == 0) sh.lsq = 1;
     __syncthreads();
-    double red[12];
+    double red[13];
     phase_lin(c, sh, red);  // Jacobians at the iterate (y = 0: no curvature terms)
     phase_resid(c, sh, true);
     __syncthreads();
@@ -3656,7 +3660,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             IpmState stt = R ? S1 : S0;
             bool done = false, redo = false, switched = false;
             do {
-                double red[12];
+                double red[13];
                 stamp(sh, ston, OPH_UPD);
                 phase_lin(cs, sh, red);
                 stamp(sh, ston, OPH_LIN);
@@ -3690,7 +3694,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     first_resto = 0;
                     if (E0 <= a.acc_tol) ++stt.acc; else stt.acc = 0;
                     if (E0 <= a.tol || stt.acc >= a.acc_iter) {
-                        if (pinf <= 1e2 * a.tol || thO <= 1e2 * a.tol) {  // feasible but filter-unacceptable
+                        // IPOPT's RestoConvergenceCheck: the ORIGINAL problem's primal infeasibility (max norm) against
+                        // resto_failure_feasibility_threshold (default 1e2 tol)
+                        if (red[12] <= 1e2 * a.tol) {  // feasible but filter-unacceptable
                             phase_leave_resto(cs, sh, S0.mu, S0.tau);
                             if (tid == 0) sh.nfl[0] = 0;
                             __syncthreads();
@@ -3837,7 +3843,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                             __syncthreads();
                             phase_update(cs, sh, mu, as, as, 0);
                             __syncthreads();
-                            double rt[12];
+                            double rt[13];
                             phase_lin(cs, sh, rt);
                             const double pd_t = rt[8] + rt[5] + phase_compl(cs, sh, mu).y;
                             const bool fin = isfinite(rt[0]) && isfinite(rt[1]);

@@ -2330,11 +2330,17 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double* th0p, double*
 }
 
 /* original-problem theta / phi at the current iterate (also valid at a restoration iterate: the shared
- * variables x, u, w, s, sf) */
-static void orig_th_phi(ws_t* W, double mu, double* th, double* ph) {
+ * variables x, u, w, s, sf); *pmax: the original problem's primal infeasibility (max norm) */
+static void orig_th_phi(ws_t* W, double mu, double* th, double* ph, double* pmax) {
     double rfo[6] = {0};
     residuals(W, W->c, W->d, W->s, W->df, W->sf, NULL, NULL, W->cr, W->dr, rfo);
     *th = infeas1(W, W->cr, W->dr, rfo);
+    double m = 0.0;
+    for (int i = 0; i < W->nrc; ++i) m = fmax(m, fabs(W->cr[i]));
+    for (int i = 0; i < W->nrd; ++i) m = fmax(m, fabs(W->dr[i]));
+    if (W->mode == TTO_OBCA_PLAN)
+        for (int i = 0; i < 6; ++i) m = fmax(m, fabs(rfo[i]));
+    *pmax = m;
     int bad = 0;
     const double b = barrier(W, W->x, W->u, W->w, W->s, W->sf, NULL, NULL, mu, &bad);
     *ph = bad ? INFINITY : cost_eval(W, W->x, W->u) + b;
@@ -2459,8 +2465,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         } else {
             /* restoration convergence (RestoConvergenceCheck): original infeasibility reduced to kappa_resto of
              * its value at entry and the point acceptable to the augmented original filter */
-            double thO, phO;
-            orig_th_phi(W, SO.mu, &thO, &phO);
+            double thO, phO, pinfO;
+            orig_th_phi(W, SO.mu, &thO, &phO, &pinfO);
             if (dbg) fprintf(stderr, "rit %3d E0 %.3e dinf %.3e pinf %.3e muR %.2e thO %.3e (%.3e)\n", iter, E0, oe.dinf,
                              oe.pinf, S->mu, thO, th_resto0);
             if (!first_resto && thO <= KAPPA_RESTO * th_resto0 && thO <= SO.th_max && !in_filter(&SO.F, thO, phO)) {
@@ -2473,8 +2479,9 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
             if (E0 <= P->acc_tol) ++S->acc_count; else S->acc_count = 0;
             if (E0 <= P->tol || S->acc_count >= P->acc_iter) {
                 /* the restoration NLP converged (or converged to an acceptable point) without reaching a point
-                 * acceptable to the original problem */
-                if (oe.pinf <= 1e2 * P->tol || thO <= 1e2 * P->tol) {
+                 * acceptable to the original problem: IPOPT (RestoConvergenceCheck) compares the ORIGINAL problem's
+                 * primal infeasibility (max norm) with resto_failure_feasibility_threshold (default 1e2 tol) */
+                if (pinfO <= 1e2 * P->tol) {
                     leave_resto(W, SO.mu, SO.tau); /* feasible but filter-unacceptable: continue with a fresh filter */
                     SO.F.n = 0;
                     --iter;
