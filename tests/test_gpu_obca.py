@@ -108,12 +108,15 @@ def test_c4_test_cases_vs_oracle():
     gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
     blocked = (gs < 0.0) | (gg < 0.0)
-    assert blocked.sum() == 6 and np.all(st[blocked] > 1) and np.all(stc[blocked] > 1)
-    assert (st[~blocked] <= 1).sum() >= 5, st
+    # infeasible by construction: IPOPT's restoration failure (status 3) on both sides, not max_iter
+    assert blocked.sum() == 6 and np.all(st[blocked] == 3) and np.all(stc[blocked] == 3), (st, stc)
+    assert (st[~blocked] <= 1).sum() >= 6 and (stc[~blocked] <= 1).sum() >= 6, (st, stc)
     both = (st <= 1) & (stc <= 1)
+    assert both.sum() >= 6, (st, stc)
     Xc = co.obca_split(zc, 200, 6)[0]
-    same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6       # same local optimum (most; OBCA is nonconvex)
-    assert same[both].sum() >= both.sum() - 1
+    same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6       # same local optimum (OBCA is nonconvex)
+    assert same[both & (st == 0) & (stc == 0)].all()     # optimal-optimal pairs: identical primal
+    assert same[both].sum() >= both.sum() - 1            # an 'acceptable' stop may sit elsewhere
     ok = st <= 1
     assert np.abs(X[ok, -1] - xg[ok]).max() <= 1e-2 + 1e-7
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
@@ -131,11 +134,12 @@ def test_c4_replan_subset_vs_oracle():
     X, U, Z, st, it, kk = _solver(200, obs).solve(x0, xg, z_guess=zg)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs), x0, xg, z_guess=zg, nthreads=16)
     ok = st <= 1
-    assert ok.sum() >= 13 and (stc <= 1).sum() >= 13, (st, stc)
+    assert ok.sum() >= 15 and (stc <= 1).sum() >= 15, (st, stc)
     both = ok & (stc <= 1)
+    assert both.sum() >= 14, (st, stc)
     Xc = co.obca_split(zc, 200, 6)[0]
     same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6
-    assert same[both].sum() >= both.sum() - 3          # same local optimum on most instances
+    assert same[both].all(), np.abs(X - Xc).max(axis=(1, 2))[both]   # same local optimum wherever both stop
     nlp = ObcaNLP(200, 6, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
     for b in np.flatnonzero(ok):
         gv, lbg, ubg = nlp.g(Z[b], x0[b], xg[b])
@@ -155,8 +159,8 @@ def test_c4_full_batch_properties_and_determinism():
     gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
     blocked = (gs < 0.0) | (gg < 0.0)
-    assert not np.any(ok & blocked)
-    assert ok[~blocked].mean() >= 0.6, np.bincount(st[~blocked])
+    assert np.all(st[blocked] == 3), np.bincount(st[blocked])        # restoration failure, not max_iter
+    assert ok[~blocked].mean() >= 0.85, np.bincount(st[~blocked])
     dyn = X[:, 1:] - (X[:, :-1] + 0.1 * _f(X[:, :-1], U))
     assert np.abs(dyn[ok]).max() <= 1e-8
     assert np.abs(X[ok, 0] - x0[ok]).max() <= 1e-8
