@@ -710,6 +710,7 @@ def main_obca(args):
     if blocked is not None:
         solver_rec["infeasible_by_construction"] = int(blocked.sum())
         solver_rec["converged_of_feasible"] = f"{int(np.sum((status <= 1) & ~blocked))}/{int(np.sum(~blocked))}"
+    traffic, traffic_src = obca_traffic(args.config, float(iters.sum()))
     out = {
         "metric": f"OBCA {'plan' if args.config != 'cobs' else 'MPC+OBCA'} solves/sec (N={N}, M={M} obstacles, "
                   f"n={n} variables; converged or acceptable solves only)",
@@ -731,7 +732,7 @@ def main_obca(args):
                    "parallelism": f"dp{world} (independent instance shards)"},
         "solver": solver_rec,
         "roofline": {"bound": "valu_fp64", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP64_PEAK_TFLOPS, 7), "traffic": None,
+                     "frac": round(achieved / FP64_PEAK_TFLOPS, 7), "traffic": traffic, "traffic_source": traffic_src,
                      "note": "latency-bound (serial Riccati over N stages per instance, one workgroup per instance); "
                              "flops: SURVEY §8(d) C4 block-arrow formula x per-instance iterations"},
     }
@@ -777,8 +778,29 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 TRAFFIC_COMMIT = "fcd2080"
 
 
-def read_traffic(paths):
-    """HBM bytes per dispatch of track_kernel = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes), averaged over
+# committed PMC passes of obca_kernel (tools/obca_pmc.sh): HBM bytes per instance-iteration, scaled by a launch's
+# summed IPM iterations for roofline.traffic of the OBCA lines (same N, M; c4all shares c4's kernel shape)
+OBCA_PMC = {"c4": "profiles/r03/obca_pmc_300", "c4all": "profiles/r03/obca_pmc_300", "cobs": "profiles/r03/obca_pmc_cobs"}
+
+
+def obca_traffic(cfg, iters_sum):
+    d = OBCA_PMC.get(cfg)
+    if d is None or not (REPO / d / "fetch" / "fetch_counter_collection.csv").exists():
+        return None, None
+    per_launch = read_traffic([REPO / d / "fetch" / "fetch_counter_collection.csv",
+                               REPO / d / "write" / "write_counter_collection.csv"], kernel="obca_kernel")
+    rec = json.loads((REPO / d / "fetch.bench.json").read_text())["solver"]
+    if per_launch is None:
+        return None, None
+    per_iter = per_launch / (rec["iters_mean"] * rec["instances"])
+    src = (f"{d}: 2 x FETCH_SIZE + WRITE_SIZE of obca_kernel = {per_launch / 1e9:.1f} GB over "
+           f"{rec['instances']} x {rec['iters_mean']:.2f} instance-iterations = {per_iter / 1e6:.2f} MB per "
+           f"instance-iteration, x this launch's {int(iters_sum)} instance-iterations")
+    return round(per_iter * iters_sum, 1), src
+
+
+def read_traffic(paths, kernel="track_kernel"):
+    """HBM bytes per dispatch of `kernel` = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes), averaged over
     the dispatches in rocprofv3 --pmc counter_collection CSVs (FETCH_SIZE and WRITE_SIZE need separate
     passes on gfx950).  The x2 on FETCH_SIZE is the gfx950 correction of MI355X_MICROARCH.md; it was
     re-calibrated for this kernel's 8-B/lane loads with tools/calib_fetch.hip (1 GiB read -> 524,299 KB
@@ -788,7 +810,7 @@ def read_traffic(paths):
     for path in paths:
         with open(path) as fh:
             for row in csv.DictReader(fh):
-                if "track_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") in acc:
+                if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") in acc:
                     acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
     if not acc["FETCH_SIZE"] or not acc["WRITE_SIZE"]:
         return None
