@@ -128,7 +128,7 @@ EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_
                     "tt_collision_device", "tt_plant_update_device", "tt_warm_start_device",
                     "tt_record_solution_device", "tt_interpolate_device", "tt_lqr_score_device",
                     "tt_sim_window_indexed_device", "tt_sim_log_advance_device", "tt_policy_plant_device",
-                    "tt_fuzzy_weights_device")
+                    "tt_fuzzy_weights_device", "tt_plant_update_noise_device", "tt_policy_plant_noise_device")
 
 
 def _ptr(a):
