@@ -82,7 +82,7 @@ enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL,
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
 constexpr int kObcaStageFields = 353;
-constexpr int kObcaBlockFields = 288;
+constexpr int kObcaBlockFields = 212;
 __host__ __device__ inline size_t obca_ws_doubles(int N, int M) {
     return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
 }

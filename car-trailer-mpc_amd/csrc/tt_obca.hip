@@ -32,6 +32,22 @@
 
 #include "tt_kernel.hpp"
 
+// FMA contraction within a source expression only (the C rule), never across statements: the backend's
+// cross-statement fusion depends on how many uses a product has in the inlined context, so the same block
+// elimination could round differently in phase_factor and in the recovery passes that recompute it
+// (block_refactor); with contraction fixed by the source they are bitwise the same computation.
+#pragma clang fp contract(on)
+
+// A/B switch: phase_factor loads block j+1's inputs during block j (1) or each block's at its start (0)
+#ifndef OBCA_FACTOR_PF
+#define OBCA_FACTOR_PF 1
+#endif
+// A/B switch: the block elimination divides through shared reciprocals (v_rcp_f64 + two Newton steps, <= 1 ulp) and
+// takes 1/sqrt by v_rsq_f64 + Newton (1), or by IEEE division / sqrt (0)
+#ifndef OBCA_RCP
+#define OBCA_RCP 1
+#endif
+
 namespace ttmpc {
 namespace {
 
@@ -72,13 +88,11 @@ enum : int {
     B_SZW = 128, B_SVL = 136, B_SVU = 140, B_WACC = 144, B_SNAP = 152,
     // iterative refinement: slack and elastic-pair constants of the correction solve (read by its recovery)
     B_OS = 184, B_OP = 188, B_ON = 192,
-    // the block's elimination as phase_factor left it (read back by phase_recover instead of refactoring):
-    // G 16 | LT 10 | LL 10 | 1/dm 4 | zf_lam 4 | t 4 | Zl 16 | Yl 16 | fw 8 | D 4
-    // (LL and LT keep S_j / L_jj on their diagonals: the signs of the signed LDL' pivots)
-    B_FR = 196, B_END = 288
+    // the right-hand side of a correction solve (phase_nres prep -> NR_CORR): fw 8 | zf_lam 4 | t 4.  The elimination
+    // itself is recomputed by every pass that needs it (block_refactor), not stored.
+    B_FR = 196, B_END = 212
 };
-enum : int { FR_G = 0, FR_LT = 16, FR_LL = 26, FR_IDM = 36, FR_ZFL = 40, FR_T = 44, FR_ZL = 48, FR_YL = 64, FR_FW = 80,
-             FR_D = 88, FR_END = 92 };
+enum : int { FR_FW = 0, FR_ZFL = 8, FR_T = 12, FR_END = 16 };
 static_assert(B_FR + FR_END == B_END, "factor record");
 static_assert(B_END == kObcaBlockFields, "block field count");
 
@@ -180,6 +194,23 @@ __device__ __forceinline__ double frcp(double x) {
     return fma(r, e, r);
 }
 
+// 1/x for the barrier terms: frcp (OBCA_RCP) or IEEE division
+__device__ __forceinline__ double inv(double x) {
+#if OBCA_RCP
+    return frcp(x);
+#else
+    return 1.0 / x;
+#endif
+}
+
+// 1/sqrt(x) by v_rsq_f64 + two Newton steps (x finite, positive, normal)
+__device__ __forceinline__ double frsqrt(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    y = y * fma(-hx * y, y, 1.5);
+    return y * fma(-hx * y, y, 1.5);
+}
+
 // sum of logs as log(prod of mantissas) + (sum of exponents) ln 2
 struct LogSum {
     double m = 1.0;
@@ -219,9 +250,22 @@ struct Ctx {
     double fL, fU;          // final box
     const double* tgt_x;    // plan: x_goal; track: xref of this instance
     const double* tgt_u;    // track: uref
-    __device__ __forceinline__ gdouble& S(int f, int k) const { return ws[(size_t)f * NP + k]; }
+    // Field rows are uniform (scalar) offsets of the instance's workspace and k only ever adds a 32-bit lane offset,
+    // so every access is one global_load / global_store with an SGPR base and a VGPR byte offset (the "saddr" form)
+    // instead of 64-bit address arithmetic on the VALU per access.
+    __device__ __forceinline__ gdouble& at(size_t row, int k) const {
+        typedef __attribute__((address_space(1))) char gchar;
+        // the phases are separate (noinline) functions that receive the context in VGPRs: readfirstlane tells the
+        // compiler that the base and the stride are wave-uniform again
+        const unsigned long long wsu = (unsigned long long)ws;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)wsu), hi = __builtin_amdgcn_readfirstlane((unsigned)(wsu >> 32));
+        gdouble* const base = (gdouble*)(((unsigned long long)hi << 32) | lo);
+        const size_t np = (size_t)(unsigned)__builtin_amdgcn_readfirstlane(NP);
+        return *(gdouble*)((gchar*)(base + row * np) + (unsigned)k * 8u);
+    }
+    __device__ __forceinline__ gdouble& S(int f, int k) const { return at((size_t)f, k); }
     __device__ __forceinline__ gdouble& B(int f, int j, int k) const {
-        return ws[(size_t)S_END * NP + ((size_t)f * nbk + j) * NP + k];
+        return at((size_t)S_END + (size_t)f * (size_t)(unsigned)__builtin_amdgcn_readfirstlane(nbk) + j, k);
     }
     __device__ __forceinline__ bool hlx(int i) const { return (hx >> i) & 1; }
     __device__ __forceinline__ bool hux(int i) const { return (hx >> (8 + i)) & 1; }
@@ -333,7 +377,11 @@ typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: 
 // per-thread LDS slab of the block phases: the 48 doubles of Yl, Zl, G (field stride T, conflict-free).  Kept in
 // registers they were what the block elimination spilled to scratch, and every scratch reload waited behind
 // the factor-record stores (one in-order vmcnt); ds_ reads wait on lgkmcnt only.
-constexpr int kSlab = 48;
+// A/B switch: W_{x lam} of the block (16 doubles) in the slab too (1) or in registers (0)
+#ifndef OBCA_HXL_SLAB
+#define OBCA_HXL_SLAB 0
+#endif
+constexpr int kSlab = OBCA_HXL_SLAB ? 64 : 48;
 struct Blk {
     lds_double* m;                   // this thread's slab (Yl 0-15 | Zl 16-31 | G 32-47)
     __device__ __forceinline__ lds_double& Yl(int a, int r) const { return m[(a * 4 + r) * T]; }  // L^-1 Jw_lam'  [a][r]
@@ -345,7 +393,14 @@ struct Blk {
     double jw0[8], ca, sa, an, cn;   // Jw row 0 + the rotation/normal data of rows 1..3
     double hl, hw;
     double hxx22, hxx23, hxx33;
+#if OBCA_HXL_SLAB
+    __device__ __forceinline__ lds_double& H(int q, int a) const { return m[(48 + q * 4 + a) * T]; }  // W_{x lam} [q][a]
+#else
     double hxl[4][4];                // W_{x lam}: rows X,Y,theta,psi
+    __device__ __forceinline__ double& H(int q, int a) { return hxl[q][a]; }
+    __device__ __forceinline__ double H(int q, int a) const { return hxl[q][a]; }
+#endif
+    double haa, hac, hcc;            // the lam-lam Hessian y4 T'H4T (LL before the elimination), see hll
     // elimination
     double idm[4];                   // 1 / (Sigma_mu + dw) (mu block is diagonal)
     double LL[10];                   // chol of the lam block (1/L_ii on the diagonal)
@@ -370,7 +425,11 @@ __device__ __forceinline__ int schol4(double* L, bool pd) {
         if (!(s > 0.0) && (pd || !(s < -1e-14 * fabs(ajj)))) return -1;
         const double sj = s > 0.0 ? 1.0 : -1.0;
         neg += s < 0.0 ? 1 : 0;
+#if OBCA_RCP
+        const double ir = frsqrt(fabs(s));
+#else
         const double ir = frcp(sqrt(fabs(s)));
+#endif
         L[lo4(j, j)] = sj * ir;
 #pragma unroll
         for (int i = j + 1; i < 4; ++i) {
@@ -410,6 +469,13 @@ __device__ __forceinline__ void ssolve4(const double* L, double* b) {
     bsub4(L, b);
 }
 
+// entry (i, q), i >= q, of the lam-lam Hessian: T = [[1,0,-1,0],[0,1,0,-1]], H[i][q] = T0i(haa T0q + hac T1q) +
+// T1i(hac T0q + hcc T1q)
+__device__ __forceinline__ double hll(const Blk& k, int i, int q) {
+    const double T0[4] = {1, 0, -1, 0}, T1[4] = {0, 1, 0, -1};
+    return T0[i] * (k.haa * T0[q] + k.hac * T1[q]) + T1[i] * (k.hac * T0[q] + k.hcc * T1[q]);
+}
+
 __device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& tr, int j, const double* w, const double* y,
                                         Blk& k) {
     Geom g;
@@ -424,7 +490,11 @@ __device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& 
     k.d[2] = (w[1] - w[3]) - g.sa * aa + g.ca * cc;
     k.d[3] = nr - 1.0;
     nr = fmax(nr, 1e-12);
+#if OBCA_RCP
+    const double inr = frcp(nr);
+#else
     const double inr = 1.0 / nr;
+#endif
     k.e2 = -g.sa * aa + g.ca * cc;
     k.e3 = -g.ca * aa - g.sa * cc;
     k.angp = g.angp;
@@ -441,21 +511,28 @@ __device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& 
     k.hxx23 = -y1 * (aa * g.ptp0 + cc * g.ptp1) + rot * g.angp;
     k.hxx33 = -y1 * (aa * g.ppp0 + cc * g.ppp1) + rot * g.angp;
     const double r0 = -y2 * g.sa - y3 * g.ca, r1 = y2 * g.ca - y3 * g.sa;
-    k.hxl[0][0] = -y1; k.hxl[0][1] = 0.0; k.hxl[0][2] = y1; k.hxl[0][3] = 0.0;
-    k.hxl[1][0] = 0.0; k.hxl[1][1] = -y1; k.hxl[1][2] = 0.0; k.hxl[1][3] = y1;
-    k.hxl[2][0] = -y1 * g.dpt0 + r0; k.hxl[2][1] = -y1 * g.dpt1 + r1;
-    k.hxl[2][2] = y1 * g.dpt0 - r0;  k.hxl[2][3] = y1 * g.dpt1 - r1;
-    k.hxl[3][0] = -y1 * g.dpp0 + g.angp * r0; k.hxl[3][1] = -y1 * g.dpp1 + g.angp * r1;
-    k.hxl[3][2] = y1 * g.dpp0 - g.angp * r0;  k.hxl[3][3] = y1 * g.dpp1 - g.angp * r1;
+    k.H(0, 0) = -y1; k.H(0, 1) = 0.0; k.H(0, 2) = y1; k.H(0, 3) = 0.0;
+    k.H(1, 0) = 0.0; k.H(1, 1) = -y1; k.H(1, 2) = 0.0; k.H(1, 3) = y1;
+    k.H(2, 0) = -y1 * g.dpt0 + r0; k.H(2, 1) = -y1 * g.dpt1 + r1;
+    k.H(2, 2) = y1 * g.dpt0 - r0;  k.H(2, 3) = y1 * g.dpt1 - r1;
+    k.H(3, 0) = -y1 * g.dpp0 + g.angp * r0; k.H(3, 1) = -y1 * g.dpp1 + g.angp * r1;
+    k.H(3, 2) = y1 * g.dpp0 - g.angp * r0;  k.H(3, 3) = y1 * g.dpp1 - g.angp * r1;
     // lam-lam block y4 T'H4T (into LL, before the diagonal is added)
-    const double n3 = nr * nr * nr, haa = y4 * cc * cc / n3, hac = -y4 * aa * cc / n3, hcc = y4 * aa * aa / n3;
-    // T = [[1,0,-1,0],[0,1,0,-1]]: entries H[i][k] = T0i(haa T0k + hac T1k) + T1i(hac T0k + hcc T1k)
-    const double T0[4] = {1, 0, -1, 0}, T1[4] = {0, 1, 0, -1};
+#if OBCA_RCP
+    const double in3 = inr * inr * inr;
+    k.haa = y4 * cc * cc * in3;
+    k.hac = -y4 * aa * cc * in3;
+    k.hcc = y4 * aa * aa * in3;
+#else
+    const double n3 = nr * nr * nr;
+    k.haa = y4 * cc * cc / n3;
+    k.hac = -y4 * aa * cc / n3;
+    k.hcc = y4 * aa * aa / n3;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int q = 0; q <= i; ++q)
-            k.LL[lo4(i, q)] = T0[i] * (haa * T0[q] + hac * T1[q]) + T1[i] * (hac * T0[q] + hcc * T1[q]);
+        for (int q = 0; q <= i; ++q) k.LL[lo4(i, q)] = hll(k, i, q);
 }
 
 // Jx[r][q] (rows 0..3, cols X,Y,theta,psi)
@@ -511,7 +588,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
     for (int q = 0; q < 4; ++q) {
         double col[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) col[a] = k.hxl[q][a];
+        for (int a = 0; a < 4; ++a) col[a] = k.H(q, a);
         fsub4(k.LL, col);
 #pragma unroll
         for (int a = 0; a < 4; ++a) k.Zl(a, q) = col[a];
@@ -664,16 +741,16 @@ __device__ __forceinline__ double push_into(double v, double lo, double hi, bool
 }
 
 __device__ __forceinline__ void clamp_mult(double& z, double sl, double mu) {
-    const double ks = 1e10;
-    z = fmax(fmin(z, ks * mu / sl), mu / (ks * sl));
+    const double ks = 1e10, t = mu * inv(sl);
+    z = fmax(fmin(z, ks * t), t * (1.0 / ks));
 }
 
 // fraction to the boundary helpers
 __device__ __forceinline__ void ftb_lo(double v, double lo, double d, double tau, double& a) {
-    if (d < 0.0) a = fmin(a, -tau * (v - lo) / d);
+    if (d < 0.0) a = fmin(a, -tau * (v - lo) * inv(d));
 }
 __device__ __forceinline__ void ftb_hi(double v, double hi, double d, double tau, double& a) {
-    if (d > 0.0) a = fmin(a, tau * (hi - v) / d);
+    if (d > 0.0) a = fmin(a, tau * (hi - v) * inv(d));
 }
 
 // ---------------- restoration-phase elastic pairs (IPOPT MinC_1NrmRestorationPhase) ----------------
@@ -691,10 +768,18 @@ struct PN {
 };
 __device__ __forceinline__ PN pn_terms(bool lsq, double p, double n, double zp, double zn, double mu, double dw) {
     PN t;
+#if OBCA_RCP
+    const double ip = frcp(p), in_ = frcp(n);
+    t.Dp = lsq ? 1.0 : zp * ip + dw;
+    t.Dn = lsq ? 1.0 : zn * in_ + dw;
+    t.gp = RHO - (lsq ? zp : mu * ip);
+    t.gn = RHO - (lsq ? zn : mu * in_);
+#else
     t.Dp = lsq ? 1.0 : zp / p + dw;
     t.Dn = lsq ? 1.0 : zn / n + dw;
     t.gp = RHO - (lsq ? zp : mu / p);
     t.gn = RHO - (lsq ? zn : mu / n);
+#endif
     return t;
 }
 
@@ -765,6 +850,7 @@ __device__ __forceinline__ void load_blk_in(const Ctx& c, bool rs, int j, int k,
 // linearise + factor + rhs of one block at the current iterate (inputs preloaded); returns false if not
 // positive definite.  Outputs D (Sigma_s + dw), E (row regularisation), the elimination and the block's
 // Hessian / gradient contribution to its stage.
+template <bool RHS = true>
 __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, const BlkIn& in, int j, const double* x,
                                             const Trig& tr, double mu, double dw, Blk& bk, double* fw, double* zf,
                                             double* t4, double* C4, double* q4) {
@@ -778,13 +864,34 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, con
             hw = sh.zeta * in.drw[e];
             gw = hw * (in.w[e] - in.wr[e]);
         }
+#if OBCA_RCP
+        const double isl = frcp(sl);
+        sw[e] = lsq ? 1.0 : zw * isl + hw;
+        fw[e] = lsq ? gw - zw : gw - mu * isl;
+#else
         sw[e] = lsq ? 1.0 : zw / sl + hw;
         fw[e] = lsq ? gw - zw : gw - mu / sl;
+#endif
     }
     blk_lin(*c.a, x, tr, j, in.w, in.y, bk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const double s = in.s[r], vl = in.vl[r], vu = in.vu[r];
+#if OBCA_RCP
+        // 1 / (rU - s) and 1 / (s - rL) shared by the row's Sigma and barrier gradient
+        const double iu = frcp(c.rU(r) - s), il = c.hrl(r) ? frcp(s - c.rL(r)) : 0.0;
+        const double sg = c.hrl(r) ? vu * iu + vl * il : vu * iu, gr = c.hrl(r) ? mu * iu - mu * il : mu * iu;
+        bk.D[r] = lsq ? 1.0 : sg + dw;
+        bk.E[r] = frcp(bk.D[r]);
+        const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : gr;
+        rd[r] = in.dr[r] + gs * bk.E[r];
+        if (rs) {
+            const PN t = pn_terms(lsq, in.pr[r], in.nr[r], in.zp[r], in.zn[r], mu, dw);
+            const double ip = frcp(t.Dp), in_ = frcp(t.Dn);
+            bk.E[r] += ip + in_;
+            rd[r] += t.gp * ip - t.gn * in_;
+        }
+#else
         bk.D[r] = lsq ? 1.0 : sig_row(c, r, s, vl, vu) + dw;
         bk.E[r] = 1.0 / bk.D[r];
         const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
@@ -794,10 +901,24 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, con
             bk.E[r] += 1.0 / t.Dp + 1.0 / t.Dn;
             rd[r] += t.gp / t.Dp - t.gn / t.Dn;
         }
+#endif
     }
     if (!blk_factor(bk, sw, dw, C4, c.pd)) return false;
-    blk_rhs(bk, fw, rd, zf, t4, q4);
+    if constexpr (RHS) blk_rhs(bk, fw, rd, zf, t4, q4);
     return true;
+}
+
+// The block's elimination recomputed where a recovery pass needs it, from the same workspace inputs through the same
+// code as phase_factor (whose stage contributions C4 / q4 are dropped here).  Round 2 stored it as a 92-double record
+// on every inertia attempt (~2.5 per iteration) and read it back in every recovery pass: 30 % of the OBCA kernel's
+// HBM traffic for arithmetic the FP64 pipes redo at a fraction of the cost.  RHS: also the main solve's right-hand
+// side fw, zf, t (the correction solves read theirs from B_FR).
+template <bool RHS>
+__device__ __forceinline__ void block_refactor(const Ctx& c, const LShared& sh, const BlkIn& in, int j, const double* x,
+                                               const Trig& tr, double mu, double dw, Blk& bk, double* fw, double* zf,
+                                               double* t4) {
+    double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
+    block_setup<RHS>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
 }
 
 // ======== phase: stage Hessians + gradients (all threads) -> fail flag (uniform) ========
@@ -814,34 +935,23 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
         // the OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
         double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
         const Trig tr = stage_trig(x);
-        // software-pipelined inputs: block j+1's loads are issued before block j's factor-record stores, so
-        // waiting for them does not wait for the stores (one in-order vmcnt queue)
+        // only the stage contributions leave this pass: the recovery passes recompute the elimination
+        // (block_refactor), so a failed inertia attempt costs the block reads and no stores
         BlkIn cur;
+#if OBCA_FACTOR_PF
         load_blk_in(c, rs, 0, k, cur);
+#endif
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4];
+#if !OBCA_FACTOR_PF
+            load_blk_in(c, rs, j, k, cur);
+#endif
             if (!block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+#if OBCA_FACTOR_PF
             if (j + 1 < c.nbk) load_blk_in(c, rs, j + 1, k, cur);
-            auto st = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) st(FR_G + 4 * r + q, bk.G(r, q));
-#pragma unroll
-            for (int i = 0; i < 10; ++i) { st(FR_LT + i, bk.LT[i]); st(FR_LL + i, bk.LL[i]); }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                st(FR_IDM + a, bk.idm[a]);
-                st(FR_ZFL + a, zf[4 + a]);
-                st(FR_T + a, t4[a]);
-                st(FR_D + a, bk.D[a]);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) { st(FR_ZL + 4 * a + q, bk.Zl(a, q)); st(FR_YL + 4 * a + q, bk.Yl(a, q)); }
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) st(FR_FW + e, fw[e]);
+#endif
         }
         double Qs[21], qv[6];
         const double sc = (k == N && plan) ? a.tfac : 1.0;
@@ -863,14 +973,14 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
             const double xv = x[i];
             double sg = dw + (rs && !lsq ? sh.zeta * c.S(S_DRX + i, k) : 0.0), g = c.S(S_GX + i, k);
             if (c.hlx(i)) {
-                const double zl = c.S(S_ZLX + i, k);
-                sg += zl / (xv - c.xl[i]);
-                g -= lsq ? zl : mu / (xv - c.xl[i]);
+                const double zl = c.S(S_ZLX + i, k), il = inv(xv - c.xl[i]);
+                sg += zl * il;
+                g -= lsq ? zl : mu * il;
             }
             if (c.hux(i)) {
-                const double zu = c.S(S_ZUX + i, k);
-                sg += zu / (c.xu[i] - xv);
-                g += lsq ? zu : mu / (c.xu[i] - xv);
+                const double zu = c.S(S_ZUX + i, k), iu = inv(c.xu[i] - xv);
+                sg += zu * iu;
+                g += lsq ? zu : mu * iu;
             }
             if (!lsq) Qs[sy6(i, i)] += sg;
             qv[i] = g;
@@ -908,8 +1018,9 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
             double ce = c.S(S_CR + i, k), sd = 0.0;
             if (rs) {
                 const PN t = pn_terms(lsq, c.S(S_PR + i, k), c.S(S_NR + i, k), c.S(S_ZP + i, k), c.S(S_ZN + i, k), mu, dw);
-                ce += t.gp / t.Dp - t.gn / t.Dn;
-                sd = sqrt(1.0 / t.Dp + 1.0 / t.Dn);
+                const double ip = inv(t.Dp), in_ = inv(t.Dn);
+                ce += t.gp * ip - t.gn * in_;
+                sd = sqrt(ip + in_);
             }
             c.S(S_CE + i, k) = ce;
             c.S(S_SD + i, k) = sd;
@@ -927,10 +1038,10 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
                 R0 = (rs ? sh.zeta * c.S(S_DRU, k) : 2.0 * a.R[0]) + dw;
                 R1 = rs ? 0.0 : a.R[1] + a.R[2];
                 R3 = (rs ? sh.zeta * c.S(S_DRU + 1, k) : 2.0 * a.R[3]) + dw;
-                if (c.hlu(0)) { R0 += c.S(S_ZLU, k) / (u0 - c.ul[0]); g0 -= mu / (u0 - c.ul[0]); }
-                if (c.huu(0)) { R0 += c.S(S_ZUU, k) / (c.uu[0] - u0); g0 += mu / (c.uu[0] - u0); }
-                if (c.hlu(1)) { R3 += c.S(S_ZLU + 1, k) / (u1 - c.ul[1]); g1 -= mu / (u1 - c.ul[1]); }
-                if (c.huu(1)) { R3 += c.S(S_ZUU + 1, k) / (c.uu[1] - u1); g1 += mu / (c.uu[1] - u1); }
+                if (c.hlu(0)) { const double t = inv(u0 - c.ul[0]); R0 += c.S(S_ZLU, k) * t; g0 -= mu * t; }
+                if (c.huu(0)) { const double t = inv(c.uu[0] - u0); R0 += c.S(S_ZUU, k) * t; g0 += mu * t; }
+                if (c.hlu(1)) { const double t = inv(u1 - c.ul[1]); R3 += c.S(S_ZLU + 1, k) * t; g1 -= mu * t; }
+                if (c.huu(1)) { const double t = inv(c.uu[1] - u1); R3 += c.S(S_ZUU + 1, k) * t; g1 += mu * t; }
             }
             c.S(S_RT, k) = R0;
             c.S(S_RT + 1, k) = R1;
@@ -1320,7 +1431,11 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         for (int p = 0; p < 6; ++p) {
             const double piv = readlane_d(mv, 7 * p);
             const double aip = __shfl(mv, 6 * i + p), apj = __shfl(mv, 6 * p + j);
+#if OBCA_RCP
+            const double ip = frcp(piv);
+#else
             const double ip = 1.0 / piv;
+#endif
             const double nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : mv - aip * apj * ip;
             fail = fail || !(piv > 0.0);
             mv = act ? nv : 0.0;
@@ -1378,7 +1493,11 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         const double G11 = o.R3 + dt2 * Pt[8 * 4 + 4];
         const double det = G00 * G11 - G01 * G01;
         fail = fail || !(G00 > 0.0) || !(det > 0.0);
+#if OBCA_RCP
+        const double idet = frcp(det);
+#else
         const double idet = 1.0 / det;
+#endif
         const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
         double Pk = 0.0;
         if (act) {  // P_kk[ii][jj] = Q~ + (A'PA)[ii][jj] + H'K
@@ -1612,35 +1731,18 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 }
                 Dm += g * d;
             }
+        const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4], yp[4], dwv[8];
-            auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
-#pragma unroll
-            for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                bk.idm[a] = ld(FR_IDM + a);
-                zf[4 + a] = ld(FR_ZFL + a);
-                t4[a] = ld(FR_T + a);
-                bk.D[a] = ld(FR_D + a);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) { bk.Zl(a, q) = ld(FR_ZL + 4 * a + q); bk.Yl(a, q) = ld(FR_YL + 4 * a + q); }
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
-            const bool trailer = (j & 1) != 0;
-            bk.jw0[0] = bk.jw0[2] = 0.5 * (trailer ? c.a->L2 : c.a->L1);
-            bk.jw0[1] = bk.jw0[3] = 0.5 * (trailer ? c.a->W2 : c.a->W1);
+            BlkIn in;
+            load_blk_in(c, sh.R != 0, j, k, in);
+            block_refactor<true>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
             blk_recover(bk, fw, zf, t4, dx, yp, dwv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const double wv = c.B(B_W + e, j, k), z = c.B(B_ZW + e, j, k), sl = wv + RELAX, d = dwv[e];
+                const double wv = in.w[e], z = in.zw[e], sl = wv + RELAX, d = dwv[e];
                 c.B(B_DW + 8 * buf + e, j, k) = d;
                 rel = fmax(rel, fabs(d) / (1.0 + fabs(wv)));
                 Dm += fw[e] * d;
@@ -1650,8 +1752,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const double s = c.B(B_S + r, j, k);
-                const double vl = c.B(B_VL + r, j, k), vu = c.B(B_VU + r, j, k);
+                const double s = in.s[r], vl = in.vl[r], vu = in.vu[r];
                 const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
                 const double ds = (yp[r] - gs) / bk.D[r];
                 c.B(B_YP + 4 * buf + r, j, k) = yp[r];
@@ -1671,8 +1772,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 }
                 if (rs) {
                     double dp, dn;
-                    pn_step(c.B(B_PR + r, j, k), c.B(B_NR + r, j, k), c.B(B_ZP + r, j, k), c.B(B_ZN + r, j, k), yp[r],
-                            mu, dw, tau, dp, dn, ap, az, Dm, rel);
+                    pn_step(in.pr[r], in.nr[r], in.zp[r], in.zn[r], yp[r], mu, dw, tau, dp, dn, ap, az, Dm, rel);
                     c.B(B_DP + 4 * buf + r, j, k) = dp;
                     c.B(B_DN + 4 * buf + r, j, k) = dn;
                 }
@@ -1985,13 +2085,13 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
             const double xn = xv + alpha * dv;
             if (c.hlx(i)) {
                 const double sl = xv - c.xl[i], z = zl[i];
-                double zn2 = z + az * (mu / sl - z - z / sl * dv);
+                double zn2 = z + az * (mu * inv(sl) - z - z * inv(sl) * dv);
                 clamp_mult(zn2, xn - c.xl[i], mu);
                 c.S(S_ZLX + i, k) = zn2;
             }
             if (c.hux(i)) {
                 const double sl = c.xu[i] - xv, z = zu[i];
-                double zn2 = z + az * (mu / sl - z + z / sl * dv);
+                double zn2 = z + az * (mu * inv(sl) - z + z * inv(sl) * dv);
                 clamp_mult(zn2, c.xu[i] - xn, mu);
                 c.S(S_ZUX + i, k) = zn2;
             }
@@ -2000,7 +2100,7 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
             if (rs) {
                 const double p = pr[i], n = nr[i], zpv = zp[i], znv = zn[i];
                 const double pn = p + alpha * dp[i], nn = n + alpha * dn[i];
-                double zpn = zpv + az * (mu / p - zpv - zpv / p * dp[i]), znn = znv + az * (mu / n - znv - znv / n * dn[i]);
+                double zpn = zpv + az * (mu * inv(p) - zpv - zpv * inv(p) * dp[i]), znn = znv + az * (mu * inv(n) - znv - znv * inv(n) * dn[i]);
                 clamp_mult(zpn, pn, mu);
                 clamp_mult(znn, nn, mu);
                 c.S(S_PR + i, k) = pn;
@@ -2016,13 +2116,13 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                 const double un = uv + alpha * dv;
                 if (c.hlu(i)) {
                     const double sl = uv - c.ul[i], z = zlu[i];
-                    double zn2 = z + az * (mu / sl - z - z / sl * dv);
+                    double zn2 = z + az * (mu * inv(sl) - z - z * inv(sl) * dv);
                     clamp_mult(zn2, un - c.ul[i], mu);
                     c.S(S_ZLU + i, k) = zn2;
                 }
                 if (c.huu(i)) {
                     const double sl = c.uu[i] - uv, z = zuu[i];
-                    double zn2 = z + az * (mu / sl - z + z / sl * dv);
+                    double zn2 = z + az * (mu * inv(sl) - z + z * inv(sl) * dv);
                     clamp_mult(zn2, c.uu[i] - un, mu);
                     c.S(S_ZUU + i, k) = zn2;
                 }
@@ -2035,7 +2135,7 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                 const double w = cur.w[e], dv = cur.dw[e], z = cur.zw[e];
                 const double sl = w + RELAX;
                 wn[e] = w + alpha * dv;
-                double zn2 = z + az * (mu / sl - z - z / sl * dv);
+                double zn2 = z + az * (mu * inv(sl) - z - z * inv(sl) * dv);
                 clamp_mult(zn2, wn[e] + RELAX, mu);
                 zwn[e] = zn2;
             }
@@ -2044,12 +2144,12 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                 const double sv = cur.s[r], dv = cur.ds[r];
                 sn[r] = sv + alpha * dv;
                 const double vu = cur.vu[r], slu = c.rU(r) - sv;
-                double vu2 = vu + az * (mu / slu - vu + vu / slu * dv);
+                double vu2 = vu + az * (mu * inv(slu) - vu + vu * inv(slu) * dv);
                 clamp_mult(vu2, c.rU(r) - sn[r], mu);
                 vun[r] = vu2;
                 if (c.hrl(r)) {
                     const double vl = cur.vl[r], sll = sv - c.rL(r);
-                    double vl2 = vl + az * (mu / sll - vl - vl / sll * dv);
+                    double vl2 = vl + az * (mu * inv(sll) - vl - vl * inv(sll) * dv);
                     clamp_mult(vl2, sn[r] - c.rL(r), mu);
                     vln[r] = vl2;
                 }
@@ -2058,8 +2158,8 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                     const double p = cur.pr[r], n = cur.nr[r], zpv = cur.zp[r], znv = cur.zn[r];
                     prn[r] = p + alpha * cur.dp[r];
                     nrn[r] = n + alpha * cur.dn[r];
-                    double a1 = zpv + az * (mu / p - zpv - zpv / p * cur.dp[r]);
-                    double a2 = znv + az * (mu / n - znv - znv / n * cur.dn[r]);
+                    double a1 = zpv + az * (mu * inv(p) - zpv - zpv * inv(p) * cur.dp[r]);
+                    double a2 = znv + az * (mu * inv(n) - znv - znv * inv(n) * cur.dn[r]);
                     clamp_mult(a1, prn[r], mu);
                     clamp_mult(a2, nrn[r], mu);
                     zpn[r] = a1;
@@ -2088,8 +2188,8 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
             for (int i = 0; i < 6; ++i) {
                 const double s = sh.sf[i], d = sh.dsf[buf][i], sn = s + alpha * d;
                 const double sl = s - c.fL, su = c.fU - s;
-                double vl = sh.vLf[i] + az * (mu / sl - sh.vLf[i] - sh.vLf[i] / sl * d);
-                double vu = sh.vUf[i] + az * (mu / su - sh.vUf[i] + sh.vUf[i] / su * d);
+                double vl = sh.vLf[i] + az * (mu * inv(sl) - sh.vLf[i] - sh.vLf[i] * inv(sl) * d);
+                double vu = sh.vUf[i] + az * (mu * inv(su) - sh.vUf[i] + sh.vUf[i] * inv(su) * d);
                 clamp_mult(vl, sn - c.fL, mu);
                 clamp_mult(vu, c.fU - sn, mu);
                 sh.vLf[i] = vl;
@@ -2100,7 +2200,7 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
                     const double p = sh.pf[i], n = sh.nf[i], zp = sh.zpf[i], zn = sh.znf[i];
                     const double dp = sh.dpf[buf][i], dn = sh.dnf[buf][i];
                     const double pn = p + alpha * dp, nn = n + alpha * dn;
-                    double zpn = zp + az * (mu / p - zp - zp / p * dp), znn = zn + az * (mu / n - zn - zn / n * dn);
+                    double zpn = zp + az * (mu * inv(p) - zp - zp * inv(p) * dp), znn = zn + az * (mu * inv(n) - zn - zn * inv(n) * dn);
                     clamp_mult(zpn, pn, mu);
                     clamp_mult(znn, nn, mu);
                     sh.pf[i] = pn;
@@ -2612,10 +2712,61 @@ __device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft
         for (int i = 0; i < 9; ++i) r[65 + i] = aj[i];
     }
 }
+// row_newbcast:l (gfx90a+ DPP on a 64-bit move): every lane of a 16-lane row receives lane l of that row
+template <int L_>
+__device__ __forceinline__ double rowbc(double v) {
+    const long long b = __double_as_longlong(v);
+    return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + L_, 0xF, 0xF, false));
+}
+
+// A/B switch: riccati_vec with lane q owning component q of the cost-to-go vector and the other components
+// broadcast by DPP (1), or every lane carrying the whole vector and reading every operand (0).  Same operations in
+// the same order either way (bitwise identical).
+#ifndef OBCA_VEC_DPP
+#define OBCA_VEC_DPP 1
+#endif
 template <class Src>
 __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft) {
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
+#if OBCA_VEC_DPP
+    // lanes 0..5 hold p[q] (q = lane); the serial chain per stage is sv -> (soft: 6 broadcasts, 6 FMAs) -> 6
+    // broadcasts of p' -> np, with only the lane's own row of PY, K, QV and W read from LDS
+    const int q = lane < 6 ? lane : 0;
+    double pq = src.QV(q, N);
+    if (lane < 6) c.S(S_PV + q, N) = pq;
+    for (int k = N; k >= 1; --k) {
+        const int km = k - 1;
+        const double sv = pq - src.W(q, k);
+        double pp = sv;
+        if (soft) {
+            double t = sv;
+            t = fma(-src.PY(q, 0, k), rowbc<0>(sv), t);
+            t = fma(-src.PY(q, 1, k), rowbc<1>(sv), t);
+            t = fma(-src.PY(q, 2, k), rowbc<2>(sv), t);
+            t = fma(-src.PY(q, 3, k), rowbc<3>(sv), t);
+            t = fma(-src.PY(q, 4, k), rowbc<4>(sv), t);
+            t = fma(-src.PY(q, 5, k), rowbc<5>(sv), t);
+            pp = t;
+        }
+        const double pp0 = rowbc<0>(pp), pp1 = rowbc<1>(pp), pp2 = rowbc<2>(pp), pp3 = rowbc<3>(pp);
+        const double pp4 = rowbc<4>(pp), pp5 = rowbc<5>(pp);
+        const double g0 = fma(dt, pp5, src.RV(0, km)), g1 = fma(dt, pp4, src.RV(1, km));
+        const double gi0 = src.GI(0, km), gi1 = src.GI(1, km), gi2 = src.GI(2, km);
+        const double kf0 = -fma(gi0, g0, gi1 * g1), kf1 = -fma(gi1, g0, gi2 * g1);
+        double np = src.QV(q, km) + pp + fma(src.K(q, km), g0, src.K(6 + q, km) * g1);
+        // D' p' (D: 0:(0,2) 1:(0,5) 2:(1,2) 3:(1,5) 4:(2,4) 5:(2,5) 6:(3,3) 7:(3,4) 8:(3,5)): the lane's own row
+        double dj[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) dj[e] = src.AJ(e, km);
+        const double t2 = fma(dj[0], pp0, dj[2] * pp1), t3 = dj[6] * pp3, t4 = fma(dj[4], pp2, dj[7] * pp3);
+        const double t5 = fma(dj[1], pp0, fma(dj[3], pp1, fma(dj[5], pp2, dj[8] * pp3)));
+        if (q >= 2) np += q == 2 ? t2 : q == 3 ? t3 : q == 4 ? t4 : t5;
+        if (lane < 6) c.S(S_PV + q, km) = np;
+        if (lane == 0) { c.S(S_KF, km) = kf0; c.S(S_KF + 1, km) = kf1; }
+        pq = np;
+    }
+#else
     const int r = lane < 6 ? lane : 0;
     auto pick = [&](const double* v) {
         double t = v[0];
@@ -2665,6 +2816,7 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
 #pragma unroll
         for (int q = 0; q < 6; ++q) p[q] = np[q];
     }
+#endif
 }
 
 // ---- residuals of the un-condensed Newton rows at the step in buffer buf (+ the correction's right-hand side) ----
@@ -2689,7 +2841,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
     double rmax = 0.0, bmax = 0.0, snorm = 0.0, ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
     auto R = [&](double v) { rmax = fmax(rmax, fabs(v)); return v; };
     auto Bc = [&](double v) { bmax = fmax(bmax, fabs(v)); return v; };
-    auto dual = [&](double z, double dz) { if (dz < 0.0) az = fmin(az, -tau * z / dz); };
+    auto dual = [&](double z, double dz) { if (dz < 0.0) az = fmin(az, -tau * z * inv(dz)); };
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         const bool st = k < N;
         double x[6], dx[6], yp[6], ypn[6] = {0, 0, 0, 0, 0, 0}, dj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, wd[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -2721,20 +2873,20 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         for (int i = 0; i < 6; ++i) {
             const double xv = x[i], d = dx[i];
             double g = c.S(S_GX + i, k), sg = dw + (rs ? zeta * c.S(S_DRX + i, k) : 0.0);
-            rel = fmax(rel, fabs(d) / (1.0 + fabs(xv)));
+            rel = fmax(rel, fabs(d) * inv(1.0 + fabs(xv)));
             if (c.hlx(i)) {
-                const double sl = xv - c.xl[i], z = c.S(S_ZLX + i, k);
-                g -= mu / sl;
-                sg += z / sl;
+                const double is = inv(xv - c.xl[i]), z = c.S(S_ZLX + i, k);
+                g -= mu * is;
+                sg += z * is;
                 ftb_lo(xv, c.xl[i], d, tau, ap);
-                dual(z, mu / sl - z - z / sl * d);
+                dual(z, mu * is - z - z * is * d);
             }
             if (c.hux(i)) {
-                const double sl = c.xu[i] - xv, z = c.S(S_ZUX + i, k);
-                g += mu / sl;
-                sg += z / sl;
+                const double is = inv(c.xu[i] - xv), z = c.S(S_ZUX + i, k);
+                g += mu * is;
+                sg += z * is;
                 ftb_hi(xv, c.xu[i], d, tau, ap);
-                dual(z, mu / sl - z + z / sl * d);
+                dual(z, mu * is - z + z * is * d);
             }
             Dm += g * d;
             double t = Bc(g) + sg * d + yp[i] - ypn[i];
@@ -2755,20 +2907,20 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
             for (int i = 0; i < 2; ++i) {
                 const double uv = u[i], d = du[i];
                 double g = c.S(S_GU + i, k), sg = dw + (rs ? zeta * c.S(S_DRU + i, k) : 0.0);
-                rel = fmax(rel, fabs(d) / (1.0 + fabs(uv)));
+                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(uv)));
                 if (c.hlu(i)) {
-                    const double sl = uv - c.ul[i], z = c.S(S_ZLU + i, k);
-                    g -= mu / sl;
-                    sg += z / sl;
+                    const double is = inv(uv - c.ul[i]), z = c.S(S_ZLU + i, k);
+                    g -= mu * is;
+                    sg += z * is;
                     ftb_lo(uv, c.ul[i], d, tau, ap);
-                    dual(z, mu / sl - z - z / sl * d);
+                    dual(z, mu * is - z - z * is * d);
                 }
                 if (c.huu(i)) {
-                    const double sl = c.uu[i] - uv, z = c.S(S_ZUU + i, k);
-                    g += mu / sl;
-                    sg += z / sl;
+                    const double is = inv(c.uu[i] - uv), z = c.S(S_ZUU + i, k);
+                    g += mu * is;
+                    sg += z * is;
                     ftb_hi(uv, c.uu[i], d, tau, ap);
-                    dual(z, mu / sl - z + z / sl * d);
+                    dual(z, mu * is - z + z * is * d);
                 }
                 Dm += g * d;
                 double t = Bc(g) + sg * d - dt * ypn[i == 0 ? 5 : 4];
@@ -2799,7 +2951,8 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
-                const double Dp = zp / p + dw, Dn = zn / n + dw, gp = RHO - mu / p, gn = RHO - mu / n;
+                const double ip = inv(p), in_ = inv(n);
+                const double Dp = zp * ip + dw, Dn = zn * in_ + dw, gp = RHO - mu * ip, gn = RHO - mu * in_;
                 double dp, dn;
                 if (mode == NR_MAIN) {  // the pair's step from the new multiplier (phase_recover's pn_step)
                     dp = (yp[i] - gp) / Dp;
@@ -2816,10 +2969,10 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                 gpnc[i] = rpc[i] / Dp - rnc[i] / Dn;
                 ftb_lo(p, 0.0, dp, tau, ap);
                 ftb_lo(n, 0.0, dn, tau, ap);
-                dual(zp, mu / p - zp - zp / p * dp);
-                dual(zn, mu / n - zn - zn / n * dn);
+                dual(zp, mu * ip - zp - zp * ip * dp);
+                dual(zn, mu * in_ - zn - zn * in_ * dn);
                 Dm += gp * dp + gn * dn;
-                rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+                rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
             }
 #pragma unroll
         for (int i = 0; i < 6; ++i) R(rc[i]);
@@ -2827,75 +2980,66 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         double q4[4] = {0, 0, 0, 0};
         const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
-            double w[8], zw[8], yd[4], sv[4], vl[4], vu[4], dres[4], dwv[8], ds[4], ydp[4];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { w[e] = c.B(B_W + e, j, k); zw[e] = c.B(B_ZW + e, j, k); }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                yd[r] = c.B(B_YD + r, j, k); sv[r] = c.B(B_S + r, j, k); vl[r] = c.B(B_VL + r, j, k);
-                vu[r] = c.B(B_VU + r, j, k); dres[r] = c.B(B_DR + r, j, k);
-            }
+            BlkIn in;
+            load_blk_in(c, rs, j, k, in);
+            const double *w = in.w, *zw = in.zw, *sv = in.s, *vl = in.vl, *vu = in.vu, *dres = in.dr;
+            double dwv[8], ds[4], ydp[4];
             Blk bk;
             bk.m = c.slab + threadIdx.x;
+            // the elimination (block_refactor, which linearises too) where the pass recovers a step or prepares a
+            // correction's right-hand side; the linearisation alone otherwise
+            if (mode == NR_MAIN || mode == NR_CORR || prep) {
+                double fw[8], zf[8], t4[4];
+                if (mode == NR_MAIN) {
+                    block_refactor<true>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
+                } else {
+                    block_refactor<false>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
+                    if (mode == NR_CORR) {  // the correction's right-hand side, as the previous prep pass left it
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) fw[e] = c.B(B_FR + FR_FW + e, j, k);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) { zf[4 + e] = c.B(B_FR + FR_ZFL + e, j, k); t4[e] = c.B(B_FR + FR_T + e, j, k); }
+                    }
+                }
+                if (mode != NR_STEP) {
+                    // ---- the block's part of the step (NR_MAIN) or of the correction (NR_CORR) ----
+                    double ypr[4], dwr[8], dxr[6];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)c.S(S_DX + 12 + i, k);
+                    blk_recover(bk, fw, zf, t4, dxr, ypr, dwr);
+                    const bool add = mode == NR_CORR;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        dwv[e] = add ? (double)c.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
+                        c.B(B_DW + 8 * buf + e, j, k) = dwv[e];
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const double gs = add ? (double)c.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
+                        const double dsr = (ypr[r] - gs) / bk.D[r];
+                        ydp[r] = add ? (double)c.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
+                        ds[r] = add ? (double)c.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
+                        c.B(B_YP + 4 * buf + r, j, k) = ydp[r];
+                        c.B(B_DS + 4 * buf + r, j, k) = ds[r];
+                        if (rs) {
+                            const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
+                            const double gp = add ? (double)c.B(B_OP + r, j, k) : RHO - mu / p;
+                            const double gn = add ? (double)c.B(B_ON + r, j, k) : RHO - mu / n;
+                            const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
+                            c.B(B_DP + 4 * buf + r, j, k) = add ? (double)c.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
+                            c.B(B_DN + 4 * buf + r, j, k) = add ? (double)c.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
+                        }
+                    }
+                }
+            } else {
+                blk_lin(a, x, tr, j, w, in.y, bk);
+            }
             if (mode == NR_STEP) {
 #pragma unroll
                 for (int e = 0; e < 8; ++e) dwv[e] = c.B(B_DW + 8 * buf + e, j, k);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) { ds[r] = c.B(B_DS + 4 * buf + r, j, k); ydp[r] = c.B(B_YP + 4 * buf + r, j, k); }
-            } else {
-                // ---- the block's part of the step (NR_MAIN) or of the correction (NR_CORR) from the factor record ----
-                auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
-                double fw[8], zf[8], t4[4], Dv[4], ypr[4], dwr[8];
-#pragma unroll
-                for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    bk.idm[e] = ld(FR_IDM + e);
-                    zf[4 + e] = ld(FR_ZFL + e);
-                    t4[e] = ld(FR_T + e);
-                    Dv[e] = ld(FR_D + e);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) { bk.Zl(e, q) = ld(FR_ZL + 4 * e + q); bk.Yl(e, q) = ld(FR_YL + 4 * e + q); }
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) fw[e] = ld(FR_FW + e);
-                const bool trailer = (j & 1) != 0;
-                bk.jw0[0] = bk.jw0[2] = 0.5 * (trailer ? a.L2 : a.L1);
-                bk.jw0[1] = bk.jw0[3] = 0.5 * (trailer ? a.W2 : a.W1);
-                double dxr[6];
-#pragma unroll
-                for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)c.S(S_DX + 12 + i, k);
-                blk_recover(bk, fw, zf, t4, dxr, ypr, dwr);
-                const bool add = mode == NR_CORR;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    dwv[e] = add ? (double)c.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
-                    c.B(B_DW + 8 * buf + e, j, k) = dwv[e];
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const double gs = add ? (double)c.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
-                    const double dsr = (ypr[r] - gs) / Dv[r];
-                    ydp[r] = add ? (double)c.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
-                    ds[r] = add ? (double)c.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
-                    c.B(B_YP + 4 * buf + r, j, k) = ydp[r];
-                    c.B(B_DS + 4 * buf + r, j, k) = ds[r];
-                    if (rs) {
-                        const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k);
-                        const double zp = c.B(B_ZP + r, j, k), zn = c.B(B_ZN + r, j, k);
-                        const double gp = add ? (double)c.B(B_OP + r, j, k) : RHO - mu / p;
-                        const double gn = add ? (double)c.B(B_ON + r, j, k) : RHO - mu / n;
-                        const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
-                        c.B(B_DP + 4 * buf + r, j, k) = add ? (double)c.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
-                        c.B(B_DN + 4 * buf + r, j, k) = add ? (double)c.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
-                    }
-                }
             }
-            blk_lin(a, x, tr, j, w, yd, bk);
             // x rows: W_xx dx + W_x lam dw_lam + Jx' y+
             rx[2] += bk.hxx22 * dx[2] + bk.hxx23 * dx[3];
             rx[3] += bk.hxx23 * dx[2] + bk.hxx33 * dx[3];
@@ -2903,7 +3047,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
             for (int q = 0; q < 4; ++q) {
                 double t = 0.0;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) t += bk.hxl[q][e] * dwv[4 + e];
+                for (int e = 0; e < 4; ++e) t += bk.H(q, e) * dwv[4 + e];
 #pragma unroll
                 for (int r = 0; r < 3; ++r) t += jx(bk, r, q) * ydp[r];
                 rx[q] += t;
@@ -2912,88 +3056,73 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
             double rw[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                const double sl = w[e] + RELAX, d = dwv[e];
-                double hw = 0.0, gw = -mu / sl;
+                const double sl = w[e] + RELAX, isl = inv(sl), d = dwv[e];
+                double hw = 0.0, gw = -mu * isl;
                 if (rs) {
-                    hw = zeta * c.B(B_DRW + e, j, k);
-                    gw += hw * (w[e] - c.B(B_WR + e, j, k));
+                    hw = zeta * in.drw[e];
+                    gw += hw * (w[e] - in.wr[e]);
                 }
-                double t = Bc(gw) + (zw[e] / sl + dw + hw) * d;
+                double t = Bc(gw) + (zw[e] * isl + dw + hw) * d;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * ydp[r];
                 if (e >= 4) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) t += bk.hxl[q][e - 4] * dx[q];
+                    for (int q = 0; q < 4; ++q) t += bk.H(q, e - 4) * dx[q];
 #pragma unroll
-                    for (int b2 = 0; b2 < 4; ++b2) t += bk.LL[lo4(max(e - 4, b2), min(e - 4, b2))] * dwv[4 + b2];
+                    for (int b2 = 0; b2 < 4; ++b2) t += hll(bk, max(e - 4, b2), min(e - 4, b2)) * dwv[4 + b2];
                 }
                 rw[e] = R(t);
                 Dm += gw * d;
-                rel = fmax(rel, fabs(d) / (1.0 + fabs(w[e])));
+                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(w[e])));
                 snorm = fmax(snorm, fabs(d));
                 ftb_lo(w[e], -RELAX, d, tau, ap);
-                dual(zw[e], mu / sl - zw[e] - zw[e] / sl * d);
+                dual(zw[e], mu * isl - zw[e] - zw[e] * isl * d);
             }
             // slack, row and elastic-pair rows
             double rsl[4], rdv[4], rpv[4] = {0, 0, 0, 0}, rnv[4] = {0, 0, 0, 0}, Dpv[4] = {1, 1, 1, 1}, Dnv[4] = {1, 1, 1, 1};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const double s = sv[r], d = ds[r];
-                const double gs = grad_row(c, r, s, mu);
-                rsl[r] = R(Bc(gs) + (sig_row(c, r, s, vl[r], vu[r]) + dw) * d - ydp[r]);
+                const double iu = inv(c.rU(r) - s), il = c.hrl(r) ? inv(s - c.rL(r)) : 0.0;
+                const double gs = c.hrl(r) ? mu * iu - mu * il : mu * iu;
+                const double sgr = c.hrl(r) ? vu[r] * iu + vl[r] * il : vu[r] * iu;
+                rsl[r] = R(Bc(gs) + (sgr + dw) * d - ydp[r]);
                 double t = Bc(dres[r]) - d;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) t += jx(bk, r, q) * dx[q];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) t += jwm(bk, r, e) * dwv[e] + jwl(bk, r, e) * dwv[4 + e];
                 if (rs) {
-                    const double p = c.B(B_PR + r, j, k), n = c.B(B_NR + r, j, k);
-                    const double zp = c.B(B_ZP + r, j, k), zn = c.B(B_ZN + r, j, k);
+                    const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
                     const double dp = c.B(B_DP + 4 * buf + r, j, k), dn = c.B(B_DN + 4 * buf + r, j, k);
                     t += -dp + dn;
-                    Dpv[r] = zp / p + dw;
-                    Dnv[r] = zn / n + dw;
-                    const double gp = RHO - mu / p, gn = RHO - mu / n;
+                    const double ip = inv(p), in_ = inv(n);
+                    Dpv[r] = zp * ip + dw;
+                    Dnv[r] = zn * in_ + dw;
+                    const double gp = RHO - mu * ip, gn = RHO - mu * in_;
                     rpv[r] = R(Bc(gp) + Dpv[r] * dp - ydp[r]);
                     rnv[r] = R(Bc(gn) + Dnv[r] * dn + ydp[r]);
                     ftb_lo(p, 0.0, dp, tau, ap);
                     ftb_lo(n, 0.0, dn, tau, ap);
-                    dual(zp, mu / p - zp - zp / p * dp);
-                    dual(zn, mu / n - zn - zn / n * dn);
+                    dual(zp, mu * ip - zp - zp * ip * dp);
+                    dual(zn, mu * in_ - zn - zn * in_ * dn);
                     Dm += gp * dp + gn * dn;
-                    rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+                    rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
                 }
                 rdv[r] = R(t);
                 Dm += gs * d;
-                rel = fmax(rel, fabs(d) / (1.0 + fabs(s)));
-                const double slu = c.rU(r) - s;
+                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(s)));
                 ftb_hi(s, c.rU(r), d, tau, ap);
-                dual(vu[r], mu / slu - vu[r] + vu[r] / slu * d);
+                dual(vu[r], mu * iu - vu[r] + vu[r] * iu * d);
                 if (c.hrl(r)) {
-                    const double sll = s - c.rL(r);
                     ftb_lo(s, c.rL(r), d, tau, ap);
-                    dual(vl[r], mu / sll - vl[r] - vl[r] / sll * d);
+                    dual(vl[r], mu * il - vl[r] - vl[r] * il * d);
                 }
             }
-            if (prep) {
-                auto ld = [&](int f) { return (double)c.B(B_FR + f, j, k); };
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) bk.G(r, q) = ld(FR_G + 4 * r + q);
-#pragma unroll
-                for (int i = 0; i < 10; ++i) { bk.LT[i] = ld(FR_LT + i); bk.LL[i] = ld(FR_LL + i); }
-                double Dv[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    bk.idm[e] = ld(FR_IDM + e);
-                    Dv[e] = ld(FR_D + e);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) { bk.Zl(e, q) = ld(FR_ZL + 4 * e + q); bk.Yl(e, q) = ld(FR_YL + 4 * e + q); }
-                }
+            if (prep) {  // bk holds the elimination (block_refactor above)
                 double rdc[4], zf[8], t4[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / Dv[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
+                for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / bk.D[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
                 blk_rhs(bk, rw, rdc, zf, t4, q4);
                 auto stf = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
 #pragma unroll
@@ -3042,11 +3171,11 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                     dual(zp, mu / p - zp - zp / p * dp);
                     dual(zn, mu / n - zn - zn / n * dn);
                     Dm += gp * dp + gn * dn;
-                    rel = fmax(rel, fmax(fabs(dp) / (1.0 + fabs(p)), fabs(dn) / (1.0 + fabs(n))));
+                    rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
                 }
                 R(rf);
                 Dm += gs * d;
-                rel = fmax(rel, fabs(d) / (1.0 + fabs(s)));
+                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(s)));
                 ftb_lo(s, c.fL, d, tau, ap);
                 ftb_hi(s, c.fU, d, tau, ap);
                 dual(sh.vLf[i], mu / sl - sh.vLf[i] - sh.vLf[i] / sl * d);
