@@ -377,11 +377,7 @@ typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: 
 // per-thread LDS slab of the block phases: the 48 doubles of Yl, Zl, G (field stride T, conflict-free).  Kept in
 // registers they were what the block elimination spilled to scratch, and every scratch reload waited behind
 // the factor-record stores (one in-order vmcnt); ds_ reads wait on lgkmcnt only.
-// A/B switch: W_{x lam} of the block (16 doubles) in the slab too (1) or in registers (0)
-#ifndef OBCA_HXL_SLAB
-#define OBCA_HXL_SLAB 0
-#endif
-constexpr int kSlab = OBCA_HXL_SLAB ? 64 : 48;
+constexpr int kSlab = 48;
 struct Blk {
     lds_double* m;                   // this thread's slab (Yl 0-15 | Zl 16-31 | G 32-47)
     __device__ __forceinline__ lds_double& Yl(int a, int r) const { return m[(a * 4 + r) * T]; }  // L^-1 Jw_lam'  [a][r]
@@ -393,13 +389,9 @@ struct Blk {
     double jw0[8], ca, sa, an, cn;   // Jw row 0 + the rotation/normal data of rows 1..3
     double hl, hw;
     double hxx22, hxx23, hxx33;
-#if OBCA_HXL_SLAB
-    __device__ __forceinline__ lds_double& H(int q, int a) const { return m[(48 + q * 4 + a) * T]; }  // W_{x lam} [q][a]
-#else
     double hxl[4][4];                // W_{x lam}: rows X,Y,theta,psi
     __device__ __forceinline__ double& H(int q, int a) { return hxl[q][a]; }
     __device__ __forceinline__ double H(int q, int a) const { return hxl[q][a]; }
-#endif
     double haa, hac, hcc;            // the lam-lam Hessian y4 T'H4T (LL before the elimination), see hll
     // elimination
     double idm[4];                   // 1 / (Sigma_mu + dw) (mu block is diagonal)
@@ -1285,8 +1277,11 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
     for (; k >= 1; k -= 2) {
         stage(k, oa, ob);
         stage(k - 1, ob, oa);
+        // a failed inertia attempt is discarded (the caller raises delta_w): stop at the first failed pivot
+        // instead of finishing the sweep (fail is wave-uniform: every lane evaluates the same G)
+        if (__builtin_amdgcn_readfirstlane((int)fail)) break;
     }
-    if (k == 0) stage(0, oa, ob);
+    if (k == 0 && !fail) stage(0, oa, ob);
     // any lane's failure flag (all lanes evaluate the same uniform G; keep it explicit)
     if (lane == 0) sh.flag = fail ? 1 : 0;
     wave_sync();
@@ -1412,6 +1407,8 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
     const int ii = min(i, j), jj = max(i, j), sij = sy6(ii, jj);
     const ColMask mj(j), mi(ii), mr(r);
     __shared__ double Pt[48], Yt[48], Tt[48];
+    constexpr int DT = 47;                   // dead tile slot (no reader: entries are 8 i + j, i, j < 6)
+    const int tij = act ? 8 * i + j : DT;    // this lane's tile entry, or the dead slot
     if (act) {
         const double q = src.QT(sij, N);
         Pt[8 * i + j] = q;
@@ -1440,54 +1437,50 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
             fail = fail || !(piv > 0.0);
             mv = act ? nv : 0.0;
         }
+        // Branch-free from here on: every lane evaluates the entry expressions at its clamped (i, j) / r and only the
+        // stores are predicated -- tile stores of idle lanes go to the dead slot DT (no exec-mask branch around each
+        // expression; the HBM stores keep theirs)
         const double mji = __shfl(mv, 6 * j + i);
-        if (act) {
-            // Y = S M^-1 S from the upper entry (symmetric by construction)
-            const double y = i <= j ? cur.si * mv * cur.sj : cur.sj * mji * cur.si;
-            Yt[8 * i + j] = y;
-            if (i <= j) c.S(S_Y + sij, k) = y;
-        }
+        // Y = S M^-1 S from the upper entry (symmetric by construction)
+        const double y = i <= j ? cur.si * mv * cur.sj : cur.sj * mji * cur.si;
+        Yt[tij] = y;
+        if (act && i <= j) c.S(S_Y + sij, k) = y;
         lds_order();
-        if (act) {
+        {
             double t = 0.0;
 #pragma unroll
             for (int l = 0; l < 6; ++l) t = fma(Pt[8 * i + l], Yt[8 * l + j], t);
-            Tt[8 * i + j] = t;  // P Y
+            Tt[tij] = t;  // P Y
         }
         double pl[6];
 #pragma unroll
         for (int q = 0; q < 6; ++q) pl[q] = readlane_d(pv, 48 + q);
         lds_order();
-        double nP = 0.0, npv = pv;
-        if (act) {
+        double nP, npv = pv;
+        {
             double t = Pt[8 * ii + jj];
 #pragma unroll
             for (int l = 0; l < 6; ++l) t = fma(-Tt[8 * ii + l], Pt[8 * l + jj], t);
             nP = t;
         }
-        if (vec) {
 #pragma unroll
-            for (int l = 0; l < 6; ++l) npv = fma(-Tt[8 * r + l], pl[l], npv);
-        }
+        for (int l = 0; l < 6; ++l) npv = fma(-Tt[8 * r + l], pl[l], npv);
         lds_order();
-        if (act) Pt[8 * i + j] = nP;
+        Pt[tij] = nP;
         pv = npv;
         lds_order();
         if (k == 0) return;
         // ---- stage kk = k-1 on P~_k, p~_k
         const int kk = k - 1;
         const RicOps& o = cur.r;
-        if (act) {  // PA[i][j] = P[i][j] + sum_{l<4} P[i][l] D[l][j]
+        {  // PA[i][j] = P[i][j] + sum_{l<4} P[i][l] D[l][j]
             double c0, c1, c2, c3;
             dcol(o.dj, mj, c0, c1, c2, c3);
-            Tt[8 * i + j] = fma(Pt[8 * i + 0], c0, fma(Pt[8 * i + 1], c1, fma(Pt[8 * i + 2], c2, fma(Pt[8 * i + 3], c3, Pt[8 * i + j]))));
+            Tt[tij] = fma(Pt[8 * i + 0], c0, fma(Pt[8 * i + 1], c1, fma(Pt[8 * i + 2], c2, fma(Pt[8 * i + 3], c3, Pt[8 * i + j]))));
         }
-        double pp = 0.0;
-        if (vec) {
-            pp = pv;
+        double pp = pv;
 #pragma unroll
-            for (int q = 0; q < 6; ++q) pp = fma(-Pt[8 * r + q], o.e[q], pp);
-        }
+        for (int q = 0; q < 6; ++q) pp = fma(-Pt[8 * r + q], o.e[q], pp);
         lds_order();
         const double G00 = o.R0 + dt2 * Pt[8 * 5 + 5], G01 = o.R1 + dt2 * Pt[8 * 5 + 4];
         const double G11 = o.R3 + dt2 * Pt[8 * 4 + 4];
@@ -1499,8 +1492,8 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         const double idet = 1.0 / det;
 #endif
         const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
-        double Pk = 0.0;
-        if (act) {  // P_kk[ii][jj] = Q~ + (A'PA)[ii][jj] + H'K
+        double Pk;
+        {  // P_kk[ii][jj] = Q~ + (A'PA)[ii][jj] + H'K
             double c0, c1, c2, c3;
             dcol(o.dj, mi, c0, c1, c2, c3);
             const double atpa = fma(c0, Tt[8 * 0 + jj], fma(c1, Tt[8 * 1 + jj], fma(c2, Tt[8 * 2 + jj], fma(c3, Tt[8 * 3 + jj], Tt[8 * ii + jj]))));
@@ -1513,8 +1506,8 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, 48 + q);
         const double g0 = fma(dt, ppl[5], o.rv0), g1 = fma(dt, ppl[4], o.rv1);
         const double kf0 = -fma(Gi00, g0, Gi01 * g1), kf1 = -fma(Gi01, g0, Gi11 * g1);
-        double pnew = 0.0;
-        if (vec) {
+        double pnew;
+        {
             double c0, c1, c2, c3;
             dcol(o.dj, mr, c0, c1, c2, c3);
             double ppr = ppl[0];
@@ -1522,9 +1515,12 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
             for (int q = 1; q < 6; ++q) ppr = r == q ? ppl[q] : ppr;
             const double H0 = dt * Tt[8 * 5 + r], H1 = dt * Tt[8 * 4 + r];
             pnew = o.qv + fma(c0, ppl[0], fma(c1, ppl[1], fma(c2, ppl[2], fma(c3, ppl[3], ppr)))) + fma(H0, kf0, H1 * kf1);
-            out.setK(r, kk, -fma(Gi00, H0, Gi01 * H1));
-            out.setK(6 + r, kk, -fma(Gi01, H0, Gi11 * H1));
-            out.setPV(r, kk, pnew);
+            const double K0 = -fma(Gi00, H0, Gi01 * H1), K1 = -fma(Gi01, H0, Gi11 * H1);
+            if (vec) {
+                out.setK(r, kk, K0);
+                out.setK(6 + r, kk, K1);
+                out.setPV(r, kk, pnew);
+            }
         }
         if (lane == 0) {
             out.setKF(0, kk, kf0);
@@ -1533,7 +1529,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         }
         if (act && i <= j) out.setP(sij, kk, Pk);
         lds_order();
-        if (act) Pt[8 * i + j] = Pk;
+        Pt[tij] = Pk;
         pv = pnew;
         lds_order();
     };
@@ -1543,8 +1539,11 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
     for (; k >= 1; k -= 2) {
         stage(k, oa, ob);
         stage(k - 1, ob, oa);
+        // stop at the first failed pivot (M or G): the attempt is discarded (fail is wave-uniform -- pivots by
+        // v_readlane, G from tile broadcasts)
+        if (__builtin_amdgcn_readfirstlane((int)fail)) break;
     }
-    if (k == 0) stage(0, oa, ob);
+    if (k == 0 && !fail) stage(0, oa, ob);
     if (lane == 0) sh.flag = fail ? 1 : 0;
     wave_sync();
 }
@@ -2759,9 +2758,10 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
         double dj[9];
 #pragma unroll
         for (int e = 0; e < 9; ++e) dj[e] = src.AJ(e, km);
-        const double t2 = fma(dj[0], pp0, dj[2] * pp1), t3 = dj[6] * pp3, t4 = fma(dj[4], pp2, dj[7] * pp3);
+        // (row 3 as the contracted np[3] += dj[6] * pp[3] of the redundant version: bitwise the same)
+        const double t2 = fma(dj[0], pp0, dj[2] * pp1), t4 = fma(dj[4], pp2, dj[7] * pp3);
         const double t5 = fma(dj[1], pp0, fma(dj[3], pp1, fma(dj[5], pp2, dj[8] * pp3)));
-        if (q >= 2) np += q == 2 ? t2 : q == 3 ? t3 : q == 4 ? t4 : t5;
+        np = q == 2 ? np + t2 : q == 3 ? fma(dj[6], pp3, np) : q == 4 ? np + t4 : q == 5 ? np + t5 : np;
         if (lane < 6) c.S(S_PV + q, km) = np;
         if (lane == 0) { c.S(S_KF, km) = kf0; c.S(S_KF + 1, km) = kf1; }
         pq = np;
