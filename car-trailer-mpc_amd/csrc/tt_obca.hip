@@ -278,6 +278,30 @@ struct Ctx {
     __device__ __forceinline__ double rU(int r) const { return (r == 1 || r == 2) ? rhi : RELAX; }
 };
 
+// The workspace as one phase sees it: base and strides read once per phase through readfirstlane, so they sit in
+// SGPRs (a noinline phase receives the context through memory, i.e. in VGPRs) and every field access is an SGPR base
+// plus this lane's 32-bit byte offset -- one global_load / global_store, no per-access VALU address arithmetic.
+struct WsView {
+    gdouble* base;
+    size_t np, bstart, nbk;
+    __device__ __forceinline__ gdouble& at(size_t row, int k) const {
+        typedef __attribute__((address_space(1))) char gchar;
+        return *(gdouble*)((gchar*)(base + row * np) + (unsigned)k * 8u);
+    }
+    __device__ __forceinline__ gdouble& S(int f, int k) const { return at((size_t)f, k); }
+    __device__ __forceinline__ gdouble& B(int f, int j, int k) const { return at(bstart + (size_t)f * nbk + j, k); }
+};
+__device__ __forceinline__ WsView ws_view(const Ctx& c) {
+    const unsigned long long w = (unsigned long long)c.ws;
+    WsView v;
+    v.base = (gdouble*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(w >> 32)) << 32) |
+                        (unsigned)__builtin_amdgcn_readfirstlane((unsigned)w));
+    v.np = (size_t)(unsigned)__builtin_amdgcn_readfirstlane(c.NP);
+    v.nbk = (size_t)(unsigned)__builtin_amdgcn_readfirstlane(c.nbk);
+    v.bstart = (size_t)S_END;
+    return v;
+}
+
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
 __device__ __forceinline__ void model_f(LArgs& a, const double* x, const double* u, double* fo) {
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
@@ -917,6 +941,7 @@ __device__ __forceinline__ void block_refactor(const Ctx& c, const LShared& sh, 
 // Also the effective dynamics-row residuals S_CE (= S_CR outside the restoration phase) and the soft-row
 // scales S_SD = sqrt(1/D_p + 1/D_n) of the restoration phase.
 __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, double dw) {
+    const WsView vw = ws_view(c);
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0, lsq = sh.lsq != 0;
@@ -952,25 +977,25 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
             for (int j2 = i; j2 < 6; ++j2)
                 Qs[sy6(i, j2)] = lsq ? (i == j2 ? 1.0 : 0.0) : rs ? 0.0 : sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
         if (k < N && !lsq) {
-            Qs[sy6(2, 2)] += c.S(S_WD + 0, k);
-            Qs[sy6(2, 5)] += c.S(S_WD + 1, k);
-            Qs[sy6(3, 3)] += c.S(S_WD + 2, k);
-            Qs[sy6(3, 4)] += c.S(S_WD + 3, k);
-            Qs[sy6(3, 5)] += c.S(S_WD + 4, k);
-            Qs[sy6(4, 4)] += c.S(S_WD + 5, k);
-            Qs[sy6(4, 5)] += c.S(S_WD + 6, k);
+            Qs[sy6(2, 2)] += vw.S(S_WD + 0, k);
+            Qs[sy6(2, 5)] += vw.S(S_WD + 1, k);
+            Qs[sy6(3, 3)] += vw.S(S_WD + 2, k);
+            Qs[sy6(3, 4)] += vw.S(S_WD + 3, k);
+            Qs[sy6(3, 5)] += vw.S(S_WD + 4, k);
+            Qs[sy6(4, 4)] += vw.S(S_WD + 5, k);
+            Qs[sy6(4, 5)] += vw.S(S_WD + 6, k);
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double xv = x[i];
-            double sg = dw + (rs && !lsq ? sh.zeta * c.S(S_DRX + i, k) : 0.0), g = c.S(S_GX + i, k);
+            double sg = dw + (rs && !lsq ? sh.zeta * vw.S(S_DRX + i, k) : 0.0), g = vw.S(S_GX + i, k);
             if (c.hlx(i)) {
-                const double zl = c.S(S_ZLX + i, k), il = inv(xv - c.xl[i]);
+                const double zl = vw.S(S_ZLX + i, k), il = inv(xv - c.xl[i]);
                 sg += zl * il;
                 g -= lsq ? zl : mu * il;
             }
             if (c.hux(i)) {
-                const double zu = c.S(S_ZUX + i, k), iu = inv(c.xu[i] - xv);
+                const double zu = vw.S(S_ZUX + i, k), iu = inv(c.xu[i] - xv);
                 sg += zu * iu;
                 g += lsq ? zu : mu * iu;
             }
@@ -1002,44 +1027,44 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
                 qv[i] += Dfe * rf;
             }
 #pragma unroll
-        for (int i = 0; i < 21; ++i) c.S(S_QT + i, k) = Qs[i];
+        for (int i = 0; i < 21; ++i) vw.S(S_QT + i, k) = Qs[i];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) c.S(S_QV + i, k) = qv[i];
+        for (int i = 0; i < 6; ++i) vw.S(S_QV + i, k) = qv[i];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            double ce = c.S(S_CR + i, k), sd = 0.0;
+            double ce = vw.S(S_CR + i, k), sd = 0.0;
             if (rs) {
-                const PN t = pn_terms(lsq, c.S(S_PR + i, k), c.S(S_NR + i, k), c.S(S_ZP + i, k), c.S(S_ZN + i, k), mu, dw);
+                const PN t = pn_terms(lsq, vw.S(S_PR + i, k), vw.S(S_NR + i, k), vw.S(S_ZP + i, k), vw.S(S_ZN + i, k), mu, dw);
                 const double ip = inv(t.Dp), in_ = inv(t.Dn);
                 ce += t.gp * ip - t.gn * in_;
                 sd = sqrt(ip + in_);
             }
-            c.S(S_CE + i, k) = ce;
-            c.S(S_SD + i, k) = sd;
+            vw.S(S_CE + i, k) = ce;
+            vw.S(S_SD + i, k) = sd;
         }
         if (k < N) {
-            const double u0 = c.S(S_U, k), u1 = c.S(S_U + 1, k);
-            double R0, R1, R3, g0 = c.S(S_GU, k), g1 = c.S(S_GU + 1, k);
+            const double u0 = vw.S(S_U, k), u1 = vw.S(S_U + 1, k);
+            double R0, R1, R3, g0 = vw.S(S_GU, k), g1 = vw.S(S_GU + 1, k);
             if (lsq) {
                 R0 = 1.0; R1 = 0.0; R3 = 1.0;
-                if (c.hlu(0)) g0 -= c.S(S_ZLU, k);
-                if (c.huu(0)) g0 += c.S(S_ZUU, k);
-                if (c.hlu(1)) g1 -= c.S(S_ZLU + 1, k);
-                if (c.huu(1)) g1 += c.S(S_ZUU + 1, k);
+                if (c.hlu(0)) g0 -= vw.S(S_ZLU, k);
+                if (c.huu(0)) g0 += vw.S(S_ZUU, k);
+                if (c.hlu(1)) g1 -= vw.S(S_ZLU + 1, k);
+                if (c.huu(1)) g1 += vw.S(S_ZUU + 1, k);
             } else {
-                R0 = (rs ? sh.zeta * c.S(S_DRU, k) : 2.0 * a.R[0]) + dw;
+                R0 = (rs ? sh.zeta * vw.S(S_DRU, k) : 2.0 * a.R[0]) + dw;
                 R1 = rs ? 0.0 : a.R[1] + a.R[2];
-                R3 = (rs ? sh.zeta * c.S(S_DRU + 1, k) : 2.0 * a.R[3]) + dw;
-                if (c.hlu(0)) { const double t = inv(u0 - c.ul[0]); R0 += c.S(S_ZLU, k) * t; g0 -= mu * t; }
-                if (c.huu(0)) { const double t = inv(c.uu[0] - u0); R0 += c.S(S_ZUU, k) * t; g0 += mu * t; }
-                if (c.hlu(1)) { const double t = inv(u1 - c.ul[1]); R3 += c.S(S_ZLU + 1, k) * t; g1 -= mu * t; }
-                if (c.huu(1)) { const double t = inv(c.uu[1] - u1); R3 += c.S(S_ZUU + 1, k) * t; g1 += mu * t; }
+                R3 = (rs ? sh.zeta * vw.S(S_DRU + 1, k) : 2.0 * a.R[3]) + dw;
+                if (c.hlu(0)) { const double t = inv(u0 - c.ul[0]); R0 += vw.S(S_ZLU, k) * t; g0 -= mu * t; }
+                if (c.huu(0)) { const double t = inv(c.uu[0] - u0); R0 += vw.S(S_ZUU, k) * t; g0 += mu * t; }
+                if (c.hlu(1)) { const double t = inv(u1 - c.ul[1]); R3 += vw.S(S_ZLU + 1, k) * t; g1 -= mu * t; }
+                if (c.huu(1)) { const double t = inv(c.uu[1] - u1); R3 += vw.S(S_ZUU + 1, k) * t; g1 += mu * t; }
             }
-            c.S(S_RT, k) = R0;
-            c.S(S_RT + 1, k) = R1;
-            c.S(S_RT + 2, k) = R3;
-            c.S(S_RV, k) = g0;
-            c.S(S_RV + 1, k) = g1;
+            vw.S(S_RT, k) = R0;
+            vw.S(S_RT + 1, k) = R1;
+            vw.S(S_RT + 2, k) = R3;
+            vw.S(S_RV, k) = g0;
+            vw.S(S_RV + 1, k) = g1;
         }
     }
     const int ops[1] = {R_MAX};
@@ -1118,6 +1143,7 @@ __device__ __forceinline__ void stage_copy(const Ctx& c, double* A, Val value) {
     }
 }
 __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
+    const WsView vw = ws_view(c);
     stage_copy<LA>(c, A, [&](int f, int k) -> double {
         int g;
         if (f < 21) g = S_QT + f;
@@ -1126,7 +1152,7 @@ __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
         else if (f < 32) g = S_RV + f - 30;
         else if (f < 41) g = S_AJ + f - 32;
         else g = S_CE + f - 41;
-        return (k < c.N || (f < 27 || f >= 41)) ? (double)c.S(g, k) : 0.0;
+        return (k < c.N || (f < 27 || f >= 41)) ? (double)vw.S(g, k) : 0.0;
     });
 }
 
@@ -1175,6 +1201,7 @@ __device__ __forceinline__ double2 ldd2(const double* p) { return *reinterpret_c
 
 template <class Src>
 __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) {
+    const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt, dt2 = dt * dt;
     const bool act = lane < 36, vec = lane >= 48 && lane < 54;
@@ -1191,7 +1218,7 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
         const double q = src.QT(sij, N);
         P[8 * i + j] = q;
         if (i <= j) src.setP(sij, N, q);
-        if (keep && i <= j) c.S(S_P + sij, N) = q;
+        if (keep && i <= j) vw.S(S_P + sij, N) = q;
     }
     double pv = vec ? src.QV(r, N) : 0.0;
     if (vec) src.setPV(r, N, pv);
@@ -1252,7 +1279,7 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
         if (act) {
             P[8 * i + j] = Pk;
             if (i <= j) src.setP(sij, k, Pk);
-            if (keep && i <= j) c.S(S_P + sij, k) = Pk;
+            if (keep && i <= j) vw.S(S_P + sij, k) = Pk;
         }
         if (vec) {
             const double H0 = dt * hi.y, H1 = dt * hi.x;
@@ -1260,12 +1287,12 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
             src.setK(r, k, K0);
             src.setK(6 + r, k, K1);
             src.setPV(r, k, pnew);
-            if (keep) { c.S(S_K + r, k) = K0; c.S(S_K + 6 + r, k) = K1; }
+            if (keep) { vw.S(S_K + r, k) = K0; vw.S(S_K + 6 + r, k) = K1; }
         }
         if (lane == 0) {
             src.setKF(0, k, kf0);
             src.setKF(1, k, kf1);
-            if (c.refine) { c.S(S_GI, k) = Gi00; c.S(S_GI + 1, k) = Gi01; c.S(S_GI + 2, k) = Gi11; }
+            if (c.refine) { vw.S(S_GI, k) = Gi00; vw.S(S_GI + 1, k) = Gi01; vw.S(S_GI + 2, k) = Gi11; }
         }
         pv = pnew;
         asm volatile("" ::: "memory");
@@ -1293,6 +1320,7 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
 // broadcast on the serial chain); lanes 0..5 then write row r of the stage outputs off the chain.
 template <class Src>
 __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
+    const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
     const int r = lane < 6 ? lane : 0;
@@ -1306,8 +1334,8 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
             for (int q = 0; q < 6; ++q) t = fma(src.P(sy6(r, q), k), dx[q], t);
 #pragma unroll
             for (int q = 1; q < 6; ++q) dxr = r == q ? dx[q] : dxr;
-            c.S(S_YCP + 6 * buf + r, k) = -t;
-            c.S(S_DX + 6 * buf + r, k) = dxr;
+            vw.S(S_YCP + 6 * buf + r, k) = -t;
+            vw.S(S_DX + 6 * buf + r, k) = dxr;
         }
         if (k == N) break;
         double du0 = src.KF(0, k), du1 = src.KF(1, k);
@@ -1317,8 +1345,8 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
             du1 = fma(src.K(6 + q, k), dx[q], du1);
         }
         if (lane == 0) {
-            c.S(S_DU + 2 * buf, k) = du0;
-            c.S(S_DU + 2 * buf + 1, k) = du1;
+            vw.S(S_DU + 2 * buf, k) = du0;
+            vw.S(S_DU + 2 * buf + 1, k) = du1;
         }
         double aj[9], e[6];
 #pragma unroll
@@ -1373,6 +1401,7 @@ struct SoftG {
     __device__ double SD(int i, int k) const { return c.S(S_SD + i, k); }
 };
 __device__ __noinline__ void stage_soft_inputs(const Ctx& c, double* A) {
+    const WsView vw = ws_view(c);
     stage_copy<LAS>(c, A, [&](int f, int k) -> double {
         int g;
         if (f < 21) g = S_QT + f;
@@ -1382,7 +1411,7 @@ __device__ __noinline__ void stage_soft_inputs(const Ctx& c, double* A) {
         else if (f < 41) g = S_AJ + f - 32;
         else if (f < 47) g = S_CE + f - 41;
         else g = S_SD + f - 47;
-        return (k < c.N || f < 27 || f >= 41) ? (double)c.S(g, k) : 0.0;
+        return (k < c.N || f < 27 || f >= 41) ? (double)vw.S(g, k) : 0.0;
     });
 }
 // operands of one soft stage: the softening of stage k (S entries of the lane) and the hard step k-1
@@ -1399,6 +1428,7 @@ __device__ __forceinline__ void soft_ops(const Src& src, int k, int i, int j, in
 
 template <class Src>
 __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& src) {
+    const WsView vw = ws_view(c);
     const GSrc out{c};
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt, dt2 = dt * dt;
@@ -1444,7 +1474,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         // Y = S M^-1 S from the upper entry (symmetric by construction)
         const double y = i <= j ? cur.si * mv * cur.sj : cur.sj * mji * cur.si;
         Yt[tij] = y;
-        if (act && i <= j) c.S(S_Y + sij, k) = y;
+        if (act && i <= j) vw.S(S_Y + sij, k) = y;
         lds_order();
         {
             double t = 0.0;
@@ -1525,7 +1555,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         if (lane == 0) {
             out.setKF(0, kk, kf0);
             out.setKF(1, kk, kf1);
-            if (c.refine) { c.S(S_GI, kk) = Gi00; c.S(S_GI + 1, kk) = Gi01; c.S(S_GI + 2, kk) = Gi11; }
+            if (c.refine) { vw.S(S_GI, kk) = Gi00; vw.S(S_GI + 1, kk) = Gi01; vw.S(S_GI + 2, kk) = Gi11; }
         }
         if (act && i <= j) out.setP(sij, kk, Pk);
         lds_order();
@@ -1574,6 +1604,7 @@ struct SoftFG {
     __device__ double CR(int i, int k) const { return c.S(S_CE + i, k); }
 };
 __device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A, bool soft = true) {
+    const WsView vw = ws_view(c);
     stage_copy<LFS>(c, A, [&](int f, int k) -> double {
         if (!soft && f >= 41 && f < 62) return 0.0;  // hard rows: Y unused
         int g;
@@ -1584,11 +1615,12 @@ __device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A, bool so
         else if (f < 62) g = S_Y + f - 41;
         else if (f < 71) g = S_AJ + f - 62;
         else g = S_CE + f - 71;
-        return (k < c.N || f < 27 || (f >= 41 && f < 62) || f >= 71) ? (double)c.S(g, k) : 0.0;
+        return (k < c.N || f < 27 || (f >= 41 && f < 62) || f >= 71) ? (double)vw.S(g, k) : 0.0;
     });
 }
 template <class Src>
 __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf) {
+    const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
     const int r = lane < 6 ? lane : 0;
@@ -1617,8 +1649,8 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf)
             for (int q = 0; q < 6; ++q) t = fma(src.P(sy6(r, q), k), dx[q], t);
 #pragma unroll
             for (int q = 1; q < 6; ++q) dxr = r == q ? dx[q] : dxr;
-            c.S(S_YCP + 6 * buf + r, k) = -t;
-            c.S(S_DX + 6 * buf + r, k) = dxr;
+            vw.S(S_YCP + 6 * buf + r, k) = -t;
+            vw.S(S_DX + 6 * buf + r, k) = dxr;
         }
         if (k == N) break;
         double du0 = src.KF(0, k), du1 = src.KF(1, k);
@@ -1628,8 +1660,8 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf)
             du1 = fma(src.K(6 + q, k), dx[q], du1);
         }
         if (lane == 0) {
-            c.S(S_DU + 2 * buf, k) = du0;
-            c.S(S_DU + 2 * buf + 1, k) = du1;
+            vw.S(S_DU + 2 * buf, k) = du0;
+            vw.S(S_DU + 2 * buf + 1, k) = du1;
         }
         double aj[9], e[6];
 #pragma unroll
@@ -1670,6 +1702,7 @@ __device__ __forceinline__ void pn_step(double p, double n, double zp, double zn
 //      [4] max |y+| (least-squares multiplier test)
 __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf,
                                            double (&out)[5]) {
+    const WsView vw = ws_view(c);
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0 && !sh.lsq, lsq = sh.lsq != 0;
     double ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0, ymax = 0.0;
@@ -1677,52 +1710,52 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
         double x[6], dx[6];
         load_x(c, k, x);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) dx[i] = c.S(S_DX + 6 * buf + i, k);
+        for (int i = 0; i < 6; ++i) dx[i] = vw.S(S_DX + 6 * buf + i, k);
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double xv = x[i], d = dx[i];
-            double g = c.S(S_GX + i, k);
+            double g = vw.S(S_GX + i, k);
             rel = fmax(rel, fabs(d) / (1.0 + fabs(xv)));
             if (c.hlx(i)) {
-                const double sl = xv - c.xl[i], z = c.S(S_ZLX + i, k);
+                const double sl = xv - c.xl[i], z = vw.S(S_ZLX + i, k);
                 g -= mu / sl;
                 ftb_lo(xv, c.xl[i], d, tau, ap);
                 const double dz = mu / sl - z - z / sl * d;
                 if (dz < 0.0) az = fmin(az, -tau * z / dz);
             }
             if (c.hux(i)) {
-                const double sl = c.xu[i] - xv, z = c.S(S_ZUX + i, k);
+                const double sl = c.xu[i] - xv, z = vw.S(S_ZUX + i, k);
                 g += mu / sl;
                 ftb_hi(xv, c.xu[i], d, tau, ap);
                 const double dz = mu / sl - z + z / sl * d;
                 if (dz < 0.0) az = fmin(az, -tau * z / dz);
             }
             Dm += g * d;
-            const double yp = c.S(S_YCP + 6 * buf + i, k);
+            const double yp = vw.S(S_YCP + 6 * buf + i, k);
             ymax = fmax(ymax, fabs(yp));
             if (rs) {
                 double dp, dn;
-                pn_step(c.S(S_PR + i, k), c.S(S_NR + i, k), c.S(S_ZP + i, k), c.S(S_ZN + i, k), yp, mu, dw, tau, dp, dn,
+                pn_step(vw.S(S_PR + i, k), vw.S(S_NR + i, k), vw.S(S_ZP + i, k), vw.S(S_ZN + i, k), yp, mu, dw, tau, dp, dn,
                         ap, az, Dm, rel);
-                c.S(S_DP + 6 * buf + i, k) = dp;
-                c.S(S_DN + 6 * buf + i, k) = dn;
+                vw.S(S_DP + 6 * buf + i, k) = dp;
+                vw.S(S_DN + 6 * buf + i, k) = dn;
             }
         }
         if (k < N)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const double uv = c.S(S_U + i, k), d = c.S(S_DU + 2 * buf + i, k);
-                double g = c.S(S_GU + i, k);
+                const double uv = vw.S(S_U + i, k), d = vw.S(S_DU + 2 * buf + i, k);
+                double g = vw.S(S_GU + i, k);
                 rel = fmax(rel, fabs(d) / (1.0 + fabs(uv)));
                 if (c.hlu(i)) {
-                    const double sl = uv - c.ul[i], z = c.S(S_ZLU + i, k);
+                    const double sl = uv - c.ul[i], z = vw.S(S_ZLU + i, k);
                     g -= mu / sl;
                     ftb_lo(uv, c.ul[i], d, tau, ap);
                     const double dz = mu / sl - z - z / sl * d;
                     if (dz < 0.0) az = fmin(az, -tau * z / dz);
                 }
                 if (c.huu(i)) {
-                    const double sl = c.uu[i] - uv, z = c.S(S_ZUU + i, k);
+                    const double sl = c.uu[i] - uv, z = vw.S(S_ZUU + i, k);
                     g += mu / sl;
                     ftb_hi(uv, c.uu[i], d, tau, ap);
                     const double dz = mu / sl - z + z / sl * d;
@@ -1742,7 +1775,7 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const double wv = in.w[e], z = in.zw[e], sl = wv + RELAX, d = dwv[e];
-                c.B(B_DW + 8 * buf + e, j, k) = d;
+                vw.B(B_DW + 8 * buf + e, j, k) = d;
                 rel = fmax(rel, fabs(d) / (1.0 + fabs(wv)));
                 Dm += fw[e] * d;
                 ftb_lo(wv, -RELAX, d, tau, ap);
@@ -1754,8 +1787,8 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 const double s = in.s[r], vl = in.vl[r], vu = in.vu[r];
                 const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
                 const double ds = (yp[r] - gs) / bk.D[r];
-                c.B(B_YP + 4 * buf + r, j, k) = yp[r];
-                c.B(B_DS + 4 * buf + r, j, k) = ds;
+                vw.B(B_YP + 4 * buf + r, j, k) = yp[r];
+                vw.B(B_DS + 4 * buf + r, j, k) = ds;
                 ymax = fmax(ymax, fabs(yp[r]));
                 rel = fmax(rel, fabs(ds) / (1.0 + fabs(s)));
                 Dm += gs * ds;
@@ -1772,8 +1805,8 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
                 if (rs) {
                     double dp, dn;
                     pn_step(in.pr[r], in.nr[r], in.zp[r], in.zn[r], yp[r], mu, dw, tau, dp, dn, ap, az, Dm, rel);
-                    c.B(B_DP + 4 * buf + r, j, k) = dp;
-                    c.B(B_DN + 4 * buf + r, j, k) = dn;
+                    vw.B(B_DP + 4 * buf + r, j, k) = dp;
+                    vw.B(B_DN + 4 * buf + r, j, k) = dn;
                 }
             }
         }
@@ -1974,22 +2007,23 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
 // waits would include those stores, one in-order vmcnt queue -- so a block's results are stored after the
 // next block's loads)
 __device__ __noinline__ void phase_soc_resid(const Ctx& c, LShared& sh, double a_soc) {
+    const WsView vw = ws_view(c);
     for (int k = (int)threadIdx.x; k <= c.N; k += T) {
         double cr[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) cr[i] = a_soc * c.S(S_CR + i, k) + c.S(S_CT + i, k);
+        for (int i = 0; i < 6; ++i) cr[i] = a_soc * vw.S(S_CR + i, k) + vw.S(S_CT + i, k);
         double dr[4], nx[4];
         auto blk = [&](int j, double* v) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = a_soc * c.B(B_DR + r, j, k) + c.B(B_DT + r, j, k);
+            for (int r = 0; r < 4; ++r) v[r] = a_soc * vw.B(B_DR + r, j, k) + vw.B(B_DT + r, j, k);
         };
         if (c.nbk > 0) blk(0, dr);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) c.S(S_CR + i, k) = cr[i];
+        for (int i = 0; i < 6; ++i) vw.S(S_CR + i, k) = cr[i];
         for (int j = 0; j < c.nbk; ++j) {
             if (j + 1 < c.nbk) blk(j + 1, nx);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) { c.B(B_DR + r, j, k) = dr[r]; dr[r] = nx[r]; }
+            for (int r = 0; r < 4; ++r) { vw.B(B_DR + r, j, k) = dr[r]; dr[r] = nx[r]; }
         }
         if (k == c.N && c.plan())
 #pragma unroll
@@ -2726,6 +2760,7 @@ __device__ __forceinline__ double rowbc(double v) {
 #endif
 template <class Src>
 __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft) {
+    const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
 #if OBCA_VEC_DPP
@@ -2733,7 +2768,7 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
     // broadcasts of p' -> np, with only the lane's own row of PY, K, QV and W read from LDS
     const int q = lane < 6 ? lane : 0;
     double pq = src.QV(q, N);
-    if (lane < 6) c.S(S_PV + q, N) = pq;
+    if (lane < 6) vw.S(S_PV + q, N) = pq;
     for (int k = N; k >= 1; --k) {
         const int km = k - 1;
         const double sv = pq - src.W(q, k);
@@ -2762,8 +2797,8 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
         const double t2 = fma(dj[0], pp0, dj[2] * pp1), t4 = fma(dj[4], pp2, dj[7] * pp3);
         const double t5 = fma(dj[1], pp0, fma(dj[3], pp1, fma(dj[5], pp2, dj[8] * pp3)));
         np = q == 2 ? np + t2 : q == 3 ? fma(dj[6], pp3, np) : q == 4 ? np + t4 : q == 5 ? np + t5 : np;
-        if (lane < 6) c.S(S_PV + q, km) = np;
-        if (lane == 0) { c.S(S_KF, km) = kf0; c.S(S_KF + 1, km) = kf1; }
+        if (lane < 6) vw.S(S_PV + q, km) = np;
+        if (lane == 0) { vw.S(S_KF, km) = kf0; vw.S(S_KF + 1, km) = kf1; }
         pq = np;
     }
 #else
@@ -2777,7 +2812,7 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
     double p[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) p[q] = src.QV(q, N);
-    if (lane < 6) c.S(S_PV + r, N) = pick(p);
+    if (lane < 6) vw.S(S_PV + r, N) = pick(p);
     for (int k = N; k >= 1; --k) {
         const int km = k - 1;
         double sv[6], pp[6];
@@ -2811,8 +2846,8 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
         np[3] += dj[6] * pp[3];
         np[4] += fma(dj[4], pp[2], dj[7] * pp[3]);
         np[5] += fma(dj[1], pp[0], fma(dj[3], pp[1], fma(dj[5], pp[2], dj[8] * pp[3])));
-        if (lane < 6) c.S(S_PV + r, km) = pick(np);
-        if (lane == 0) { c.S(S_KF, km) = kf0; c.S(S_KF + 1, km) = kf1; }
+        if (lane < 6) vw.S(S_PV + r, km) = pick(np);
+        if (lane == 0) { vw.S(S_KF, km) = kf0; vw.S(S_KF + 1, km) = kf1; }
 #pragma unroll
         for (int q = 0; q < 6; ++q) p[q] = np[q];
     }
@@ -2834,6 +2869,7 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft
 enum { NR_STEP = 0, NR_MAIN = 1, NR_CORR = 2 };
 __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, bool prep,
                                         int mode, double (&out)[7]) {
+    const WsView vw = ws_view(c);
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0;
@@ -2848,16 +2884,16 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         double u[2] = {0.0, 0.0}, du[2] = {0.0, 0.0};
         load_x(c, k, x);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) { dx[i] = c.S(S_DX + 6 * buf + i, k); yp[i] = c.S(S_YCP + 6 * buf + i, k); }
+        for (int i = 0; i < 6; ++i) { dx[i] = vw.S(S_DX + 6 * buf + i, k); yp[i] = vw.S(S_YCP + 6 * buf + i, k); }
         if (st) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) ypn[i] = c.S(S_YCP + 6 * buf + i, k + 1);
+            for (int i = 0; i < 6; ++i) ypn[i] = vw.S(S_YCP + 6 * buf + i, k + 1);
 #pragma unroll
-            for (int i = 0; i < 9; ++i) dj[i] = c.S(S_AJ + i, k);
+            for (int i = 0; i < 9; ++i) dj[i] = vw.S(S_AJ + i, k);
 #pragma unroll
-            for (int i = 0; i < 7; ++i) wd[i] = c.S(S_WD + i, k);
+            for (int i = 0; i < 7; ++i) wd[i] = vw.S(S_WD + i, k);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) { u[i] = c.S(S_U + i, k); du[i] = c.S(S_DU + 2 * buf + i, k); }
+            for (int i = 0; i < 2; ++i) { u[i] = vw.S(S_U + i, k); du[i] = vw.S(S_DU + 2 * buf + i, k); }
         }
         // ---- x rows (without the block terms, added below) ----
         double rx[6];
@@ -2872,17 +2908,17 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double xv = x[i], d = dx[i];
-            double g = c.S(S_GX + i, k), sg = dw + (rs ? zeta * c.S(S_DRX + i, k) : 0.0);
+            double g = vw.S(S_GX + i, k), sg = dw + (rs ? zeta * vw.S(S_DRX + i, k) : 0.0);
             rel = fmax(rel, fabs(d) * inv(1.0 + fabs(xv)));
             if (c.hlx(i)) {
-                const double is = inv(xv - c.xl[i]), z = c.S(S_ZLX + i, k);
+                const double is = inv(xv - c.xl[i]), z = vw.S(S_ZLX + i, k);
                 g -= mu * is;
                 sg += z * is;
                 ftb_lo(xv, c.xl[i], d, tau, ap);
                 dual(z, mu * is - z - z * is * d);
             }
             if (c.hux(i)) {
-                const double is = inv(c.xu[i] - xv), z = c.S(S_ZUX + i, k);
+                const double is = inv(c.xu[i] - xv), z = vw.S(S_ZUX + i, k);
                 g += mu * is;
                 sg += z * is;
                 ftb_hi(xv, c.xu[i], d, tau, ap);
@@ -2906,17 +2942,17 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const double uv = u[i], d = du[i];
-                double g = c.S(S_GU + i, k), sg = dw + (rs ? zeta * c.S(S_DRU + i, k) : 0.0);
+                double g = vw.S(S_GU + i, k), sg = dw + (rs ? zeta * vw.S(S_DRU + i, k) : 0.0);
                 rel = fmax(rel, fabs(d) * inv(1.0 + fabs(uv)));
                 if (c.hlu(i)) {
-                    const double is = inv(uv - c.ul[i]), z = c.S(S_ZLU + i, k);
+                    const double is = inv(uv - c.ul[i]), z = vw.S(S_ZLU + i, k);
                     g -= mu * is;
                     sg += z * is;
                     ftb_lo(uv, c.ul[i], d, tau, ap);
                     dual(z, mu * is - z - z * is * d);
                 }
                 if (c.huu(i)) {
-                    const double is = inv(c.uu[i] - uv), z = c.S(S_ZUU + i, k);
+                    const double is = inv(c.uu[i] - uv), z = vw.S(S_ZUU + i, k);
                     g += mu * is;
                     sg += z * is;
                     ftb_hi(uv, c.uu[i], d, tau, ap);
@@ -2931,14 +2967,14 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         // ---- dynamics rows of stage k: c_k + dx_k - A_{k-1} dx_{k-1} - B du_{k-1} (- dp + dn) ----
         double rc[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) rc[i] = Bc(c.S(S_CR + i, k)) + dx[i];
+        for (int i = 0; i < 6; ++i) rc[i] = Bc(vw.S(S_CR + i, k)) + dx[i];
         if (k > 0) {
             double dxp[6], ajp[9];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) dxp[i] = c.S(S_DX + 6 * buf + i, k - 1);
+            for (int i = 0; i < 6; ++i) dxp[i] = vw.S(S_DX + 6 * buf + i, k - 1);
 #pragma unroll
-            for (int i = 0; i < 9; ++i) ajp[i] = c.S(S_AJ + i, k - 1);
-            const double dup0 = c.S(S_DU + 2 * buf, k - 1), dup1 = c.S(S_DU + 2 * buf + 1, k - 1);
+            for (int i = 0; i < 9; ++i) ajp[i] = vw.S(S_AJ + i, k - 1);
+            const double dup0 = vw.S(S_DU + 2 * buf, k - 1), dup1 = vw.S(S_DU + 2 * buf + 1, k - 1);
             rc[0] -= dxp[0] + fma(ajp[0], dxp[2], ajp[1] * dxp[5]);
             rc[1] -= dxp[1] + fma(ajp[2], dxp[2], ajp[3] * dxp[5]);
             rc[2] -= dxp[2] + fma(ajp[4], dxp[4], ajp[5] * dxp[5]);
@@ -2950,18 +2986,18 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         if (rs)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
+                const double p = vw.S(S_PR + i, k), n = vw.S(S_NR + i, k), zp = vw.S(S_ZP + i, k), zn = vw.S(S_ZN + i, k);
                 const double ip = inv(p), in_ = inv(n);
                 const double Dp = zp * ip + dw, Dn = zn * in_ + dw, gp = RHO - mu * ip, gn = RHO - mu * in_;
                 double dp, dn;
                 if (mode == NR_MAIN) {  // the pair's step from the new multiplier (phase_recover's pn_step)
                     dp = (yp[i] - gp) / Dp;
                     dn = (-yp[i] - gn) / Dn;
-                    c.S(S_DP + 6 * buf + i, k) = dp;
-                    c.S(S_DN + 6 * buf + i, k) = dn;
+                    vw.S(S_DP + 6 * buf + i, k) = dp;
+                    vw.S(S_DN + 6 * buf + i, k) = dn;
                 } else {
-                    dp = c.S(S_DP + 6 * buf + i, k);
-                    dn = c.S(S_DN + 6 * buf + i, k);
+                    dp = vw.S(S_DP + 6 * buf + i, k);
+                    dn = vw.S(S_DN + 6 * buf + i, k);
                 }
                 rc[i] += -dp + dn;
                 rpc[i] = R(Bc(gp) + Dp * dp - yp[i]);
@@ -2996,38 +3032,38 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                     block_refactor<false>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
                     if (mode == NR_CORR) {  // the correction's right-hand side, as the previous prep pass left it
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) fw[e] = c.B(B_FR + FR_FW + e, j, k);
+                        for (int e = 0; e < 8; ++e) fw[e] = vw.B(B_FR + FR_FW + e, j, k);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) { zf[4 + e] = c.B(B_FR + FR_ZFL + e, j, k); t4[e] = c.B(B_FR + FR_T + e, j, k); }
+                        for (int e = 0; e < 4; ++e) { zf[4 + e] = vw.B(B_FR + FR_ZFL + e, j, k); t4[e] = vw.B(B_FR + FR_T + e, j, k); }
                     }
                 }
                 if (mode != NR_STEP) {
                     // ---- the block's part of the step (NR_MAIN) or of the correction (NR_CORR) ----
                     double ypr[4], dwr[8], dxr[6];
 #pragma unroll
-                    for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)c.S(S_DX + 12 + i, k);
+                    for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)vw.S(S_DX + 12 + i, k);
                     blk_recover(bk, fw, zf, t4, dxr, ypr, dwr);
                     const bool add = mode == NR_CORR;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        dwv[e] = add ? (double)c.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
-                        c.B(B_DW + 8 * buf + e, j, k) = dwv[e];
+                        dwv[e] = add ? (double)vw.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
+                        vw.B(B_DW + 8 * buf + e, j, k) = dwv[e];
                     }
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const double gs = add ? (double)c.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
+                        const double gs = add ? (double)vw.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
                         const double dsr = (ypr[r] - gs) / bk.D[r];
-                        ydp[r] = add ? (double)c.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
-                        ds[r] = add ? (double)c.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
-                        c.B(B_YP + 4 * buf + r, j, k) = ydp[r];
-                        c.B(B_DS + 4 * buf + r, j, k) = ds[r];
+                        ydp[r] = add ? (double)vw.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
+                        ds[r] = add ? (double)vw.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
+                        vw.B(B_YP + 4 * buf + r, j, k) = ydp[r];
+                        vw.B(B_DS + 4 * buf + r, j, k) = ds[r];
                         if (rs) {
                             const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
-                            const double gp = add ? (double)c.B(B_OP + r, j, k) : RHO - mu / p;
-                            const double gn = add ? (double)c.B(B_ON + r, j, k) : RHO - mu / n;
+                            const double gp = add ? (double)vw.B(B_OP + r, j, k) : RHO - mu / p;
+                            const double gn = add ? (double)vw.B(B_ON + r, j, k) : RHO - mu / n;
                             const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
-                            c.B(B_DP + 4 * buf + r, j, k) = add ? (double)c.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
-                            c.B(B_DN + 4 * buf + r, j, k) = add ? (double)c.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
+                            vw.B(B_DP + 4 * buf + r, j, k) = add ? (double)vw.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
+                            vw.B(B_DN + 4 * buf + r, j, k) = add ? (double)vw.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
                         }
                     }
                 }
@@ -3036,9 +3072,9 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
             }
             if (mode == NR_STEP) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e) dwv[e] = c.B(B_DW + 8 * buf + e, j, k);
+                for (int e = 0; e < 8; ++e) dwv[e] = vw.B(B_DW + 8 * buf + e, j, k);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) { ds[r] = c.B(B_DS + 4 * buf + r, j, k); ydp[r] = c.B(B_YP + 4 * buf + r, j, k); }
+                for (int r = 0; r < 4; ++r) { ds[r] = vw.B(B_DS + 4 * buf + r, j, k); ydp[r] = vw.B(B_YP + 4 * buf + r, j, k); }
             }
             // x rows: W_xx dx + W_x lam dw_lam + Jx' y+
             rx[2] += bk.hxx22 * dx[2] + bk.hxx23 * dx[3];
@@ -3094,7 +3130,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                 for (int e = 0; e < 4; ++e) t += jwm(bk, r, e) * dwv[e] + jwl(bk, r, e) * dwv[4 + e];
                 if (rs) {
                     const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
-                    const double dp = c.B(B_DP + 4 * buf + r, j, k), dn = c.B(B_DN + 4 * buf + r, j, k);
+                    const double dp = vw.B(B_DP + 4 * buf + r, j, k), dn = vw.B(B_DN + 4 * buf + r, j, k);
                     t += -dp + dn;
                     const double ip = inv(p), in_ = inv(n);
                     Dpv[r] = zp * ip + dw;
@@ -3124,15 +3160,15 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
 #pragma unroll
                 for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / bk.D[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
                 blk_rhs(bk, rw, rdc, zf, t4, q4);
-                auto stf = [&](int f, double v) { c.B(B_FR + f, j, k) = v; };
+                auto stf = [&](int f, double v) { vw.B(B_FR + f, j, k) = v; };
 #pragma unroll
                 for (int e = 0; e < 8; ++e) stf(FR_FW + e, rw[e]);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) { stf(FR_ZFL + e, zf[4 + e]); stf(FR_T + e, t4[e]); }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    c.B(B_OS + r, j, k) = rsl[r];
-                    if (rs) { c.B(B_OP + r, j, k) = rpv[r]; c.B(B_ON + r, j, k) = rnv[r]; }
+                    vw.B(B_OS + r, j, k) = rsl[r];
+                    if (rs) { vw.B(B_OP + r, j, k) = rpv[r]; vw.B(B_ON + r, j, k) = rnv[r]; }
                 }
             }
         }
@@ -3192,11 +3228,11 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         if (prep) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                c.S(S_QV + i, k) = rx[i] + (i < 4 ? q4[i] : 0.0) + qf[i];
-                c.S(S_CE + i, k) = rc[i] + (rs ? gpnc[i] : 0.0);
-                if (rs) { c.S(S_OP + i, k) = rpc[i]; c.S(S_ON + i, k) = rnc[i]; }
+                vw.S(S_QV + i, k) = rx[i] + (i < 4 ? q4[i] : 0.0) + qf[i];
+                vw.S(S_CE + i, k) = rc[i] + (rs ? gpnc[i] : 0.0);
+                if (rs) { vw.S(S_OP + i, k) = rpc[i]; vw.S(S_ON + i, k) = rnc[i]; }
             }
-            if (st) { c.S(S_RV, k) = ru[0]; c.S(S_RV + 1, k) = ru[1]; }
+            if (st) { vw.S(S_RV, k) = ru[0]; vw.S(S_RV + 1, k) = ru[1]; }
         }
     }
     out[0] = rmax; out[1] = bmax; out[2] = snorm; out[3] = ap; out[4] = az; out[5] = Dm; out[6] = rel;
@@ -3208,34 +3244,35 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
 // added into the step in buffer buf; the blocks' parts follow in phase_nres (NR_CORR), which reads the summed
 // stage fields of neighbouring stages (hence a pass of its own) ----
 __device__ __noinline__ void phase_stage_add(const Ctx& c, LShared& sh, double dw, int buf) {
+    const WsView vw = ws_view(c);
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double dxc[6], ypc[6], sdx[6], syp[6], sdp[6] = {0, 0, 0, 0, 0, 0}, sdn[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            dxc[i] = c.S(S_DX + 12 + i, k); ypc[i] = c.S(S_YCP + 12 + i, k);
-            sdx[i] = c.S(S_DX + 6 * buf + i, k); syp[i] = c.S(S_YCP + 6 * buf + i, k);
+            dxc[i] = vw.S(S_DX + 12 + i, k); ypc[i] = vw.S(S_YCP + 12 + i, k);
+            sdx[i] = vw.S(S_DX + 6 * buf + i, k); syp[i] = vw.S(S_YCP + 6 * buf + i, k);
         }
         if (rs)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const double p = c.S(S_PR + i, k), n = c.S(S_NR + i, k), zp = c.S(S_ZP + i, k), zn = c.S(S_ZN + i, k);
-                sdp[i] = c.S(S_DP + 6 * buf + i, k) + (ypc[i] - c.S(S_OP + i, k)) / (zp / p + dw);
-                sdn[i] = c.S(S_DN + 6 * buf + i, k) + (-ypc[i] - c.S(S_ON + i, k)) / (zn / n + dw);
+                const double p = vw.S(S_PR + i, k), n = vw.S(S_NR + i, k), zp = vw.S(S_ZP + i, k), zn = vw.S(S_ZN + i, k);
+                sdp[i] = vw.S(S_DP + 6 * buf + i, k) + (ypc[i] - vw.S(S_OP + i, k)) / (zp / p + dw);
+                sdn[i] = vw.S(S_DN + 6 * buf + i, k) + (-ypc[i] - vw.S(S_ON + i, k)) / (zn / n + dw);
             }
         double du0 = 0.0, du1 = 0.0;
         if (k < N) {
-            du0 = c.S(S_DU + 2 * buf, k) + c.S(S_DU + 4, k);
-            du1 = c.S(S_DU + 2 * buf + 1, k) + c.S(S_DU + 5, k);
+            du0 = vw.S(S_DU + 2 * buf, k) + vw.S(S_DU + 4, k);
+            du1 = vw.S(S_DU + 2 * buf + 1, k) + vw.S(S_DU + 5, k);
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            c.S(S_DX + 6 * buf + i, k) = sdx[i] + dxc[i];
-            c.S(S_YCP + 6 * buf + i, k) = syp[i] + ypc[i];
-            if (rs) { c.S(S_DP + 6 * buf + i, k) = sdp[i]; c.S(S_DN + 6 * buf + i, k) = sdn[i]; }
+            vw.S(S_DX + 6 * buf + i, k) = sdx[i] + dxc[i];
+            vw.S(S_YCP + 6 * buf + i, k) = syp[i] + ypc[i];
+            if (rs) { vw.S(S_DP + 6 * buf + i, k) = sdp[i]; vw.S(S_DN + 6 * buf + i, k) = sdn[i]; }
         }
-        if (k < N) { c.S(S_DU + 2 * buf, k) = du0; c.S(S_DU + 2 * buf + 1, k) = du1; }
+        if (k < N) { vw.S(S_DU + 2 * buf, k) = du0; vw.S(S_DU + 2 * buf + 1, k) = du1; }
         if (k == N && plan)
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
@@ -3340,20 +3377,21 @@ __device__ __noinline__ void phase_snapshot(const Ctx& c, LShared& sh, bool save
 
 // last acceptable iterate (IPOPT's stored acceptable point): store (x, u, w) or restore it
 __device__ __noinline__ void phase_acc(const Ctx& c, bool restore) {
+    const WsView vw = ws_view(c);
     for (int k = (int)threadIdx.x; k <= c.N; k += T) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            if (restore) c.S(S_X + i, k) = c.S(S_XACC + i, k); else c.S(S_XACC + i, k) = c.S(S_X + i, k);
+            if (restore) vw.S(S_X + i, k) = vw.S(S_XACC + i, k); else vw.S(S_XACC + i, k) = vw.S(S_X + i, k);
         }
         if (k < c.N)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                if (restore) c.S(S_U + i, k) = c.S(S_UACC + i, k); else c.S(S_UACC + i, k) = c.S(S_U + i, k);
+                if (restore) vw.S(S_U + i, k) = vw.S(S_UACC + i, k); else vw.S(S_UACC + i, k) = vw.S(S_U + i, k);
             }
         for (int j = 0; j < c.nbk; ++j)
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-                if (restore) c.B(B_W + e, j, k) = c.B(B_WACC + e, j, k); else c.B(B_WACC + e, j, k) = c.B(B_W + e, j, k);
+                if (restore) vw.B(B_W + e, j, k) = vw.B(B_WACC + e, j, k); else vw.B(B_WACC + e, j, k) = vw.B(B_W + e, j, k);
             }
     }
 }
@@ -3574,6 +3612,7 @@ __device__ __noinline__ void phase_leave_resto(const Ctx& c, LShared& sh, double
 // least-squares constraint multipliers of the current NLP (IPOPT constr_mult_init_max = 1000):
 // [[I, J'], [J, 0]] [d; y] = [-(grad f - z); 0] with unit slack / elastic Hessians; kept when max |y| <= 1000
 __device__ __noinline__ void ls_multipliers(const Ctx& c, LShared& sh) {
+    const WsView vw = ws_view(c);
     if (threadIdx.x == 0) sh.lsq = 1;
     __syncthreads();
     double red[13];
@@ -3586,10 +3625,10 @@ __device__ __noinline__ void ls_multipliers(const Ctx& c, LShared& sh) {
         if (isfinite(rec[4]) && rec[4] <= CONSTR_MULT_INIT_MAX) {
             for (int k = (int)threadIdx.x; k <= c.N; k += T) {
 #pragma unroll
-                for (int i = 0; i < 6; ++i) c.S(S_YC + i, k) = c.S(S_YCP + i, k);
+                for (int i = 0; i < 6; ++i) vw.S(S_YC + i, k) = vw.S(S_YCP + i, k);
                 for (int j = 0; j < c.nbk; ++j)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) c.B(B_YD + r, j, k) = c.B(B_YP + r, j, k);
+                    for (int r = 0; r < 4; ++r) vw.B(B_YD + r, j, k) = vw.B(B_YP + r, j, k);
                 if (k == c.N && c.plan())
 #pragma unroll
                     for (int i = 0; i < 6; ++i) sh.ydf[i] = sh.ydpf[0][i];
