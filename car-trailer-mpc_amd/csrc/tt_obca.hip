@@ -211,6 +211,20 @@ __device__ __forceinline__ double frsqrt(double x) {
     return y * fma(-hx * y, y, 1.5);
 }
 
+// row_newbcast:l (gfx90a+ DPP on a 64-bit move): every lane of a 16-lane row receives lane l of that row
+template <int L_>
+__device__ __forceinline__ double rowbc(double v) {
+    const long long b = __double_as_longlong(v);
+    return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + L_, 0xF, 0xF, false));
+}
+
+// A/B switch: riccati_vec / forward_soft with lane q owning component q of the vector and the other components
+// broadcast by DPP (1), or every lane carrying the whole vector and reading every operand (0).  Same operations in
+// the same order either way (bitwise identical).
+#ifndef OBCA_VEC_DPP
+#define OBCA_VEC_DPP 1
+#endif
+
 // sum of logs as log(prod of mantissas) + (sum of exponents) ln 2
 struct LogSum {
     double m = 1.0;
@@ -401,7 +415,11 @@ typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: 
 // per-thread LDS slab of the block phases: the 48 doubles of Yl, Zl, G (field stride T, conflict-free).  Kept in
 // registers they were what the block elimination spilled to scratch, and every scratch reload waited behind
 // the factor-record stores (one in-order vmcnt); ds_ reads wait on lgkmcnt only.
-constexpr int kSlab = 48;
+// A/B switch: W_{x lam} of the block (16 doubles) in the slab too (1) or in registers (0)
+#ifndef OBCA_HXL_SLAB
+#define OBCA_HXL_SLAB 0
+#endif
+constexpr int kSlab = OBCA_HXL_SLAB ? 64 : 48;
 struct Blk {
     lds_double* m;                   // this thread's slab (Yl 0-15 | Zl 16-31 | G 32-47)
     __device__ __forceinline__ lds_double& Yl(int a, int r) const { return m[(a * 4 + r) * T]; }  // L^-1 Jw_lam'  [a][r]
@@ -413,9 +431,13 @@ struct Blk {
     double jw0[8], ca, sa, an, cn;   // Jw row 0 + the rotation/normal data of rows 1..3
     double hl, hw;
     double hxx22, hxx23, hxx33;
+#if OBCA_HXL_SLAB
+    __device__ __forceinline__ lds_double& H(int q, int a) const { return m[(48 + q * 4 + a) * T]; }  // W_{x lam} [q][a]
+#else
     double hxl[4][4];                // W_{x lam}: rows X,Y,theta,psi
     __device__ __forceinline__ double& H(int q, int a) { return hxl[q][a]; }
     __device__ __forceinline__ double H(int q, int a) const { return hxl[q][a]; }
+#endif
     double haa, hac, hcc;            // the lam-lam Hessian y4 T'H4T (LL before the elimination), see hll
     // elimination
     double idm[4];                   // 1 / (Sigma_mu + dw) (mu block is diagonal)
@@ -1623,6 +1645,62 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf)
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
+#if OBCA_VEC_DPP
+    // lanes 0..5 own dx[q] (q = lane); the 6-vectors the rows need (dx, P dx + p) arrive by DPP row_newbcast, so each
+    // lane reads only its own rows of P and Y.  Same operations in the same order as the redundant form (bitwise).
+    const int q = lane < 6 ? lane : 0;
+    double dq = -src.CR(q, 0);
+    for (int k = 0;; ++k) {
+        double d[6];
+        d[0] = rowbc<0>(dq); d[1] = rowbc<1>(dq); d[2] = rowbc<2>(dq);
+        d[3] = rowbc<3>(dq); d[4] = rowbc<4>(dq); d[5] = rowbc<5>(dq);
+        double bq = src.PV(q, k);
+#pragma unroll
+        for (int l = 0; l < 6; ++l) bq = fma(src.P(sy6(q, l), k), d[l], bq);
+        double bv[6];
+        bv[0] = rowbc<0>(bq); bv[1] = rowbc<1>(bq); bv[2] = rowbc<2>(bq);
+        bv[3] = rowbc<3>(bq); bv[4] = rowbc<4>(bq); bv[5] = rowbc<5>(bq);
+        {
+            double t = 0.0;
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(src.Y(sy6(q, l), k), bv[l], t);
+            dq -= t;
+        }
+        d[0] = rowbc<0>(dq); d[1] = rowbc<1>(dq); d[2] = rowbc<2>(dq);
+        d[3] = rowbc<3>(dq); d[4] = rowbc<4>(dq); d[5] = rowbc<5>(dq);
+        {
+            double t = src.PV(q, k);
+#pragma unroll
+            for (int l = 0; l < 6; ++l) t = fma(src.P(sy6(q, l), k), d[l], t);
+            if (lane < 6) {
+                vw.S(S_YCP + 6 * buf + q, k) = -t;
+                vw.S(S_DX + 6 * buf + q, k) = dq;
+            }
+        }
+        if (k == N) break;
+        double du0 = src.KF(0, k), du1 = src.KF(1, k);
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {
+            du0 = fma(src.K(l, k), d[l], du0);
+            du1 = fma(src.K(6 + l, k), d[l], du1);
+        }
+        if (lane == 0) {
+            vw.S(S_DU + 2 * buf, k) = du0;
+            vw.S(S_DU + 2 * buf + 1, k) = du1;
+        }
+        double aj[9];
+#pragma unroll
+        for (int l = 0; l < 9; ++l) aj[l] = src.AJ(l, k);
+        const double eq = src.CR(q, k + 1);
+        const double n0 = (d[0] - eq) + fma(aj[0], d[2], aj[1] * d[5]);
+        const double n1 = (d[1] - eq) + fma(aj[2], d[2], aj[3] * d[5]);
+        const double n2 = (d[2] - eq) + fma(aj[4], d[4], aj[5] * d[5]);
+        const double n3 = (d[3] - eq) + fma(aj[6], d[3], fma(aj[7], d[4], aj[8] * d[5]));
+        const double n4 = (d[4] - eq) + dt * du1;
+        const double n5 = (d[5] - eq) + dt * du0;
+        dq = q == 0 ? n0 : q == 1 ? n1 : q == 2 ? n2 : q == 3 ? n3 : q == 4 ? n4 : n5;
+    }
+#else
     const int r = lane < 6 ? lane : 0;
     double dx[6];
 #pragma unroll
@@ -1678,6 +1756,7 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf)
 #pragma unroll
         for (int q = 0; q < 6; ++q) dx[q] = nx[q];
     }
+#endif
 }
 
 // elastic-pair step of one row from its new multiplier: dp = (y+ - g_p)/D_p, dn = (-y+ - g_n)/D_n, plus
@@ -2397,6 +2476,7 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
 #pragma unroll
                 for (int r = 0; r < 4; ++r) c.B(B_D + r, pj, k) = pdv[r];
             Blk bk;
+            bk.m = c.slab + threadIdx.x;
             blk_lin(a, x, tr, j, w, y, bk);
 #pragma unroll
             for (int r = 0; r < 4; ++r) pdv[r] = bk.d[r];
@@ -2745,19 +2825,6 @@ __device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft
         for (int i = 0; i < 9; ++i) r[65 + i] = aj[i];
     }
 }
-// row_newbcast:l (gfx90a+ DPP on a 64-bit move): every lane of a 16-lane row receives lane l of that row
-template <int L_>
-__device__ __forceinline__ double rowbc(double v) {
-    const long long b = __double_as_longlong(v);
-    return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + L_, 0xF, 0xF, false));
-}
-
-// A/B switch: riccati_vec with lane q owning component q of the cost-to-go vector and the other components
-// broadcast by DPP (1), or every lane carrying the whole vector and reading every operand (0).  Same operations in
-// the same order either way (bitwise identical).
-#ifndef OBCA_VEC_DPP
-#define OBCA_VEC_DPP 1
-#endif
 template <class Src>
 __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft) {
     const WsView vw = ws_view(c);
