@@ -417,7 +417,7 @@ typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: 
 // the factor-record stores (one in-order vmcnt); ds_ reads wait on lgkmcnt only.
 // A/B switch: W_{x lam} of the block (16 doubles) in the slab too (1) or in registers (0)
 #ifndef OBCA_HXL_SLAB
-#define OBCA_HXL_SLAB 0
+#define OBCA_HXL_SLAB 1
 #endif
 constexpr int kSlab = OBCA_HXL_SLAB ? 64 : 48;
 struct Blk {
