@@ -1923,10 +1923,12 @@ __device__ __noinline__ void phase_recover(const Ctx& c, LShared& sh, double mu,
 
 // ======== phase: trial point x + alpha d (step buffer buf) -> theta, phi (barrier objective), bad ========
 // of the current NLP; also stores the trial residual rows (for second-order corrections)
-__device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, double alpha, int buf, double (&out)[3]) {
+template <bool RS_>
+__device__ __noinline__ void phase_trial_t(const Ctx& c, LShared& sh, double mu, double alpha, int buf, double (&out)[3]) {
     LArgs& a = *c.a;
     const int N = c.N;
-    const bool plan = c.plan(), rs = sh.R != 0;
+    const bool plan = c.plan();
+    constexpr bool rs = RS_;
     double th = 0.0, F = 0.0, logs = 0.0, bad = 0.0;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0};
@@ -2081,6 +2083,13 @@ __device__ __noinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, d
     out[2] = v[3];
 }
 
+// one instantiation per problem (original / restoration phase): the original problem's skips every restoration
+// branch and its loads (bitwise the same results, profiles/r03/ab_one/)
+__device__ __forceinline__ void phase_trial(const Ctx& c, LShared& sh, double mu, double alpha, int buf, double (&out)[3]) {
+    sh.R ? phase_trial_t<true>(c, sh, mu, alpha, buf, out) : phase_trial_t<false>(c, sh, mu, alpha, buf, out);
+}
+
+
 // ======== phase: second-order-correction residual r <- a_soc r + r(trial) ========
 // (both residual phases load every value before the stores that would precede it in program order -- their
 // waits would include those stores, one in-order vmcnt queue -- so a block's results are stored after the
@@ -2165,9 +2174,10 @@ __device__ __forceinline__ void load_upd_in(const Ctx& c, bool rs, int buf, int 
 // All loads of a stage are issued before its stores, and block j+1's loads before block j's stores: the
 // workspace fields may alias as far as the compiler knows, so interleaved load / store pairs would each wait
 // for the previous stores (one in-order vmcnt queue).
-__device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
+template <bool RS_>
+__device__ __noinline__ void phase_update_t(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
     const int N = c.N;
-    const bool rs = sh.R != 0;
+    constexpr bool rs = RS_;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], d[6], zl[6], zu[6], y[6], yp[6], pr[6], nr[6], zp[6], zn[6], dp[6], dn[6];
 #pragma unroll
@@ -2324,6 +2334,13 @@ __device__ __noinline__ void phase_update(const Ctx& c, LShared& sh, double mu, 
     }
 }
 
+// one instantiation per problem (original / restoration phase): the original problem's skips every restoration
+// branch and its loads (bitwise the same results, profiles/r03/ab_one/)
+__device__ __forceinline__ void phase_update(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
+    sh.R ? phase_update_t<true>(c, sh, mu, alpha, az, buf) : phase_update_t<false>(c, sh, mu, alpha, az, buf);
+}
+
+
 // filters: [0] original problem, [1] restoration problem
 __device__ __forceinline__ bool in_filter(const LShared& sh, int f, double th, double ph) {
     for (int i = 0; i < sh.nfl[f]; ++i)
@@ -2348,10 +2365,12 @@ __device__ __forceinline__ void add_filter(LShared& sh, int f, double th, double
 //      [5] theta (l1 of the residual rows) [6] objective [7] sum log slacks [8] sum |dual residuals|
 //      [9] original theta [10] original cost [11] original sum log slacks [12] original primal inf (max)
 //      (restoration: the original problem's rows without p, n)
-__device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[13]) {
+template <bool RS_>
+__device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red)[13]) {
     LArgs& a = *c.a;
     const int N = c.N;
-    const bool plan = c.plan(), rs = sh.R != 0;
+    const bool plan = c.plan();
+    constexpr bool rs = RS_;
     const double zeta = sh.zeta;
 #pragma unroll
     for (int i = 0; i < 13; ++i) red[i] = 0.0;
@@ -2623,6 +2642,13 @@ __device__ __noinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[
     const int ops[13] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_MAX};
     wg_reduce(sh, red, ops);
 }
+
+// one instantiation per problem (original / restoration phase): the original problem's skips every restoration
+// branch and its loads (bitwise the same results, profiles/r03/ab_one/)
+__device__ __forceinline__ void phase_lin(const Ctx& c, LShared& sh, double (&red)[13]) {
+    sh.R ? phase_lin_t<true>(c, sh, red) : phase_lin_t<false>(c, sh, red);
+}
+
 
 // ======== phase: complementarity vs mu: max and sum of |z s - mu| (elastic pairs included) ========
 __device__ __noinline__ double2 phase_compl(const Ctx& c, LShared& sh, double mu) {
