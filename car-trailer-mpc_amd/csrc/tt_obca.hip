@@ -2365,6 +2365,55 @@ __device__ __forceinline__ void add_filter(LShared& sh, int f, double th, double
 //      [5] theta (l1 of the residual rows) [6] objective [7] sum log slacks [8] sum |dual residuals|
 //      [9] original theta [10] original cost [11] original sum log slacks [12] original primal inf (max)
 //      (restoration: the original problem's rows without p, n)
+// |z s - mu| over every bound and elastic pair of stage k (its blocks and, at k = N in plan mode, the final rows):
+// max into cm[0], sum into cm[1].  (Evaluated inside phase_lin as well it measured slower than this pass of its own:
+// profiles/r03/ab_cfold/.)
+__device__ __forceinline__ void compl_stage(const Ctx& c, const LShared& sh, int k, double mu, bool rs, double (&cm)[2]) {
+    const int N = c.N;
+    auto acc = [&](double v) { cm[0] = fmax(cm[0], v); cm[1] += v; };
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const double xv = c.S(S_X + i, k);
+        if (c.hlx(i)) acc(fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
+        if (c.hux(i)) acc(fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
+        if (rs) {
+            acc(fabs(c.S(S_ZP + i, k) * c.S(S_PR + i, k) - mu));
+            acc(fabs(c.S(S_ZN + i, k) * c.S(S_NR + i, k) - mu));
+        }
+    }
+    if (k < N)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const double uv = c.S(S_U + i, k);
+            if (c.hlu(i)) acc(fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
+            if (c.huu(i)) acc(fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
+        }
+    for (int j = 0; j < c.nbk; ++j) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc(fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double s = c.B(B_S + r, j, k);
+            acc(fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
+            if (c.hrl(r)) acc(fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
+            if (rs) {
+                acc(fabs(c.B(B_ZP + r, j, k) * c.B(B_PR + r, j, k) - mu));
+                acc(fabs(c.B(B_ZN + r, j, k) * c.B(B_NR + r, j, k) - mu));
+            }
+        }
+    }
+    if (k == N && c.plan())
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            acc(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu));
+            acc(fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu));
+            if (rs) {
+                acc(fabs(sh.zpf[i] * sh.pf[i] - mu));
+                acc(fabs(sh.znf[i] * sh.nf[i] - mu));
+            }
+        }
+}
+
 template <bool RS_>
 __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red)[13]) {
     LArgs& a = *c.a;
@@ -2374,6 +2423,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
     const double zeta = sh.zeta;
 #pragma unroll
     for (int i = 0; i < 13; ++i) red[i] = 0.0;
+
     const double* xinit = a.x0 + 6 * (size_t)c.b;
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], u[2] = {0.0, 0.0}, gl[6];
@@ -2431,6 +2481,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
             for (int i = 0; i < 6; ++i) ck[i] = x[i] - (xp[i] + a.dt * fo[i]);
         }
         LogSum lsum, lorig;
+        double crs[6];  // the Newton right-hand side's dynamics rows (phase_resid's S_CR), stored with the stage
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             double res = ck[i];
@@ -2452,6 +2503,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
             red[5] += fabs(res);
             red[9] += fabs(ck[i]);
             red[12] = fmax(red[12], fabs(ck[i]));
+            crs[i] = res;
         }
         double yk[6], yn[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -2473,7 +2525,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
 #pragma unroll
         for (int i = 0; i < 6; ++i) red[3] += fabs(yk[i]);
         const Trig tr = stage_trig(x);
-        double pdv[4] = {0, 0, 0, 0};
+        double pdv[4] = {0, 0, 0, 0}, pdr[4] = {0, 0, 0, 0};  // the previous block's row values and residual rows
         int pj = -1;
         for (int j = 0; j < c.nbk; ++j) {
             double w[8], y[4], zw[8], drw[8], wrv[8], sv[4], vlv[4], vuv[4], prv[4], nrv[4], zpv[4], znv[4];
@@ -2493,7 +2545,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
             }
             if (pj >= 0)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) c.B(B_D + r, pj, k) = pdv[r];
+                for (int r = 0; r < 4; ++r) { c.B(B_D + r, pj, k) = pdv[r]; c.B(B_DR + r, pj, k) = pdr[r]; }
             Blk bk;
             bk.m = c.slab + threadIdx.x;
             blk_lin(a, x, tr, j, w, y, bk);
@@ -2550,6 +2602,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
                 }
                 red[1] = fmax(red[1], fabs(res));
                 red[5] += fabs(res);
+                pdr[r] = res;
                 red[3] += fabs(y[r]) + vu;
                 red[4] += vu;
                 red[2] = fmax(red[2], fabs(vu * (c.rU(r) - s)));
@@ -2591,6 +2644,7 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
                 }
                 red[1] = fmax(red[1], fabs(res));
                 red[5] += fabs(res);
+                sh.dfr[i] = res;
                 const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
                 red[2] = fmax(red[2], fmax(fabs(sh.vLf[i] * sl), fabs(sh.vUf[i] * su)));
                 red[3] += fabs(sh.ydf[i]) + sh.vLf[i] + sh.vUf[i];
@@ -2621,9 +2675,9 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
             }
         if (pj >= 0)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) c.B(B_D + r, pj, k) = pdv[r];
+            for (int r = 0; r < 4; ++r) { c.B(B_D + r, pj, k) = pdv[r]; c.B(B_DR + r, pj, k) = pdr[r]; }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) { c.S(S_GX + i, k) = gxs[i]; c.S(S_C + i, k) = ck[i]; }
+        for (int i = 0; i < 6; ++i) { c.S(S_GX + i, k) = gxs[i]; c.S(S_C + i, k) = ck[i]; c.S(S_CR + i, k) = crs[i]; }
         if (k < N) {
 #pragma unroll
             for (int i = 0; i < 2; ++i) c.S(S_GU + i, k) = gus[i];
@@ -2655,50 +2709,7 @@ __device__ __noinline__ double2 phase_compl(const Ctx& c, LShared& sh, double mu
     const int N = c.N;
     const bool rs = sh.R != 0;
     double cm[2] = {0.0, 0.0};
-    auto acc = [&](double v) { cm[0] = fmax(cm[0], v); cm[1] += v; };
-    for (int k = (int)threadIdx.x; k <= N; k += T) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const double xv = c.S(S_X + i, k);
-            if (c.hlx(i)) acc(fabs(c.S(S_ZLX + i, k) * (xv - c.xl[i]) - mu));
-            if (c.hux(i)) acc(fabs(c.S(S_ZUX + i, k) * (c.xu[i] - xv) - mu));
-            if (rs) {
-                acc(fabs(c.S(S_ZP + i, k) * c.S(S_PR + i, k) - mu));
-                acc(fabs(c.S(S_ZN + i, k) * c.S(S_NR + i, k) - mu));
-            }
-        }
-        if (k < N)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const double uv = c.S(S_U + i, k);
-                if (c.hlu(i)) acc(fabs(c.S(S_ZLU + i, k) * (uv - c.ul[i]) - mu));
-                if (c.huu(i)) acc(fabs(c.S(S_ZUU + i, k) * (c.uu[i] - uv) - mu));
-            }
-        for (int j = 0; j < c.nbk; ++j) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc(fabs(c.B(B_ZW + e, j, k) * (c.B(B_W + e, j, k) + RELAX) - mu));
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double s = c.B(B_S + r, j, k);
-                acc(fabs(c.B(B_VU + r, j, k) * (c.rU(r) - s) - mu));
-                if (c.hrl(r)) acc(fabs(c.B(B_VL + r, j, k) * (s - c.rL(r)) - mu));
-                if (rs) {
-                    acc(fabs(c.B(B_ZP + r, j, k) * c.B(B_PR + r, j, k) - mu));
-                    acc(fabs(c.B(B_ZN + r, j, k) * c.B(B_NR + r, j, k) - mu));
-                }
-            }
-        }
-        if (k == N && c.plan())
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                acc(fabs(sh.vLf[i] * (sh.sf[i] - c.fL) - mu));
-                acc(fabs(sh.vUf[i] * (c.fU - sh.sf[i]) - mu));
-                if (rs) {
-                    acc(fabs(sh.zpf[i] * sh.pf[i] - mu));
-                    acc(fabs(sh.znf[i] * sh.nf[i] - mu));
-                }
-            }
-    }
+    for (int k = (int)threadIdx.x; k <= N; k += T) compl_stage(c, sh, k, mu, rs, cm);
     const int ops[2] = {R_MAX, R_SUM};
     wg_reduce(sh, cm, ops);
     return make_double2(cm[0], cm[1]);
@@ -3995,8 +4006,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 }
                 const double mu = stt.mu;
                 const double th0 = red[5], phi0 = red[6] - mu * red[7];
-                phase_resid(cs, sh, false);
-                __syncthreads();
+                // the Newton right-hand side's residual rows (S_CR / B_DR / dfr) were stored by phase_lin at this
+                // iterate: the same expressions as phase_resid's
                 // ---- Newton step with inertia correction (IPOPT delta_w schedule) ----
                 double dw = 0.0;
                 bool ok = false;
