@@ -3986,9 +3986,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 }
                 // ---- barrier update (monotone, Fiacco-McCormick); the filter is reset on every change ----
                 while (stt.mu > a.tol / 10.0 * 1.0000001) {
+                    // E_mu = max(dual, primal, complementarity): when the first two already exceed kappa_eps mu the
+                    // test fails whatever the complementarity is (fmax(a, b) >= a for a non-NaN a), so its pass is
+                    // skipped -- the usual case away from convergence; the decision is the same as with it
+                    const double e_dp = fmax(dinf / sd, pinf);
+                    if (e_dp > kappa_eps * stt.mu) break;
                     const double2 cm = phase_compl(cs, sh, stt.mu);
                     stamp(sh, ston, OPH_COMPL);
-                    if (!(fmax(fmax(dinf / sd, pinf), cm.x / sc) <= kappa_eps * stt.mu)) break;
+                    if (!(fmax(e_dp, cm.x / sc) <= kappa_eps * stt.mu)) break;
                     stt.mu = fmax(a.tol / 10.0, fmin(kappa_mu * stt.mu, pow(stt.mu, theta_mu)));
                     stt.tau = fmax(0.99, 1.0 - stt.mu);
                     __syncthreads();
