@@ -780,8 +780,8 @@ TRAFFIC_COMMIT = "fcd2080"
 
 # committed PMC passes of obca_kernel (tools/obca_pmc.sh): HBM bytes per instance-iteration, scaled by a launch's
 # summed IPM iterations for roofline.traffic of the OBCA lines (same N, M; c4all shares c4's kernel shape)
-OBCA_PMC = {"c4": "profiles/r03/final_6c9da3e/pmc_c4", "c4all": "profiles/r03/final_6c9da3e/pmc_c4",
-            "cobs": "profiles/r03/final_6c9da3e/pmc_cobs"}
+OBCA_PMC = {"c4": "profiles/r03/final_c844f7e/pmc_c4", "c4all": "profiles/r03/final_c844f7e/pmc_c4",
+            "cobs": "profiles/r03/final_c844f7e/pmc_cobs"}
 
 
 def obca_traffic(cfg, iters_sum):
