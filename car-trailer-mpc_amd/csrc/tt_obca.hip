@@ -4064,8 +4064,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                             }
                             if (okls) { accepted = true; break; }
                             if (ls == 0 && isfinite(tr[1]) && tr[0] >= th0) {
-                                // second-order corrections into step buffer 1
-                                phase_resid(cs, sh, false);
+                                // second-order corrections into step buffer 1 (the residual rows S_CR / B_DR / dfr
+                                // still hold phase_lin's values at the iterate: nothing since the linearisation
+                                // writes them, and this is the iteration's only SOC sequence)
                                 __syncthreads();
                                 double a_soc = alpha, th_old = th0, th_t = tr[0];
                                 bool soc_ok = false;
