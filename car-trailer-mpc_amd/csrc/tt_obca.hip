@@ -36,16 +36,26 @@
 // cross-statement fusion depends on how many uses a product has in the inlined context, so the same block
 // elimination could round differently in phase_factor and in the recovery passes that recompute it
 // (block_refactor); with contraction fixed by the source they are bitwise the same computation.
+#ifndef OBCA_CONTRACT
+#define OBCA_CONTRACT 1
+#endif
+#if OBCA_CONTRACT == 0
+#pragma clang fp contract(off)
+#elif OBCA_CONTRACT == 1
 #pragma clang fp contract(on)
+#else
+#pragma clang fp contract(fast)
+#endif
 
 // A/B switch: phase_factor loads block j+1's inputs during block j (1) or each block's at its start (0)
 #ifndef OBCA_FACTOR_PF
 #define OBCA_FACTOR_PF 1
 #endif
 // A/B switch: the block elimination divides through shared reciprocals (v_rcp_f64 + two Newton steps, <= 1 ulp) and
-// takes 1/sqrt by v_rsq_f64 + Newton (1), or by IEEE division / sqrt (0)
+// takes 1/sqrt by v_rsq_f64 + Newton (1), or by IEEE division / sqrt (0, the default since round 4: the oracle
+// divides, and the GPU-vs-oracle status agreement is measured closer with it, profiles/r04/parity/)
 #ifndef OBCA_RCP
-#define OBCA_RCP 1
+#define OBCA_RCP 0
 #endif
 
 namespace ttmpc {
@@ -152,7 +162,8 @@ struct Shared {
     int R;       // 1 while in the restoration phase
     int lsq;     // 1 while assembling the least-squares multiplier system
     double zeta; // restoration proximity weight sqrt(mu_R)
-    int flag;
+    double dc;   // delta_c (= delta_d) of the current factorisation: -dc on every constraint row's diagonal
+    int flag;    // the Riccati sweep's factorisation code (F_OK / F_MANY / F_ZERO)
     unsigned long long stamp[kObcaPhases];
     unsigned long long t0;
 };
@@ -447,10 +458,26 @@ struct Blk {
     double E[4];                     // E of the 4 rows: 1/D (+ 1/D_p + 1/D_n in the restoration phase)
 };
 
+// Factorisation outcomes (oracle/c/tt_obca.c: factor): F_MANY a negative pivot where IPOPT's inertia (n, m, 0) wants a
+// positive one (PerturbForWrongInertia), F_ZERO a numerically zero pivot, F_FEW too few negative eigenvalues (both
+// PerturbForSingularity: IPOPT's PDFullSpaceSolver treats the second as singular once IncreaseQuality fails, and the
+// elimination here has no pivot tolerance to raise).
+enum { F_OK = 0, F_MANY = 1, F_ZERO = 2, F_FEW = 3 };
+// a failed Cholesky pivot s of a positive-definiteness test (diagonal entry ajj): negative, or numerically zero
+__device__ __forceinline__ int pivot_fail(double s, double ajj) { return s < -1e-14 * fabs(ajj) ? F_MANY : F_ZERO; }
+// the 2x2 reduced input Hessian G of a Riccati stage: F_OK when positive definite, else how its Cholesky fails
+// (first pivot G00, second G11 - G01^2 / G00 = det / G00)
+__device__ __forceinline__ int g2_code(double G00, double G11, double det) {
+    if (!(G00 >= 2.2250738585072014e-308)) return pivot_fail(G00, G00);
+    if (!(det >= 2.2250738585072014e-308 * G00)) return pivot_fail(det, G11 * G00);
+    return F_OK;
+}
+
 // Signed LDL' of a packed lower 4x4, A = L S L' (S = diag(+-1), |L_jj| = sqrt|d_j|, no pivoting; the oracle's
 // schol).  The diagonal keeps S_j / L_jj: the solves multiply by its magnitude and read S_j from its sign.  Returns
-// the number of negative pivots, or -1 on a (numerically) zero pivot; with pd a negative pivot fails too (round 2's
-// positive-definite test).  On a positive definite matrix every operation is the plain Cholesky's (S = 1 exactly).
+// the number of negative pivots, -1 on a (numerically) zero pivot (|s| <= 1e-14 |a_jj|; a subnormal positive pivot
+// counts as zero, since 1/sqrt of it overflows), or -2 on a negative pivot with pd (round 2's positive-definite test).
+// On a positive definite matrix every operation is the plain Cholesky's (S = 1 exactly).
 __device__ __forceinline__ double sgn(double d) { return copysign(1.0, d); }
 __device__ __forceinline__ int schol4(double* L, bool pd) {
     int neg = 0;
@@ -460,7 +487,10 @@ __device__ __forceinline__ int schol4(double* L, bool pd) {
         double s = ajj;
 #pragma unroll
         for (int k = 0; k < j; ++k) s = fma(-(L[lo4(j, k)] * sgn(L[lo4(k, k)])), L[lo4(j, k)], s);
-        if (!(s > 0.0) && (pd || !(s < -1e-14 * fabs(ajj)))) return -1;
+        if (!(s >= 2.2250738585072014e-308)) {  // s < DBL_MIN, or NaN
+            if (!(s < -1e-14 * fabs(ajj))) return -1;
+            if (pd) return -2;
+        }
         const double sj = s > 0.0 ? 1.0 : -1.0;
         neg += s < 0.0 ? 1 : 0;
 #if OBCA_RCP
@@ -602,14 +632,14 @@ __device__ __forceinline__ double jwm(const Blk& k, int r, int a) {
 // sig_w: diagonal Hessian of the 8 duals (Sigma_w, plus zeta D_R^2 in the restoration phase); E: the rows'
 // dual regularisation (1/D, plus 1/D_p + 1/D_n in the restoration phase).  Adds the Schur complement
 // W_xx - Z' S_A Z + G' T^-1 G into the stage Hessian contribution C (10 packed lower entries over X,Y,theta,psi).
-__device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double dw, double* C, bool pd) {
+__device__ __forceinline__ int blk_factor(Blk& k, const double* sig_w, double dw, double* C, bool pd) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         k.idm[i] = frcp(sig_w[i] + dw);
         k.LL[lo4(i, i)] += sig_w[4 + i] + dw;
     }
     const int negA = schol4(k.LL, pd);
-    if (negA < 0) return false;
+    if (negA < 0) return negA == -1 ? F_ZERO : F_MANY;
     double SA[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) SA[a] = sgn(k.LL[lo4(a, a)]);
@@ -650,7 +680,11 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
             for (int a = 0; a < 4; ++a) g += (k.Yl(a, r) * SA[a]) * k.Zl(a, q);
             k.G(r, q) = g;
         }
-    if (schol4(k.LT, pd) != negA) return false;
+    const int negT = schol4(k.LT, pd);
+    // Haynsworth: the block has IPOPT's inertia (8, 4, 0) iff negT == negA; negT > negA leaves it with too few negative
+    // eigenvalues (its rows need delta_c), negT < negA with too many (negative curvature: delta_x)
+    if (negT < 0) return negT == -1 ? F_ZERO : F_MANY;
+    if (negT != negA) return negT > negA ? F_FEW : F_MANY;
     double Wm[4][4];  // LT^-1 G
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -670,7 +704,7 @@ __device__ __forceinline__ bool blk_factor(Blk& k, const double* sig_w, double d
                 t += (Wm[a][p] * sgn(k.LT[lo4(a, a)])) * Wm[a][q] - (k.Zl(a, p) * SA[a]) * k.Zl(a, q);
             C[lo4(p, q)] += t;
         }
-    return true;
+    return F_OK;
 }
 
 // right-hand side of a factored block.  fw: gradient constants of the 8 duals; rd: row constant
@@ -885,14 +919,16 @@ __device__ __forceinline__ void load_blk_in(const Ctx& c, bool rs, int j, int k,
     }
 }
 
-// linearise + factor + rhs of one block at the current iterate (inputs preloaded); returns false if not
-// positive definite.  Outputs D (Sigma_s + dw), E (row regularisation), the elimination and the block's
-// Hessian / gradient contribution to its stage.
+// linearise + factor + rhs of one block at the current iterate (inputs preloaded); returns the factorisation outcome
+// (F_OK ...).  Outputs D (Sigma_s + dw), E (row regularisation: 1/D + delta_c, plus 1/D_p + 1/D_n in the restoration
+// phase), the elimination and the block's Hessian / gradient contribution to its stage.  With delta_c the row
+// constant carries + delta_c y (IPOPT perturbs dy; the unknown here is y+ = y + dy).
 template <bool RHS = true>
-__device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, const BlkIn& in, int j, const double* x,
+__device__ __forceinline__ int block_setup(const Ctx& c, const LShared& sh, const BlkIn& in, int j, const double* x,
                                             const Trig& tr, double mu, double dw, Blk& bk, double* fw, double* zf,
                                             double* t4, double* C4, double* q4) {
     const bool rs = sh.R != 0, lsq = sh.lsq != 0;
+    const double dc = sh.dc;
     double sw[8], rd[4];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -920,9 +956,10 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, con
         const double iu = frcp(c.rU(r) - s), il = c.hrl(r) ? frcp(s - c.rL(r)) : 0.0;
         const double sg = c.hrl(r) ? vu * iu + vl * il : vu * iu, gr = c.hrl(r) ? mu * iu - mu * il : mu * iu;
         bk.D[r] = lsq ? 1.0 : sg + dw;
-        bk.E[r] = frcp(bk.D[r]);
+        const double iD = frcp(bk.D[r]);
+        bk.E[r] = iD + dc;
         const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : gr;
-        rd[r] = in.dr[r] + gs * bk.E[r];
+        rd[r] = (dc > 0.0 ? fma(dc, in.y[r], in.dr[r]) : in.dr[r]) + gs * iD;
         if (rs) {
             const PN t = pn_terms(lsq, in.pr[r], in.nr[r], in.zp[r], in.zn[r], mu, dw);
             const double ip = frcp(t.Dp), in_ = frcp(t.Dn);
@@ -931,9 +968,9 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, con
         }
 #else
         bk.D[r] = lsq ? 1.0 : sig_row(c, r, s, vl, vu) + dw;
-        bk.E[r] = 1.0 / bk.D[r];
+        bk.E[r] = 1.0 / bk.D[r] + dc;
         const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
-        rd[r] = in.dr[r] + gs / bk.D[r];
+        rd[r] = (dc > 0.0 ? fma(dc, in.y[r], in.dr[r]) : in.dr[r]) + gs / bk.D[r];
         if (rs) {
             const PN t = pn_terms(lsq, in.pr[r], in.nr[r], in.zp[r], in.zn[r], mu, dw);
             bk.E[r] += 1.0 / t.Dp + 1.0 / t.Dn;
@@ -941,9 +978,10 @@ __device__ __forceinline__ bool block_setup(const Ctx& c, const LShared& sh, con
         }
 #endif
     }
-    if (!blk_factor(bk, sw, dw, C4, c.pd)) return false;
+    const int f = blk_factor(bk, sw, dw, C4, c.pd);
+    if (f != F_OK) return f;
     if constexpr (RHS) blk_rhs(bk, fw, rd, zf, t4, q4);
-    return true;
+    return F_OK;
 }
 
 // The block's elimination recomputed where a recovery pass needs it, from the same workspace inputs through the same
@@ -959,15 +997,17 @@ __device__ __forceinline__ void block_refactor(const Ctx& c, const LShared& sh, 
     block_setup<RHS>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
 }
 
-// ======== phase: stage Hessians + gradients (all threads) -> fail flag (uniform) ========
-// Also the effective dynamics-row residuals S_CE (= S_CR outside the restoration phase) and the soft-row
-// scales S_SD = sqrt(1/D_p + 1/D_n) of the restoration phase.
-__device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, double dw) {
+// ======== phase: stage Hessians + gradients (all threads) -> factorisation outcome (uniform) ========
+// Also the effective dynamics-row residuals S_CE (= S_CR + delta_c y outside the restoration phase) and the soft-row
+// scales S_SD = sqrt(E) (E = 1/D_p + 1/D_n in the restoration phase, + delta_c).
+__device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, double dw) {
     const WsView vw = ws_view(c);
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0, lsq = sh.lsq != 0;
-    double fail[1] = {0.0};
+    const double dc = sh.dc;
+    const bool soft = rs || dc > 0.0;
+    double fail[3] = {0.0, 0.0, 0.0};  // F_ZERO, F_MANY, F_FEW seen
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6];
         load_x(c, k, x);
@@ -987,7 +1027,10 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
 #if !OBCA_FACTOR_PF
             load_blk_in(c, rs, j, k, cur);
 #endif
-            if (!block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4)) fail[0] = 1.0;
+            const int f = block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
+            if (f == F_ZERO) fail[0] = 1.0;
+            if (f == F_MANY) fail[1] = 1.0;
+            if (f == F_FEW) fail[2] = 1.0;
 #if OBCA_FACTOR_PF
             if (j + 1 < c.nbk) load_blk_in(c, rs, j + 1, k, cur);
 #endif
@@ -1035,7 +1078,7 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
                 const double sl = sh.sf[i] - c.fL, su = c.fU - sh.sf[i];
                 const double Ds = lsq ? 1.0 : sh.vLf[i] / sl + sh.vUf[i] / su + dw;
                 const double gs = lsq ? -sh.vLf[i] + sh.vUf[i] : -mu / sl + mu / su;
-                double E = 1.0 / Ds, rf = sh.dfr[i] + gs / Ds;
+                double E = 1.0 / Ds + dc, rf = (dc > 0.0 ? fma(dc, sh.ydf[i], sh.dfr[i]) : sh.dfr[i]) + gs / Ds;
                 if (rs) {
                     const PN t = pn_terms(lsq, sh.pf[i], sh.nf[i], sh.zpf[i], sh.znf[i], mu, dw);
                     E += 1.0 / t.Dp + 1.0 / t.Dn;
@@ -1054,13 +1097,15 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
         for (int i = 0; i < 6; ++i) vw.S(S_QV + i, k) = qv[i];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
-            double ce = vw.S(S_CR + i, k), sd = 0.0;
+            double ce = vw.S(S_CR + i, k), sd = 0.0, e = dc;
+            if (dc > 0.0) ce = fma(dc, (double)vw.S(S_YC + i, k), ce);
             if (rs) {
                 const PN t = pn_terms(lsq, vw.S(S_PR + i, k), vw.S(S_NR + i, k), vw.S(S_ZP + i, k), vw.S(S_ZN + i, k), mu, dw);
                 const double ip = inv(t.Dp), in_ = inv(t.Dn);
                 ce += t.gp * ip - t.gn * in_;
-                sd = sqrt(ip + in_);
+                e = (ip + in_) + dc;
             }
+            if (soft) sd = sqrt(e);
             vw.S(S_CE + i, k) = ce;
             vw.S(S_SD + i, k) = sd;
         }
@@ -1089,9 +1134,9 @@ __device__ __noinline__ bool phase_factor(const Ctx& c, LShared& sh, double mu, 
             vw.S(S_RV + 1, k) = g1;
         }
     }
-    const int ops[1] = {R_MAX};
+    const int ops[3] = {R_MAX, R_MAX, R_MAX};
     wg_reduce(sh, fail, ops);
-    return fail[0] == 0.0;
+    return fail[0] != 0.0 ? F_ZERO : fail[1] != 0.0 ? F_MANY : fail[2] != 0.0 ? F_FEW : F_OK;
 }
 
 // Stage data of the serial sweeps, either straight from the HBM workspace (GSrc) or from LDS copies
@@ -1245,6 +1290,7 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
     double pv = vec ? src.QV(r, N) : 0.0;
     if (vec) src.setPV(r, N, pv);
     bool fail = false;
+    int fcode = F_OK;  // the first failed pivot's outcome (the oracle stops there)
     // one stage; `cur` = this stage's operands, `nx` receives stage k-1's (ping-pong, no struct copies)
     auto stage = [&](int k, const RicOps& cur, RicOps& nx) __attribute__((always_inline)) {
         // ---- row `row` of P_{k+1}: PA[i][j] (act lanes) and p' = p - P c (vector lanes)
@@ -1267,7 +1313,9 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
         // ---- reduced input Hessian G = R~ + B'PB and its inverse
         const double G00 = cur.R0 + dt2 * p55, G01 = cur.R1 + dt2 * g44.y, G11 = cur.R3 + dt2 * g44.x;
         const double det = G00 * G11 - G01 * G01;
-        fail = fail || !(G00 > 0.0) || !(det > 0.0);
+        const int gc = g2_code(G00, G11, det);
+        if (!fail) fcode = gc;
+        fail = fail || gc != F_OK;
         const double idet = frcp(det);
         const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
         // ---- column jj of PA, and PA[4..5][ii] (H at ii); vector lanes: PA[4..5][r]
@@ -1331,8 +1379,8 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
         if (__builtin_amdgcn_readfirstlane((int)fail)) break;
     }
     if (k == 0 && !fail) stage(0, oa, ob);
-    // any lane's failure flag (all lanes evaluate the same uniform G; keep it explicit)
-    if (lane == 0) sh.flag = fail ? 1 : 0;
+    // the failure code (all lanes evaluate the same uniform G; keep it explicit)
+    if (lane == 0) sh.flag = fcode;
     wave_sync();
 }
 
@@ -1469,6 +1517,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
     double pv = vec ? src.QV(r, N) : 0.0;
     if (vec) out.setPV(r, N, pv);
     bool fail = false;
+    int fcode = F_OK;
     lds_order();
     auto stage = [&](int k, const SoftOps& cur, SoftOps& nx) __attribute__((always_inline)) {
         if (k > 0) soft_ops(src, k - 1, i, j, sij, r, vec, nx);  // next stage's operands, one stage ahead
@@ -1476,9 +1525,11 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         // each pivot arrives by v_readlane, its row and column entries by ds_bpermute, so no LDS write / read
         // round trip sits on the six-pivot chain (same arithmetic as an LDS tile)
         double mv = act ? (i == j ? 1.0 : 0.0) + cur.si * Pt[8 * ii + jj] * cur.sj : 0.0;
+        const double m0 = mv;  // M before elimination (its diagonal classifies a failed pivot)
 #pragma unroll
         for (int p = 0; p < 6; ++p) {
             const double piv = readlane_d(mv, 7 * p);
+            if (!fail && !(piv >= 2.2250738585072014e-308)) fcode = pivot_fail(piv, readlane_d(m0, 7 * p));
             const double aip = __shfl(mv, 6 * i + p), apj = __shfl(mv, 6 * p + j);
 #if OBCA_RCP
             const double ip = frcp(piv);
@@ -1486,7 +1537,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
             const double ip = 1.0 / piv;
 #endif
             const double nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : mv - aip * apj * ip;
-            fail = fail || !(piv > 0.0);
+            fail = fail || !(piv >= 2.2250738585072014e-308);
             mv = act ? nv : 0.0;
         }
         // Branch-free from here on: every lane evaluates the entry expressions at its clamped (i, j) / r and only the
@@ -1537,7 +1588,9 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         const double G00 = o.R0 + dt2 * Pt[8 * 5 + 5], G01 = o.R1 + dt2 * Pt[8 * 5 + 4];
         const double G11 = o.R3 + dt2 * Pt[8 * 4 + 4];
         const double det = G00 * G11 - G01 * G01;
-        fail = fail || !(G00 > 0.0) || !(det > 0.0);
+        const int gc = g2_code(G00, G11, det);
+        if (!fail) fcode = gc;
+        fail = fail || gc != F_OK;
 #if OBCA_RCP
         const double idet = frcp(det);
 #else
@@ -1596,7 +1649,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         if (__builtin_amdgcn_readfirstlane((int)fail)) break;
     }
     if (k == 0 && !fail) stage(0, oa, ob);
-    if (lane == 0) sh.flag = fail ? 1 : 0;
+    if (lane == 0) sh.flag = fcode;
     wave_sync();
 }
 
@@ -2717,13 +2770,18 @@ __device__ __noinline__ double2 phase_compl(const Ctx& c, LShared& sh, double mu
 
 // Newton solve for the current residual arrays (S_CR / B_DR / sh.dfr) with the given dw into buffer buf.
 // Returns false when the Riccati/blocks are not positive definite.
-__device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
+// One factorisation + condensed solve with the perturbations (dw, dc) into step buffer buf: F_OK, or the outcome of the
+// failed factorisation (F_MANY / F_ZERO / F_FEW) for the perturbation handler.
+__device__ __noinline__ int newton_solve(const Ctx& c, LShared& sh, double mu, double dw, double dc, int buf) {
     const bool on = c.a->stamps != nullptr;
     stamp(sh, on, OPH_UPD);
-    const bool f = phase_factor(c, sh, mu, dw);
+    __syncthreads();
+    if (threadIdx.x == 0) sh.dc = dc;
+    __syncthreads();
+    const int f = phase_factor(c, sh, mu, dw);
     stamp(sh, on, OPH_FACTOR);
-    if (!f) return false;
-    if (sh.R) {  // soft dynamics rows (restoration phase)
+    if (f != F_OK) return f;
+    if (sh.R || dc > 0.0) {  // soft dynamics rows (restoration phase, delta_c)
         if (c.lds) {
             stage_soft_inputs(c, c.lds);
             __syncthreads();
@@ -2733,7 +2791,7 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
         }
         __syncthreads();
         stamp(sh, on, OPH_RIC_SOFT);
-        if (sh.flag) return false;
+        if (sh.flag) return sh.flag;
         if (c.lds) {
             stage_soft_forward(c, c.lds);
             __syncthreads();
@@ -2743,7 +2801,7 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
         }
         __syncthreads();
         stamp(sh, on, OPH_FWD_SOFT);
-        return true;
+        return F_OK;
     } else if (c.lds) {
         stage_inputs(c, c.lds);
         __syncthreads();
@@ -2752,19 +2810,19 @@ __device__ __noinline__ bool newton_solve(const Ctx& c, LShared& sh, double mu, 
         if (threadIdx.x < 64) riccati(c, sh, src);
         __syncthreads();
         stamp(sh, on, OPH_RIC);
-        if (sh.flag) return false;
+        if (sh.flag) return sh.flag;
         if (threadIdx.x < 64) forward(c, src, buf);
     } else {
         const GSrc src{c};
         if (threadIdx.x < 64) riccati(c, sh, src);
         __syncthreads();
         stamp(sh, on, OPH_RIC);
-        if (sh.flag) return false;
+        if (sh.flag) return sh.flag;
         if (threadIdx.x < 64) forward(c, src, buf);
     }
     __syncthreads();
     stamp(sh, on, OPH_FWD);
-    return true;
+    return F_OK;
 }
 
 // ================= IPOPT's iterative refinement (PDFullSpaceSolver; oracle/c/tt_obca.c:refined_solve) =================
@@ -2977,7 +3035,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan(), rs = sh.R != 0;
-    const double zeta = sh.zeta, dt = c.dt;
+    const double zeta = sh.zeta, dt = c.dt, dc = sh.dc;
     double rmax = 0.0, bmax = 0.0, snorm = 0.0, ap = 1.0, az = 1.0, Dm = 0.0, rel = 0.0;
     auto R = [&](double v) { rmax = fmax(rmax, fabs(v)); return v; };
     auto Bc = [&](double v) { bmax = fmax(bmax, fabs(v)); return v; };
@@ -3068,10 +3126,14 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                                       : (a.R[1] + a.R[2]) * du[0] + 2.0 * a.R[3] * du[1]);
                 ru[i] = R(t);
             }
-        // ---- dynamics rows of stage k: c_k + dx_k - A_{k-1} dx_{k-1} - B du_{k-1} (- dp + dn) ----
+        // ---- dynamics rows of stage k: c_k (+ delta_c y_k) + dx_k - A_{k-1} dx_{k-1} - B du_{k-1} (- dp + dn)
+        // (- delta_c y+_k) ----
         double rc[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) rc[i] = Bc(vw.S(S_CR + i, k)) + dx[i];
+        for (int i = 0; i < 6; ++i) {
+            const double cr = vw.S(S_CR + i, k);
+            rc[i] = Bc(dc > 0.0 ? fma(dc, (double)vw.S(S_YC + i, k), cr) : cr) + dx[i];
+        }
         if (k > 0) {
             double dxp[6], ajp[9];
 #pragma unroll
@@ -3114,6 +3176,9 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                 Dm += gp * dp + gn * dn;
                 rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
             }
+        if (dc > 0.0)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) rc[i] -= dc * yp[i];
 #pragma unroll
         for (int i = 0; i < 6; ++i) R(rc[i]);
         // ---- OBCA blocks ----
@@ -3227,7 +3292,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                 const double gs = c.hrl(r) ? mu * iu - mu * il : mu * iu;
                 const double sgr = c.hrl(r) ? vu[r] * iu + vl[r] * il : vu[r] * iu;
                 rsl[r] = R(Bc(gs) + (sgr + dw) * d - ydp[r]);
-                double t = Bc(dres[r]) - d;
+                double t = Bc(dc > 0.0 ? fma(dc, in.y[r], dres[r]) : dres[r]) - d;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) t += jx(bk, r, q) * dx[q];
 #pragma unroll
@@ -3249,6 +3314,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                     Dm += gp * dp + gn * dn;
                     rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
                 }
+                if (dc > 0.0) t -= dc * ydp[r];
                 rdv[r] = R(t);
                 Dm += gs * d;
                 rel = fmax(rel, fabs(d) * inv(1.0 + fabs(s)));
@@ -3295,7 +3361,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                 rx[i] += ypf;
                 const double sl = s - c.fL, su = c.fU - s;
                 const double gs = -mu / sl + mu / su;
-                double rf = Bc(sh.dfr[i]) + dx[i] - d;
+                double rf = Bc(dc > 0.0 ? fma(dc, sh.ydf[i], sh.dfr[i]) : sh.dfr[i]) + dx[i] - d;
                 const double rsf = R(Bc(gs) + (sh.vLf[i] / sl + sh.vUf[i] / su + dw) * d - ypf);
                 double gpn = 0.0;
                 if (rs) {
@@ -3313,6 +3379,7 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                     Dm += gp * dp + gn * dn;
                     rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
                 }
+                if (dc > 0.0) rf -= dc * ypf;
                 R(rf);
                 Dm += gs * d;
                 rel = fmax(rel, fabs(d) * inv(1.0 + fabs(s)));
@@ -3395,7 +3462,7 @@ __device__ __noinline__ void phase_stage_add(const Ctx& c, LShared& sh, double d
 // through the stored factorisation into buffer 2, its stage parts added into buffer buf (the blocks' parts: the
 // next phase_nres, NR_CORR)
 __device__ __noinline__ void correction_solve(const Ctx& c, LShared& sh, double mu, double dw, int buf) {
-    const bool soft = sh.R != 0, on = c.a->stamps != nullptr;
+    const bool soft = sh.R != 0 || sh.dc > 0.0, on = c.a->stamps != nullptr;
     if (c.lds) {
         stage_vec_inputs(c, c.lds, soft);
         __syncthreads();
@@ -3423,16 +3490,21 @@ __device__ __noinline__ void correction_solve(const Ctx& c, LShared& sh, double 
 
 // the step solve's recovery + IPOPT's iterative refinement for the step in buffer buf (factorisation, sweeps and
 // forward sweep done; the blocks' recovery is fused into the first residual pass).  rec: the line-search quantities
-// of the refined step (alpha_primal, alpha_dual, grad phi' d, max relative step), as phase_recover's
-__device__ __noinline__ void refine(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, double (&rec)[5]) {
+// of the refined step (alpha_primal, alpha_dual, grad phi' d, max relative step), as phase_recover's.
+// PDFullSpaceSolver::Solve: at least min_refinement_steps 1 correction; continue while the residual ratio
+// max|r| / (min(max|sol|, 1e6) + max|rhs|) exceeds residual_ratio_max 1e-10; give up ("quit", returned true) after more
+// than one correction when the ratio did not improve (residual_improvement_factor 1) or after max_refinement_steps 10.
+// *ratio: the final residual ratio (the caller's pretend-singular test, oracle/c/tt_obca.c: pd_solve).
+__device__ __noinline__ bool refine(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, double (&rec)[5],
+                                    double* ratio_out) {
     const bool on = c.a->stamps != nullptr;
     double q[7];
     phase_nres(c, sh, mu, dw, tau, buf, true, NR_MAIN, q);
     stamp(sh, on, OPH_REC);
-    double res = q[0];
     const double bnorm = q[1];
-    for (int it = 0; it < 10; ++it) {
-        if (it >= 1 && res <= 1e-10 * (fmin(q[2], 1e6) + bnorm)) break;
+    double ratio = q[0] / (fmin(q[2], 1e6) + bnorm);
+    bool quit = false;
+    for (int it = 0; !quit && (it < 1 || ratio > 1e-10); ++it) {
         // one correction is the rule (the oracle's census: > 99.9 % of the solves), so the check after it runs
         // without the correction's right-hand side; a second correction re-runs the residual pass with it
         if (it >= 1) phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
@@ -3440,12 +3512,14 @@ __device__ __noinline__ void refine(const Ctx& c, LShared& sh, double mu, double
         correction_solve(c, sh, mu, dw, buf);
         phase_nres(c, sh, mu, dw, tau, buf, false, NR_CORR, q);
         stamp(sh, on, OPH_REF_REC);
-        const double res2 = q[0];
-        if (!(res2 < res)) { res = res2; break; }  // no improvement: IPOPT stops refining
-        res = res2;
+        const double ratio2 = q[0] / (fmin(q[2], 1e6) + bnorm);
+        if (ratio2 > 1e-10 && it + 1 > 1 && (it + 1 > 10 || ratio2 > ratio)) quit = true;
+        ratio = ratio2;
     }
     __syncthreads();
     rec[0] = q[3]; rec[1] = q[4]; rec[2] = q[5]; rec[3] = q[6];
+    *ratio_out = ratio;
+    return quit;
 }
 
 // ======== restoration / soft-restoration / acceptable-point bookkeeping (all stage-parallel) ========
@@ -3723,7 +3797,7 @@ __device__ __noinline__ void ls_multipliers(const Ctx& c, LShared& sh) {
     phase_lin(c, sh, red);  // Jacobians at the iterate (y = 0: no curvature terms)
     phase_resid(c, sh, true);
     __syncthreads();
-    if (newton_solve(c, sh, 0.0, 0.0, 0)) {
+    if (newton_solve(c, sh, 0.0, 0.0, 0.0, 0) == F_OK) {
         double rec[5];
         phase_recover(c, sh, 0.0, 0.0, 0.99, 0, rec);
         if (isfinite(rec[4]) && rec[4] <= CONSTR_MULT_INIT_MAX) {
@@ -3744,10 +3818,120 @@ __device__ __noinline__ void ls_multipliers(const Ctx& c, LShared& sh) {
     __syncthreads();
 }
 
-struct IpmState {
-    double mu, tau, th_max, th_min, dw_last;
-    int acc;
+// IPOPT's PDPerturbationHandler, restated (oracle/c/tt_obca.c: ph_new / ph_singular / ph_inertia, which cite the
+// options): delta_x (= delta_s) on the Hessian, delta_c (= delta_d) on the constraint rows, the structural degeneracy
+// test of the first singular matrices (degen_iters_max 3).  Every thread carries the same (uniform) state.
+struct Perturb {
+    enum { UNDET = -1, NOT = 0, DEG = 1 };
+    enum { T_NONE = 0, T_C0X0, T_CPX0, T_C0XP, T_CPXP };
+    int hess, jac, degen, test, gdwi;
+    double dx, dx_last, dc;
+    __device__ void reset() {
+        hess = jac = UNDET;
+        degen = 0;
+        test = T_NONE;
+        gdwi = 0;
+        dx = dx_last = dc = 0.0;
+    }
+    __device__ static double dcd(double mu) { return 1e-8 * pow(mu, 0.25); }
+    __device__ void finalize() {
+        if (test == T_C0X0) {
+            if (hess == UNDET && jac == UNDET) { hess = NOT; jac = NOT; }
+            else if (hess == UNDET) hess = NOT;
+            else if (jac == UNDET) jac = NOT;
+        } else if (test == T_CPX0) {
+            if (hess == UNDET) hess = NOT;
+            if (jac == UNDET && ++degen >= 3) jac = DEG;
+        } else if (test == T_C0XP) {
+            if (jac == UNDET) jac = NOT;
+            if (hess == UNDET && ++degen >= 3) hess = DEG;
+        } else if (test == T_CPXP) {
+            if (++degen >= 3) { hess = DEG; jac = DEG; }
+        }
+    }
+    // get_deltas_for_wrong_inertia: false once delta_x would exceed max_hessian_perturbation 1e20
+    __device__ bool wrong_inertia_deltas() {
+        if (dx == 0.0) dx = dx_last == 0.0 ? 1e-4 : fmax(1e-20, dx_last / 3.0);
+        else dx *= (dx_last == 0.0 || 1e5 * dx_last < dx) ? 100.0 : 8.0;
+        if (dx > 1e20) { dx_last = 0.0; return false; }
+        gdwi = 1;
+        return true;
+    }
+    __device__ bool consider_new(double mu) {  // ConsiderNewSystem
+        finalize();
+        if (dx > 0.0) dx_last = dx;
+        test = (hess == UNDET || jac == UNDET) ? T_C0X0 : T_NONE;
+        dc = jac == DEG ? dcd(mu) : 0.0;
+        dx = 0.0;
+        if (hess == DEG && !wrong_inertia_deltas()) return false;
+        gdwi = 0;
+        return true;
+    }
+    __device__ bool singular(double mu) {  // PerturbForSingularity
+        if (hess == UNDET || jac == UNDET) {
+            if (test == T_C0X0) {
+                if (jac == UNDET) { dc = dcd(mu); test = T_CPX0; }
+                else { if (!wrong_inertia_deltas()) return false; test = T_C0XP; }
+            } else if (test == T_CPX0) {
+                dc = 0.0;
+                if (!wrong_inertia_deltas()) return false;
+                test = T_C0XP;
+            } else if (test == T_C0XP) {
+                dc = dcd(mu);
+                if (!wrong_inertia_deltas()) return false;
+                test = T_CPXP;
+            } else {
+                if (!wrong_inertia_deltas()) return false;
+            }
+        } else if (dc > 0.0 || gdwi) {
+            if (!wrong_inertia_deltas()) return false;
+        } else {
+            dc = dcd(mu);
+        }
+        return true;
+    }
+    __device__ bool inertia(double mu) {  // PerturbForWrongInertia
+        finalize();
+        if (wrong_inertia_deltas()) return true;
+        if (dc != 0.0) return false;
+        dc = dcd(mu);  // delta_x gave up without delta_c: again with the constraint rows regularised
+        dx = 0.0;
+        test = T_NONE;
+        if (hess == DEG) hess = NOT;
+        return wrong_inertia_deltas();
+    }
 };
+
+struct IpmState {
+    double mu, tau, th_max, th_min;
+    int acc;
+    Perturb ph;  // one handler per NLP (original / restoration), as IPOPT's restoration algorithm has its own
+};
+
+// factorisations until the inertia is right (PDFullSpaceSolver::SolveOnce); false when the perturbation gave up
+__device__ __forceinline__ bool factor_loop(const Ctx& c, LShared& sh, Perturb& ph, double mu, int buf) {
+#pragma unroll 1
+    for (int attempt = 0; attempt < 64; ++attempt) {
+        const int f = newton_solve(c, sh, mu, ph.dx, ph.dc, buf);
+        if (f == F_OK) return true;
+        if (!(f == F_MANY ? ph.inertia(mu) : ph.singular(mu))) return false;
+    }
+    return false;
+}
+
+// one step solve (factorisation current) + refinement with IPOPT's pretend-singular safeguard: a refinement that gives
+// up above residual_ratio_singular 1e-5 makes the handler treat the matrix as singular once (refactorisation, solve
+// again).  false when the perturbation gave up.  rec: refine()'s line-search quantities.
+__device__ __forceinline__ bool pd_solve(const Ctx& c, LShared& sh, Perturb& ph, double mu, double tau, int buf,
+                                         double (&rec)[5]) {
+    double ratio = 0.0;
+    const bool quit = refine(c, sh, mu, ph.dx, tau, buf, rec, &ratio);
+    if (!quit || ratio < 1e-5) return true;
+    if (!ph.singular(mu)) return false;
+    if (!factor_loop(c, sh, ph, mu, buf)) return false;
+    refine(c, sh, mu, ph.dx, tau, buf, rec, &ratio);
+    return true;
+}
 
 // ---------------- the kernel ----------------
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void obca_kernel(ObcaArgs args) {
@@ -3920,7 +4104,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         const bool use_lsq = !(a.opts & OBCA_OPT_NO_LSQ_MULT);
         if (use_lsq) ls_multipliers(cs, sh);
         IpmState S0, S1;
-        S0.mu = 0.1; S0.tau = fmax(0.99, 1.0 - 0.1); S0.th_max = S0.th_min = 0.0; S0.dw_last = 0.0; S0.acc = 0;
+        S0.mu = 0.1; S0.tau = fmax(0.99, 1.0 - 0.1); S0.th_max = S0.th_min = 0.0; S0.acc = 0;
+        S0.ph.reset();
         S1 = S0;
         int in_soft = 0, soft_cnt = 0, first_resto = 0, resto_iter0 = 0, have_acc = 0;
         double th_resto0 = 0.0;
@@ -4013,28 +4198,22 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 const double th0 = red[5], phi0 = red[6] - mu * red[7];
                 // the Newton right-hand side's residual rows (S_CR / B_DR / dfr) were stored by phase_lin at this
                 // iterate: the same expressions as phase_resid's
-                // ---- Newton step with inertia correction (IPOPT delta_w schedule) ----
-                double dw = 0.0;
-                bool ok = false;
-                for (int attempt = 0; attempt < 40; ++attempt) {
-                    if (newton_solve(cs, sh, mu, dw, 0)) { ok = true; break; }
-                    dw = (dw == 0.0) ? (stt.dw_last == 0.0 ? 1e-4 : fmax(1e-20, stt.dw_last / 3.0))
-                                     : (stt.dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-                    if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
+                // ---- Newton step with inertia correction (IPOPT's perturbation handler) ----
+                double rec[5];
+                bool ok = stt.ph.consider_new(mu) && factor_loop(cs, sh, stt.ph, mu, 0);
+                if (ok) {
+                    if (cs.refine) {
+                        ok = pd_solve(cs, sh, stt.ph, mu, stt.tau, 0, rec);
+                    } else {
+                        phase_recover(cs, sh, mu, stt.ph.dx, stt.tau, 0, rec);
+                        stamp(sh, ston, OPH_REC);
+                    }
                 }
                 bool go_resto = false;
                 if (!ok) {
                     if (R || !use_resto) { status = 5; done = true; break; } /* Error_In_Step_Computation */
                     go_resto = true;                                         /* IPOPT's fallback: restoration */
                 } else {
-                    if (dw > 0) stt.dw_last = dw;
-                    double rec[5];
-                    if (cs.refine) {
-                        refine(cs, sh, mu, dw, stt.tau, 0, rec);
-                    } else {
-                        phase_recover(cs, sh, mu, dw, stt.tau, 0, rec);
-                        stamp(sh, ston, OPH_REC);
-                    }
                     const double ap = rec[0], Dm = rec[2], rel = rec[3];
                     double az = rec[1], alpha = ap;
                     int buf = 0;
@@ -4076,12 +4255,13 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                                     th_old = th_t;
                                     phase_soc_resid(cs, sh, a_soc);
                                     __syncthreads();
-                                    if (!newton_solve(cs, sh, mu, dw, 1)) break;
+                                    // the same matrix (iterate and perturbations) with the SOC right-hand side
+                                    if (newton_solve(cs, sh, mu, stt.ph.dx, stt.ph.dc, 1) != F_OK) break;
                                     double rs[5];
                                     if (cs.refine) {
-                                        refine(cs, sh, mu, dw, stt.tau, 1, rs);
+                                        if (!pd_solve(cs, sh, stt.ph, mu, stt.tau, 1, rs)) break;
                                     } else {
-                                        phase_recover(cs, sh, mu, dw, stt.tau, 1, rs);
+                                        phase_recover(cs, sh, mu, stt.ph.dx, stt.tau, 1, rs);
                                         stamp(sh, ston, OPH_REC);
                                     }
                                     a_soc = rs[0];
@@ -4187,7 +4367,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     phase_enter_resto(cs, sh, muR);
                     if (use_lsq) ls_multipliers(cs, sh);
                     S0 = stt;
-                    S1.mu = muR; S1.tau = fmax(0.99, 1.0 - muR); S1.th_max = S1.th_min = 0.0; S1.dw_last = 0.0; S1.acc = 0;
+                    S1.mu = muR; S1.tau = fmax(0.99, 1.0 - muR); S1.th_max = S1.th_min = 0.0; S1.acc = 0;
+                    S1.ph.reset();
                     if (tid == 0) sh.nfl[1] = 0;
                     __syncthreads();
                     first_resto = 1;

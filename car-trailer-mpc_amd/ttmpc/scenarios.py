@@ -370,8 +370,11 @@ def mpc_obs_batch(state_traj, input_traj, B: int, horizon: int, seed: int = 0, d
             x0[b] = np.clip(Xr[:, 0] + pert, lo, hi)
             if obstacles is None or sat_gap(x0[b, :4], PARAMS, obstacles).min() >= min_gap:
                 break
-        else:  # every redraw too close: fall back to the window's own (plan) start and say so
+        else:  # every redraw too close: fall back to the window's own (plan) start, which must itself keep the gap
             x0[b] = np.clip(Xr[:, 0], lo, hi)
+            if sat_gap(x0[b, :4], PARAMS, obstacles).min() < min_gap:
+                raise ValueError(f"mpc_obs_batch: instance {b}: neither 1000 perturbed draws nor the window's own start "
+                                 f"keep the gap {min_gap} to the obstacles (the NLP would be infeasible)")
             import warnings
             warnings.warn(f"mpc_obs_batch: instance {b}: no perturbed start at >= {min_gap} from the obstacles in "
                           "1000 draws; using the unperturbed window start", RuntimeWarning, stacklevel=2)

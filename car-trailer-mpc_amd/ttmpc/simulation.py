@@ -248,11 +248,21 @@ class ClosedLoop:
         # the buffers were allocated and filled on the current stream; step() works on self.stream
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))
 
+    def _check_noise(self, noise, shape):
+        """noise must be a float64 tensor of exactly `shape` on the loop's device (the kernels index it as such)."""
+        if not (isinstance(noise, torch.Tensor) and noise.dtype == torch.float64 and noise.device == self.dev and
+                tuple(noise.shape) == tuple(shape)):
+            got = (tuple(noise.shape), noise.dtype, noise.device) if isinstance(noise, torch.Tensor) else type(noise)
+            raise ValueError(f"noise must be a float64 tensor of shape {tuple(shape)} on {self.dev}, got {got}")
+
     def step(self, k, noise=None):
-        """Enqueue one closed-loop step at window index k (noise: (B,6) device tensor or None: the measurement
-        noise, or with noise_in_plant the plant's process noise before its dt factor)."""
+        """Enqueue one closed-loop step at window index k (noise: (B,6) float64 device tensor or None: the measurement
+        noise, or with noise_in_plant -- the default of the "nmpc" / "fuzzy" policies -- the plant's process noise
+        before its dt factor)."""
         L, s, B, N = lib(), self.stream, self.B, self.N
         sp = C.c_void_p(s.cuda_stream)
+        if noise is not None:
+            self._check_noise(noise, (B, 6))
         with torch.cuda.stream(s):
             if (self.measurement_noise or self.noise_in_plant) and noise is None and self.dist is not None:
                 noise = torch.randn((B, 6), generator=self.gen, dtype=torch.float64, device=self.dev)
@@ -290,6 +300,7 @@ class ClosedLoop:
         p = plant(self.params, self.dist)
         sn = None
         if state_noise is not None:
+            self._check_noise(state_noise, (self.B, 6))
             state_noise = state_noise.contiguous()
             self._sn = state_noise    # keep it alive until the stream has consumed it
             sn = state_noise.data_ptr()
@@ -381,7 +392,10 @@ class ClosedLoop:
                 noise_all = torch.randn((K, B, 6), generator=self.gen, dtype=torch.float64, device=d)
                 noise_all.mul_(float(self.dist.get("process_noise_std", 0.0)))
             else:
-                noise_all = _dev(np.asarray(noise, dtype=np.float64).reshape(K, B, 6), d)
+                arr = noise if isinstance(noise, torch.Tensor) else np.asarray(noise, dtype=np.float64)
+                if tuple(arr.shape) != (K, B, 6):
+                    raise ValueError(f"noise must have shape (steps, B, 6) = {(K, B, 6)}, got {tuple(arr.shape)}")
+                noise_all = _dev(arr, d)
         logs = (torch.empty((K + 1, B, 6), dtype=torch.float64, device=d),
                 torch.empty((K, B, 2), dtype=torch.float64, device=d),
                 torch.zeros((K, B), dtype=torch.int32, device=d), torch.zeros((K, B), dtype=torch.int32, device=d),
@@ -437,6 +451,8 @@ class ClosedLoop:
             Sa = torch.empty((K, B), dtype=torch.int32, device=self.dev)
             S[0].copy_(self.state)
         nz = None if noise is None else _dev(noise, self.dev)
+        if nz is not None and tuple(nz.shape) != (K, B, 6):
+            raise ValueError(f"noise must have shape (steps, B, 6) = {(K, B, 6)}, got {tuple(nz.shape)}")
         for j, k in enumerate(ks):
             self.step(k, None if nz is None else nz[j])
             if record:

@@ -83,6 +83,13 @@ typedef struct {
 
 enum { M_ORIG = 0, M_RESTO = 1 };
 
+/* IPOPT's PDPerturbationHandler state (see ph_new below): degeneracy flags, test status, current / last deltas */
+typedef struct {
+    int hess, jac, degen, test, gdwi;
+    double dx_curr, dx_last, dc_curr, dc_last;
+} perturb_t;
+static void ph_reset(perturb_t* H);
+
 typedef struct {
     const tto_obca_problem* P;
     int N, M, nbk, nb, n, mode;
@@ -140,7 +147,9 @@ typedef struct {
     double *ov, *ovx, *ovu, *ovw, *ovs, *ovsf, *ovp, *ovn;
     double *rsx, *rsu, *rsw, *rss, *rssf, *rsp, *rsn, *rrc, *rrd, *rrf; /* residuals of the un-condensed rows */
     double *sol;    /* refinement save area of the solution */
-    double dw_cur;
+    double dw_cur, dc_cur; /* the perturbations (delta_x = delta_s, delta_c = delta_d) of the current factorisation */
+    int soft;              /* soft dynamics rows: restoration phase (E = 1/D_p + 1/D_n) and/or delta_c > 0 (E += delta_c) */
+    double* csh;           /* the solve's row constants shifted by delta_c y (new-multiplier form of IPOPT's -delta_c dy) */
     int dbg;        /* diagnostics, read once per solve: 1 TTO_DEBUG, 2 TTO_DEBUG2, 4 TTO_CHECK */
     double* cc;     /* refinement row-residual constants */
     double* mem;
@@ -362,6 +371,7 @@ static int ws_init(ws_t* W, const tto_obca_problem* P) {
     TAKE(W->rsp, nr); TAKE(W->rsn, nr); TAKE(W->rrc, N1 * 6); TAKE(W->rrd, nb * 4); TAKE(W->rrf, 6);
     TAKE(W->sol, N1 * 12 + N * 2 + nb * 16 + 12 + 2 * nr);
     TAKE(W->cc, N1 * 6 + nb * 4 + 6);
+    TAKE(W->csh, N1 * 6 + nb * 4 + 6);
 #undef TAKE
     W->mem = (double*)calloc(tot, sizeof(double));
     if (!W->mem) return -1;
@@ -516,11 +526,15 @@ static double barrier(const ws_t* W, const double* x, const double* u, const dou
 }
 
 /* ------------------------------------------------------------------ small dense helpers */
-static int chol(double* a, int n) { /* in-place lower Cholesky, row-major n x n; 0 ok */
+/* in-place lower Cholesky, row-major n x n; 0 ok, F_MANY on a negative pivot (one negative eigenvalue too many),
+ * F_ZERO on a numerically zero pivot (|s| <= 1e-14 |a_jj|: the matrix is singular to round-off) */
+enum { F_OK = 0, F_MANY = 1, F_ZERO = 2, F_FEW = 3 };
+static int pivot_fail(double s, double ajj) { return s < -1e-14 * fabs(ajj) ? F_MANY : F_ZERO; }
+static int chol(double* a, int n) {
     for (int j = 0; j < n; ++j) {
         double s = a[j * n + j];
         for (int k = 0; k < j; ++k) s -= a[j * n + k] * a[j * n + k];
-        if (!(s > 0.0)) return -1;
+        if (!(s >= DBL_MIN)) return pivot_fail(s, a[j * n + j]); /* a subnormal pivot counts as zero */
         const double r = sqrt(s);
         a[j * n + j] = r;
         for (int i = j + 1; i < n; ++i) {
@@ -533,14 +547,18 @@ static int chol(double* a, int n) { /* in-place lower Cholesky, row-major n x n;
 }
 /* signed Cholesky A = L S L' (S = diag(+-1), L_jj = sqrt|d_j|), no pivoting; identical to chol() on a
  * positive definite matrix (IPOPT's inertia test needs the signs, not definiteness).  Returns the number of negative pivots, -1 on a (numerically) zero pivot. */
+/* TTO_CENSUS diagnostic counters (per solve): factorisations, block inertia failures by kind, zero pivots,
+ * refinements that stop above IPOPT's residual_ratio_singular 1e-5 */
+static _Thread_local long g_cen[8];
 static int schol(double* a, int n, double* S) {
     int neg = 0;
     for (int j = 0; j < n; ++j) {
         const double ajj = a[j * n + j];
         double s = ajj;
         for (int k = 0; k < j; ++k) s -= a[j * n + k] * a[j * n + k] * S[k];
-        /* a positive pivot is taken as chol() takes it; a negative one only when it is not numerically zero */
-        if (!(s > 0.0) && !(s < -1e-14 * fabs(ajj))) return -1;
+        /* a positive pivot is taken as chol() takes it (a subnormal one counts as zero, as there); a negative one only
+         * when it is not numerically zero */
+        if (!(s >= DBL_MIN) && !(s < -1e-14 * fabs(ajj))) return -1;
         S[j] = s > 0.0 ? 1.0 : -1.0;
         neg += s < 0.0;
         const double r = sqrt(fabs(s));
@@ -670,13 +688,13 @@ static void linearise(ws_t* W) {
  * A^-1 / T^-1 carries its sign vector.  That exact test is the default (the GPU kernel runs it too); TTO_OPT_PD_BLOCKS
  * switches back to round 2's sufficient condition A positive definite (S = I), which raises delta_w where IPOPT
  * would not. */
-static int block_factor(ws_t* W, int bi, double dw, double* Q) {
+static int block_factor(ws_t* W, int bi, double dw, double dc, double* Q) {
     const double *Jx = W->Jx + 16 * bi, *Jw = W->Jw + 32 * bi;
     double* D = W->Dd + 4 * bi;
     double* E = W->Ed + 4 * bi;
     for (int r = 0; r < 4; ++r) {
         D[r] = W->lsq ? 1.0 : sig_s(W, bi, r) + dw;
-        E[r] = 1.0 / D[r];
+        E[r] = 1.0 / D[r] + dc;
         if (W->R == M_RESTO) {
             const int ro = W->nrc + 4 * bi + r;
             E[r] += 1.0 / W->Dpr[ro] + 1.0 / W->Dnr[ro];
@@ -711,7 +729,7 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
                     for (int r = 0; r < 4; ++r) t += Jw[r * 8 + a] * Jw[r * 8 + b] / E[r];
                     Lb[a * 8 + b] = t;
                 }
-            if (chol(Lb, 8) != 0) return 1;
+            if (chol(Lb, 8) != 0) return F_MANY;
             W->alt[bi] = 1.0;
             double* Zb = W->V + 32 * bi;
             for (int q = 0; q < 4; ++q) {
@@ -735,9 +753,10 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
         }
     } else if (inert) {
         negA = schol(Lb, 8, SA);
-        if (negA < 0) return 1;
+        if (negA < 0) { ++g_cen[3]; return F_ZERO; }
     } else {
-        if (chol(Lb, 8) != 0) return 1;
+        const int f = chol(Lb, 8);
+        if (f != 0) return f;
         for (int e = 0; e < 8; ++e) SA[e] = 1.0;
     }
     double *Yb = W->Yb + 32 * bi, *Zb = W->V + 32 * bi, *LT = W->LT + 16 * bi, *Gm = W->Gm + 16 * bi;
@@ -766,11 +785,14 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
          * (IPOPT counts the negative eigenvalues of the whole KKT matrix): the block's surplus of negative
          * pivots negA - negT is summed with the Riccati's and must vanish overall */
         const int negT = schol(LT, 4, ST);
-        if (negT < 0) return 1;
+        if (negT < 0) { ++g_cen[3]; return F_ZERO; }
         if (W->P->opts & TTO_OPT_GLOBAL_INERTIA) W->negx += negA - negT;
-        else if (negT != negA) return 1;
+        /* negT > negA: the block has fewer negative eigenvalues than its 4 rows need (IPOPT's "too few negative
+         * eigenvalues", which it treats as a singular matrix); negT < negA: too many (negative curvature) */
+        else if (negT != negA) { ++g_cen[negT > negA ? 1 : 2]; return negT > negA ? F_FEW : F_MANY; }
     } else {
-        if (chol(LT, 4) != 0) return 1;
+        const int f = chol(LT, 4);
+        if (f != 0) return f;
         for (int r = 0; r < 4; ++r) ST[r] = 1.0;
     }
     /* Q += W_xx - Z'Z + G' T^-1 G   (T^-1 G via two triangular solves per column) */
@@ -796,7 +818,7 @@ static int block_factor(ws_t* W, int bi, double dw, double* Q) {
 static int soften(ws_t* W, int k) {
     const double* Pk = W->Pm + 36 * k;
     double* Pt = W->Ptl + 36 * k;
-    if (W->R != M_RESTO) { memcpy(Pt, Pk, 36 * sizeof(double)); return 0; }
+    if (!W->soft) { memcpy(Pt, Pk, 36 * sizeof(double)); return 0; }
     const double* S = W->Sd + 6 * k;
     double* Mk = W->Mch + 36 * k;
     for (int i = 0; i < 6; ++i)
@@ -806,10 +828,11 @@ static int soften(ws_t* W, int k) {
         /* the soft row pair [[P, -I], [-I, -E]] has inertia (6, 6) iff M > 0; each negative pivot of M is one
          * surplus negative eigenvalue of the KKT matrix */
         const int negM = schol(Mk, 6, Ms);
-        if (negM < 0) return 1;
+        if (negM < 0) return F_ZERO;
         W->negx += negM;
     } else {
-        if (chol(Mk, 6) != 0) return 1;
+        const int f = chol(Mk, 6);
+        if (f != 0) return f;
         for (int i = 0; i < 6; ++i) Ms[i] = 1.0;
     }
     /* X = M^-1 S P (column by column), P~ = P - (P S) X */
@@ -839,13 +862,21 @@ static void soft_apply(const ws_t* W, int k, const double* b, double* v) {
     for (int i = 0; i < 6; ++i) v[i] -= S[i] * t[i];
 }
 
-/* matrices: block eliminations, stage Hessians, Riccati factorisation.  0 = inertia ok */
-static int factor(ws_t* W, double dw) {
+/* matrices: block eliminations, stage Hessians, Riccati factorisation with the perturbations dw (delta_x = delta_s)
+ * and dc (delta_c = delta_d: -dc on the diagonal of every constraint row).  F_OK = inertia ok; F_MANY a negative
+ * pivot where IPOPT's (n, m, 0) wants a positive one (PerturbForWrongInertia); F_ZERO a numerically zero pivot or
+ * F_FEW too few negative eigenvalues (both PerturbForSingularity in IPOPT's PDFullSpaceSolver::SolveOnce, the second
+ * after IncreaseQuality fails -- there is no pivot tolerance to raise in this elimination) */
+static int factor(ws_t* W, double dw, double dc) {
     const tto_obca_problem* P = W->P;
     const int N = W->N;
     const double dt = P->dt;
-    int fail = 0;
+    int fz = 0, fm = 0, ff = 0;
     W->negx = 0;
+    W->dw_cur = dw;
+    W->dc_cur = dc;
+    W->soft = W->R == M_RESTO || dc > 0.0;
+    ++g_cen[0];
     if (W->R == M_RESTO)
         for (int i = 0; i < W->nrow; ++i) {
             W->Dpr[i] = W->lsq ? 1.0 : W->zp[i] / W->pr[i] + dw;
@@ -865,13 +896,14 @@ static int factor(ws_t* W, double dw) {
         }
         for (int j = 0; j < W->nbk; ++j) {
             const int bi = k * W->nbk + j;
-            if (block_factor(W, bi, dw, Q) != 0) fail = 1;
+            const int f = block_factor(W, bi, dw, dc, Q);
+            fm |= f == F_MANY; fz |= f == F_ZERO; ff |= f == F_FEW;
         }
         if (k == N && W->mode == TTO_OBCA_PLAN)
             for (int i = 0; i < 6; ++i) {
                 double s = W->lsq ? 1.0 : dw + W->vLf[i] / (W->sf[i] - W->fL) + W->vUf[i] / (W->fU - W->sf[i]);
                 W->Dsf[i] = s;
-                double E = 1.0 / s;
+                double E = 1.0 / s + dc;
                 if (W->R == M_RESTO) {
                     const int ro = W->nrc + W->nrd + i;
                     E += 1.0 / W->Dpr[ro] + 1.0 / W->Dnr[ro];
@@ -887,14 +919,17 @@ static int factor(ws_t* W, double dw) {
                 R[i * 2 + i] += sig_u(W, k, i) + dw + (W->R == M_RESTO ? W->zeta * W->dRu[2 * k + i] : 0.0);
         }
     }
-    if (fail) return 1;
-    if (W->R == M_RESTO)
-        for (int i = 0; i < W->nrc; ++i) W->Sd[i] = sqrt(1.0 / W->Dpr[i] + 1.0 / W->Dnr[i]);
+    if (fz | fm | ff) return fz ? F_ZERO : fm ? F_MANY : F_FEW;
+    ++g_cen[4]; /* blocks passed: the stage Riccati decides */
+    if (W->soft)
+        for (int i = 0; i < W->nrc; ++i)
+            W->Sd[i] = sqrt((W->R == M_RESTO ? 1.0 / W->Dpr[i] + 1.0 / W->Dnr[i] : 0.0) + dc);
     /* Riccati: P_N = Q~_N; G = R~ + B'P~B, H = B'P~A, K = -G^-1 H, P = Q~ + A'P~A + H'K  (P~ = P unless the
      * dynamics rows are soft) */
     memcpy(W->Pm + 36 * N, W->Qt + 36 * N, 36 * sizeof(double));
     for (int k = N; k >= 1; --k) {
-        if (soften(W, k) != 0) return 1;
+        const int fs = soften(W, k);
+        if (fs != 0) return fs;
         const double* Pn = W->Ptl + 36 * k;
         const double* A = W->A + 36 * (k - 1);
         const int kk = k - 1;
@@ -916,10 +951,11 @@ static int factor(ws_t* W, double dw) {
         if (P->opts & TTO_OPT_GLOBAL_INERTIA) {
             /* each negative pivot of the reduced input Hessian is one surplus negative eigenvalue */
             const int negG = schol(G, 2, Gs);
-            if (negG < 0) return 1;
+            if (negG < 0) return F_ZERO;
             W->negx += negG;
         } else {
-            if (chol(G, 2) != 0) return 1;
+            const int f = chol(G, 2);
+            if (f != 0) return f;
             Gs[0] = Gs[1] = 1.0;
         }
         double* Kk = W->K + 12 * kk;
@@ -947,8 +983,9 @@ static int factor(ws_t* W, double dw) {
         for (int i = 0; i < 6; ++i)
             for (int j = 0; j < i; ++j) Pk[i * 6 + j] = Pk[j * 6 + i] = 0.5 * (Pk[i * 6 + j] + Pk[j * 6 + i]);
     }
-    if (soften(W, 0) != 0) return 1;
-    return W->negx != 0; /* global inertia test: IPOPT's (n, m, 0) (W->negx stays 0 in the other modes) */
+    const int fs = soften(W, 0);
+    if (fs != 0) return fs;
+    return W->negx != 0 ? F_MANY : F_OK; /* global inertia test: IPOPT's (n, m, 0) (W->negx stays 0 in the other modes) */
 }
 
 /* right-hand side + back-substitution.  cres: dynamics residual rows ((N+1)*6), dres: OBCA residual rows
@@ -1023,7 +1060,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
     for (int k = N;; --k) {
         double* pt = W->ptl + 6 * k;
         memcpy(pt, W->pv + 6 * k, 6 * sizeof(double));
-        if (rs) {
+        if (W->soft) {
             double Pp[6];
             for (int i = 0; i < 6; ++i) Pp[i] = W->pv[6 * k + i];
             /* pt -= P S M^-1 S p  */
@@ -1064,7 +1101,7 @@ static void solve_rhs(ws_t* W, double mu, const double* cres, const double* dres
     for (int i = 0; i < 6; ++i) W->dx[i] = -W->rct[i];
     for (int k = 0; k <= N; ++k) {
         double* dxk = W->dx + 6 * k;
-        if (rs) {
+        if (W->soft) {
             double b[6];
             for (int i = 0; i < 6; ++i) {
                 double t = W->pv[6 * k + i];
@@ -1818,7 +1855,7 @@ static void ls_multipliers(ws_t* W) {
     double zero6[6] = {0};
     for (size_t i = 0; i < N1 * 6; ++i) W->cr[i] = 0.0;
     for (size_t i = 0; i < nb * 4; ++i) W->dr[i] = 0.0;
-    int ok = factor(W, 0.0) == 0;
+    int ok = factor(W, 0.0, 0.0) == F_OK;
     if (ok) {
         solve_rhs(W, 0.0, W->cr, W->dr, zero6);
         double m = 0.0;
@@ -1838,7 +1875,8 @@ static void ls_multipliers(ws_t* W) {
 
 /* ------------------------------------------------------------------ one barrier solve (original or restoration) */
 typedef struct {
-    double mu, tau, th_max, th_min, dw_last;
+    double mu, tau, th_max, th_min;
+    perturb_t ph;   /* one handler per NLP (original / restoration), as IPOPT's restoration algorithm has its own */
     int acc_count;
     filter_t F;
     /* watchdog (IPOPT BacktrackingLineSearch): shortened-step count, active flag, trials, reference point */
@@ -1850,7 +1888,7 @@ static void ipm_reset(ipm_state_t* S, double mu) {
     S->mu = mu;
     S->tau = fmax(0.99, 1.0 - mu);
     S->th_max = S->th_min = 0.0;
-    S->dw_last = 0.0;
+    ph_reset(&S->ph);
     S->acc_count = 0;
     S->F.n = 0;
     S->wd_short = S->wd_on = S->wd_trial = 0;
@@ -2065,6 +2103,7 @@ static double newton_resid(ws_t* W, double mu, const double* cres, const double*
                 for (int a = 0; a < 8; ++a) t += W->Jw[32 * bi + r * 8 + a] * W->dw[8 * bi + a];
                 t -= W->ds[v];
                 if (rs) t += -W->dpr[ro] + W->dnr[ro];
+                t -= W->dc_cur * W->ydp[v];
                 W->rrd[v] = t;
                 rmax = fmax(rmax, fabs(t));
             }
@@ -2078,6 +2117,7 @@ static double newton_resid(ws_t* W, double mu, const double* cres, const double*
                 if (i == 4) t -= P->dt * W->du[2 * (k - 1) + 1];
             }
             if (rs) t += -W->dpr[v] + W->dnr[v];
+            t -= W->dc_cur * W->ycp[v];
             W->rrc[v] = t;
             rmax = fmax(rmax, fabs(t));
         }
@@ -2087,6 +2127,7 @@ static double newton_resid(ws_t* W, double mu, const double* cres, const double*
             const int ro = W->nrc + W->nrd + i;
             double t = CST(fres[i]) + W->dx[6 * N + i] - W->dsf[i];
             if (rs) t += -W->dpr[ro] + W->dnr[ro];
+            t -= W->dc_cur * W->ydpf[i];
             W->rrf[i] = t;
             rmax = fmax(rmax, fabs(t));
             t = CST(W->ov ? W->ovsf[i] : bgrad_sf(W, i, mu));
@@ -2111,22 +2152,42 @@ static double newton_resid(ws_t* W, double mu, const double* cres, const double*
     return rmax;
 }
 
-/* the step solve with IPOPT's iterative refinement on the un-condensed system (min_refinement_steps 1,
- * max_refinement_steps 10, residual_ratio_max 1e-10): correction solves reuse the factorisation with the
- * residuals as constants (default; TTO_OPT_NO_REFINE switches it off) */
-static void refined_solve(ws_t* W, double mu, double* cres, double* dres, double* fres) {
-    solve_rhs(W, mu, cres, dres, fres);
-    if ((W->P->opts & TTO_OPT_NO_REFINE) || W->lsq) return;
+/* the solution norm and the residual ratio of IPOPT's PDFullSpaceSolver::ComputeResidualRatio:
+ * max|resid| / (min(max|sol|, 1e6) + max|rhs|) */
+static double resid_ratio(const ws_t* W, double res, double bnorm) {
+    const size_t N1 = (size_t)W->N + 1, nb = (size_t)W->nb;
+    double snorm = 0.0;
+    for (size_t i = 0; i < N1 * 6; ++i) snorm = fmax(snorm, fmax(fabs(W->dx[i]), fabs(W->ycp[i])));
+    for (size_t i = 0; i < nb * 8; ++i) snorm = fmax(snorm, fabs(W->dw[i]));
+    return res / (fmin(snorm, 1e6) + bnorm);
+}
+
+/* the step solve with IPOPT's iterative refinement on the un-condensed system (PDFullSpaceSolver::Solve:
+ * min_refinement_steps 1, max_refinement_steps 10, residual_ratio_max 1e-10, residual_improvement_factor 1):
+ * correction solves reuse the factorisation with the residuals as constants (TTO_OPT_NO_REFINE switches it off).
+ * With delta_c > 0 the row constants are shifted by delta_c y (IPOPT perturbs dy; the unknowns here are y+ = y + dy).
+ * Returns 1 when the refinement quit (IPOPT's "iterative refinement failed"), with the final residual ratio. */
+static int refined_solve(ws_t* W, double mu, double* cres, double* dres, double* fres, double* ratio_out) {
     const int N = W->N, rs = W->R == M_RESTO;
     const size_t N1 = (size_t)N + 1, nb = (size_t)W->nb, nr = (size_t)W->nrow;
+    *ratio_out = 0.0;
+    if (W->dc_cur > 0.0 && !W->lsq) {
+        double* c = W->csh;
+        for (size_t i = 0; i < N1 * 6; ++i) c[i] = cres[i] + W->dc_cur * W->yc[i];
+        for (size_t i = 0; i < nb * 4; ++i) c[N1 * 6 + i] = dres[i] + W->dc_cur * W->yd[i];
+        for (int i = 0; i < 6; ++i) c[N1 * 6 + nb * 4 + i] = fres[i] + (W->mode == TTO_OBCA_PLAN ? W->dc_cur * W->ydf[i] : 0.0);
+        cres = c; dres = c + N1 * 6; fres = c + N1 * 6 + nb * 4;
+    }
+    solve_rhs(W, mu, cres, dres, fres);
+    if ((W->P->opts & TTO_OPT_NO_REFINE) || W->lsq) return 0;
+    const int r3 = (W->P->opts & TTO_OPT_R3_PERTURB) != 0;
     double bnorm = 0.0;
     double res = newton_resid(W, mu, cres, dres, fres, &bnorm);
+    double ratio = resid_ratio(W, res, bnorm);
     double* cc = W->cc;
-    for (int it = 0; it < 10; ++it) {
-        double snorm = 0.0;
-        for (size_t i = 0; i < N1 * 6; ++i) snorm = fmax(snorm, fmax(fabs(W->dx[i]), fabs(W->ycp[i])));
-        for (size_t i = 0; i < nb * 8; ++i) snorm = fmax(snorm, fabs(W->dw[i]));
-        if (it >= 1 && res <= 1e-10 * (fmin(snorm, 1e6) + bnorm)) break;
+    int quit = 0;
+    for (int it = 0; !quit && (it < 1 || ratio > 1e-10); ++it) {
+        if (r3 && it >= 10) break;
         /* save the solution, solve for the correction with the residuals as constants, add */
         double* o = W->sol;
         memcpy(o, W->dx, N1 * 48); o += N1 * 6; memcpy(o, W->ycp, N1 * 48); o += N1 * 6;
@@ -2148,31 +2209,177 @@ static void refined_solve(ws_t* W, double mu, double* cres, double* dres, double
         if (rs) { ADD(W->dpr, nr); ADD(W->dnr, nr); }
 #undef ADD
         const double res2 = newton_resid(W, mu, cres, dres, fres, NULL);
-        if (!(res2 < res)) { /* no improvement: IPOPT stops refining (residual_improvement_factor 1) */
+        const double ratio2 = resid_ratio(W, res2, bnorm);
+        if (r3) {
+            /* round 3: raw residuals, stop on the first non-improvement or when the ratio test passes */
+            const int stop = !(res2 < res);
             res = res2;
+            ratio = ratio2;
+            if (stop) break;
+            if (ratio <= 1e-10) break;
+            continue;
+        }
+        /* IPOPT gives up when the ratio is still above residual_ratio_max after more than min_refinement_steps
+         * corrections and either max_refinement_steps is exceeded or the ratio did not improve */
+        if (ratio2 > 1e-10 && it + 1 > 1 && (it + 1 > 10 || ratio2 > ratio)) quit = 1;
+        res = res2;
+        ratio = ratio2;
+    }
+    if (ratio > 1e-10) ++g_cen[5];
+    if (ratio > 1e-5) ++g_cen[6];
+    *ratio_out = ratio;
+    return quit;
+}
+
+/* ---------------- IPOPT's PDPerturbationHandler (restated) ----------------
+ * delta_x (= delta_s) regularises the Hessian, delta_c (= delta_d) the constraint rows.  Each new matrix starts from
+ * ConsiderNewSystem; a singular factorisation (or too few negative eigenvalues, IncreaseQuality being unavailable)
+ * goes to PerturbForSingularity, a wrong inertia to PerturbForWrongInertia.  The Hessian / Jacobian structural
+ * degeneracy flags are determined in the first iterations whose unperturbed matrix is singular (degen_iters_max 3);
+ * a structurally degenerate Jacobian gets delta_c = 1e-8 mu^0.25 on every matrix, a degenerate Hessian starts from the
+ * decreased last delta_x instead of 0.  Options are IPOPT's defaults: first_hessian_perturbation 1e-4,
+ * perturb_inc_fact_first 100, perturb_inc_fact 8, perturb_dec_fact 1/3, min/max_hessian_perturbation 1e-20 / 1e20,
+ * jacobian_regularization_value 1e-8, jacobian_regularization_exponent 0.25, perturb_always_cd no. */
+enum { PH_UNDET = -1, PH_NOT = 0, PH_DEG = 1 };
+enum { PT_NONE = 0, PT_C0X0, PT_CPX0, PT_C0XP, PT_CPXP };
+static void ph_reset(perturb_t* H) {
+    H->hess = H->jac = PH_UNDET;
+    H->degen = 0;
+    H->test = PT_NONE;
+    H->gdwi = 0;
+    H->dx_curr = H->dx_last = H->dc_curr = H->dc_last = 0.0;
+}
+static double ph_dcd(double mu) { return 1e-8 * pow(mu, 0.25); }
+static void ph_finalize(perturb_t* H) {
+    switch (H->test) {
+    case PT_C0X0:
+        if (H->hess == PH_UNDET && H->jac == PH_UNDET) { H->hess = PH_NOT; H->jac = PH_NOT; }
+        else if (H->hess == PH_UNDET) H->hess = PH_NOT;
+        else if (H->jac == PH_UNDET) H->jac = PH_NOT;
+        break;
+    case PT_CPX0:
+        if (H->hess == PH_UNDET) H->hess = PH_NOT;
+        if (H->jac == PH_UNDET && ++H->degen >= 3) H->jac = PH_DEG;
+        break;
+    case PT_C0XP:
+        if (H->jac == PH_UNDET) H->jac = PH_NOT;
+        if (H->hess == PH_UNDET && ++H->degen >= 3) H->hess = PH_DEG;
+        break;
+    case PT_CPXP:
+        if (++H->degen >= 3) { H->hess = PH_DEG; H->jac = PH_DEG; }
+        break;
+    default:
+        break;
+    }
+}
+/* get_deltas_for_wrong_inertia: 0 when delta_x would exceed max_hessian_perturbation */
+static int ph_gdwi(perturb_t* H) {
+    if (H->dx_curr == 0.0) H->dx_curr = H->dx_last == 0.0 ? 1e-4 : fmax(1e-20, H->dx_last / 3.0);
+    else H->dx_curr *= (H->dx_last == 0.0 || 1e5 * H->dx_last < H->dx_curr) ? 100.0 : 8.0;
+    if (H->dx_curr > 1e20) { H->dx_last = 0.0; return 0; }
+    H->gdwi = 1;
+    return 1;
+}
+static int ph_new(perturb_t* H, double mu) {
+    ph_finalize(H);
+    if (H->dx_curr > 0.0) H->dx_last = H->dx_curr;
+    if (H->dc_curr > 0.0) H->dc_last = H->dc_curr;
+    H->test = (H->hess == PH_UNDET || H->jac == PH_UNDET) ? PT_C0X0 : PT_NONE;
+    H->dc_curr = H->jac == PH_DEG ? ph_dcd(mu) : 0.0;
+    H->dx_curr = 0.0;
+    if (H->hess == PH_DEG && !ph_gdwi(H)) return 0;
+    H->gdwi = 0;
+    return 1;
+}
+static int ph_singular(perturb_t* H, double mu) {
+    if (H->hess == PH_UNDET || H->jac == PH_UNDET) {
+        switch (H->test) {
+        case PT_C0X0:
+            if (H->jac == PH_UNDET) { H->dc_curr = ph_dcd(mu); H->test = PT_CPX0; }
+            else { if (!ph_gdwi(H)) return 0; H->test = PT_C0XP; }
+            break;
+        case PT_CPX0:
+            H->dc_curr = 0.0;
+            if (!ph_gdwi(H)) return 0;
+            H->test = PT_C0XP;
+            break;
+        case PT_C0XP:
+            H->dc_curr = ph_dcd(mu);
+            if (!ph_gdwi(H)) return 0;
+            H->test = PT_CPXP;
+            break;
+        default:
+            if (!ph_gdwi(H)) return 0;
             break;
         }
-        res = res2;
+    } else if (H->dc_curr > 0.0 || H->gdwi) {
+        if (!ph_gdwi(H)) return 0;
+    } else {
+        H->dc_curr = ph_dcd(mu);
     }
+    return 1;
+}
+static int ph_inertia(perturb_t* H, double mu) {
+    ph_finalize(H);
+    if (ph_gdwi(H)) return 1;
+    if (H->dc_curr != 0.0) return 0;
+    /* delta_x gave up without delta_c: try again with the constraint rows regularised */
+    H->dc_curr = ph_dcd(mu);
+    H->dx_curr = 0.0;
+    H->test = PT_NONE;
+    if (H->hess == PH_DEG) H->hess = PH_NOT;
+    return ph_gdwi(H);
+}
+/* round 3's schedule (TTO_OPT_R3_PERTURB, A/B only): delta_x from 0 on every matrix, no delta_c */
+static int ph_r3(perturb_t* H) {
+    const double dw = H->dx_curr;
+    H->dx_curr = dw == 0.0 ? (H->dx_last == 0.0 ? 1e-4 : fmax(1e-20, H->dx_last / 3.0))
+                           : (H->dx_last == 0.0 ? 100.0 * dw : 8.0 * dw);
+    return H->dx_curr <= 1e20;
+}
+
+/* factorisations until the inertia is right (PDFullSpaceSolver::SolveOnce); 0 when the perturbation gave up */
+static int factor_loop(ws_t* W, ipm_state_t* S) {
+    perturb_t* H = &S->ph;
+    const int r3 = (W->P->opts & TTO_OPT_R3_PERTURB) != 0;
+    for (int attempt = 0; attempt < 64; ++attempt) {
+        const int f = factor(W, H->dx_curr, H->dc_curr);
+        if (f == F_OK) return 1;
+        const int ok = r3 ? ph_r3(H) : (f == F_MANY ? ph_inertia(H, S->mu) : ph_singular(H, S->mu));
+        if (!ok) return 0;
+    }
+    return 0;
+}
+
+/* one linear solve of the current matrix with IPOPT's safeguards (PDFullSpaceSolver::Solve): refinement, and when it
+ * fails with a residual ratio above residual_ratio_singular 1e-5 the matrix is treated as singular once
+ * (pretend_singular: PerturbForSingularity, refactorisation, solve again).  0 when the perturbation gave up. */
+static int pd_solve(ws_t* W, ipm_state_t* S, double* cres, double* dres, double* fres) {
+    double ratio = 0.0;
+    const int quit = refined_solve(W, S->mu, cres, dres, fres, &ratio);
+    if (!quit || (W->P->opts & TTO_OPT_R3_PERTURB) || ratio < 1e-5) return 1;
+    ++g_cen[7];
+    if (!ph_singular(&S->ph, S->mu)) return 0;
+    if (!factor_loop(W, S)) return 0;
+    refined_solve(W, S->mu, cres, dres, fres, &ratio);
+    return 1;
 }
 
 /* Newton step with inertia correction into dx..; 0 on success */
 static int newton(ws_t* W, ipm_state_t* S, double* dw_out) {
-    double dw = 0.0;
-    int ok = 0;
-    for (int attempt = 0; attempt < 40; ++attempt) {
-        if (factor(W, dw) == 0) { ok = 1; break; }
-        dw = (dw == 0.0) ? (S->dw_last == 0.0 ? 1e-4 : fmax(1e-20, S->dw_last / 3.0)) : (S->dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);
-        if (dw > 1e20) break; /* IPOPT max_hessian_perturbation 1e20 */
+    perturb_t* H = &S->ph;
+    if (W->P->opts & TTO_OPT_R3_PERTURB) {
+        if (H->dx_curr > 0.0) H->dx_last = H->dx_curr;
+        H->dx_curr = H->dc_curr = 0.0;
+    } else if (!ph_new(H, S->mu)) {
+        return 1;
     }
-    if (!ok) return 1;
-    if (dw > 0) S->dw_last = dw;
-    *dw_out = dw;
-    W->dw_cur = dw;
+    if (!factor_loop(W, S)) return 1;
     memcpy(W->cr, W->rc0, (size_t)W->nrc * 8);
     memcpy(W->dr, W->rd0, (size_t)W->nrd * 8);
-    refined_solve(W, S->mu, W->cr, W->dr, W->rf0);
-    if (W->dbg & 4) check_newton(W, S->mu, dw);
+    if (!pd_solve(W, S, W->cr, W->dr, W->rf0)) return 1;
+    *dw_out = W->dw_cur;
+    if (W->dbg & 4) check_newton(W, S->mu, W->dw_cur);
     mult_steps(W, S->mu);
     return 0;
 }
@@ -2283,7 +2490,7 @@ static int line_search(ws_t* W, ipm_state_t* S, int iter0, double* th0p, double*
                 for (size_t i = 0; i < nx_; ++i) W->cr[i] = a_soc * W->cr[i] + W->ct[i];
                 for (size_t i = 0; i < ns_; ++i) W->dr[i] = a_soc * W->dr[i] + W->dtr[i];
                 if (W->mode == TTO_OBCA_PLAN) for (int i = 0; i < 6; ++i) frs[i] = a_soc * frs[i] + W->dft[i];
-                refined_solve(W, mu, W->cr, W->dr, frs);
+                if (!pd_solve(W, S, W->cr, W->dr, frs)) break;
                 a_soc = ftb_primal(W, tau);
                 set_trial(W, a_soc);
                 trial_eval(W, mu, &tht, &pht);
@@ -2351,6 +2558,7 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     const tto_obca_problem* P = W->P;
     const int N = W->N;
     W->xinit = xinit; W->xgoal = xgoal; W->xref = xref; W->uref = uref;
+    memset(g_cen, 0, sizeof(g_cen));
     W->R = M_ORIG;
     W->lsq = 0;
     W->have_acc = 0;
@@ -2605,6 +2813,9 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     }
     if (W->R == M_RESTO) W->R = M_ORIG;
     if (dbg) fprintf(stderr, "status %d iters %d resto %d soft %d\n", status, iter, n_resto, n_soft);
+    if (getenv("TTO_CENSUS"))
+        fprintf(stderr, "CENSUS status %d iters %d fact %ld blocks_ok %ld few %ld many %ld zero %ld ref>1e-10 %ld ref>1e-5 %ld pretend %ld\n",
+                status, iter, g_cen[0], g_cen[4], g_cen[1], g_cen[2], g_cen[3], g_cen[5], g_cen[6], g_cen[7]);
     pack(W, zout);
     if (iters_out) *iters_out = iter;
     if (kkt_out) *kkt_out = E0;

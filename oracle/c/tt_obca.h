@@ -58,6 +58,8 @@ typedef struct {
 #define TTO_OPT_WATCHDOG 16      /* watchdog (trigger 10 shortened steps, 3 trial iterations) in the line search */
 #define TTO_OPT_BLOCK_MW 128     /* a block with indefinite A eliminated rows-first through M_w = A + Jw' E^-1 Jw */
 #define TTO_OPT_GLOBAL_INERTIA 256 /* inertia counted over the whole factorisation (blocks, Riccati G_k, soft M_k) */
+#define TTO_OPT_R3_PERTURB 512   /* round 3's inertia correction (delta_x only, from 0 on every matrix; raw-residual
+                                    refinement stop) instead of IPOPT's perturbation handler (delta_c, degeneracy) */
 
 /* x_init (6); plan mode: x_goal (6); track mode: xref ((N+1)*6), uref (N*2).
  * z_guess (n) or NULL (plan: _generate_initial_trajectory_guess 209-225; track: reference copy +

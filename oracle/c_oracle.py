@@ -13,7 +13,8 @@ from pathlib import Path
 import numpy as np
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "build" / "libttoracle.so"
+# TTO_ORACLE_LIB: another build of the oracle (the ASan/UBSan one of `make -C oracle sanitize`)
+LIB_PATH = Path(os.environ["TTO_ORACLE_LIB"]).resolve() if os.environ.get("TTO_ORACLE_LIB") else _HERE / "build" / "libttoracle.so"
 
 
 class TTOProblem(C.Structure):
@@ -110,6 +111,7 @@ OBCA_PLAN, OBCA_TRACK = 0, 1
 # IPOPT features (kappa_d damping, line-search watchdog, rows-first elimination of indefinite blocks)
 OPT_PD_BLOCKS, OPT_NO_REFINE = 32, 64
 OPT_KAPPA_D, OPT_WATCHDOG, OPT_BLOCK_MW, OPT_GLOBAL_INERTIA = 8, 16, 128, 256
+OPT_R3_PERTURB = 512  # round 3's delta_x-only inertia correction instead of IPOPT's perturbation handler (A/B)
 
 
 class TTOObcaProblem(C.Structure):

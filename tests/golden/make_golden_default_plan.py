@@ -1,5 +1,5 @@
-"""Generate tests/golden/reference_default_plan.npz: the C oracle's solution of the reference's own default OBCA
-call (run HERE; ~1 min on one core).
+"""Generate tests/golden/oracle_default_plan.npz: the C ORACLE's solution (not an output of the reference, which cannot
+run here: CasADi/IPOPT are absent) of the reference's own default OBCA call (run HERE; ~1 min on one core).
 
 The reference's default plan (trajectory_animation.py:43-52, 77-83, 109) is N = 200, dt = 0.1, the OBCA bounds and
 all 11 obstacles of obstacles.json, with plan()'s guess built from a Hybrid-A* initialize.json
@@ -49,9 +49,12 @@ def main():
     z, st, it, kk = co.obca_solve_batch(P, x0, xg, z_guess=zg, nthreads=1)
     X, Uo, _, _ = co.obca_split(z, N, M)
     c = plan_cost(X[0], Uo[0], xg[0])
-    np.savez_compressed(HERE / "reference_default_plan.npz", x_init=x0, x_goal=xg, z_guess=zg, z=z, status=st,
-                        iters=it, kkt=kk, cost=c)
-    print(f"reference_default_plan.npz: status {st.tolist()} iterations {it.tolist()} kkt {kk.tolist()} cost {c:.3f}")
+    prov = ("C oracle (oracle/c/tt_obca.c, restated IPOPT incl. its perturbation handler) optimum of the reference's "
+            "default OBCA problem; not produced by the reference (CasADi/IPOPT absent). OBCA optimality parity with "
+            "IPOPT itself is unpinned beyond dynamics, bounds and collision (DESIGN.md section 5).")
+    np.savez_compressed(HERE / "oracle_default_plan.npz", x_init=x0, x_goal=xg, z_guess=zg, z=z, status=st,
+                        iters=it, kkt=kk, cost=c, provenance=np.array(prov))
+    print(f"oracle_default_plan.npz: status {st.tolist()} iterations {it.tolist()} kkt {kk.tolist()} cost {c:.3f}")
 
 
 if __name__ == "__main__":

@@ -74,13 +74,16 @@ def test_mpc_obca_windows_match_oracle():
     bnd = (sc.XLB, sc.XUB, sc.ULB, sc.UUB)
     X, U, Z, st, it, kk = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0, xref=xr, uref=ur)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0, xref=xr, uref=ur, nthreads=16)
-    assert (st == stc).sum() >= 14, (st, stc)          # long restoration runs may branch on round-off
+    assert np.array_equal(st, stc), (st, stc)           # identical statuses on all 16 windows
     both = (st <= 1) & (stc <= 1)
     assert both.sum() >= 9, (st, stc)
     Xc = co.obca_split(zc, 50, 11)[0]
-    # same optimum: identical to round-off on the windows that take the same path, within the stopping
-    # tolerance's reach (tol 1e-8 on the scaled KKT error) on those that reach it through different iterates
-    assert np.max(np.abs(X[both] - Xc[both])) <= 1e-6
+    # the same optimum: to 1e-8 wherever both runs stop at the tol-1e-8 optimum (to round-off where they take the
+    # same path); a run that stops at an acceptable point (acceptable_tol 1e-6 on the scaled KKT error, 15 times)
+    # is compared within that tolerance's reach
+    opt = both & (st == 0) & (stc == 0)
+    assert np.max(np.abs(X[opt] - Xc[opt])) <= 1e-8, np.abs(X - Xc).max(axis=(1, 2))
+    assert np.max(np.abs(X[both] - Xc[both])) <= 1e-6, np.abs(X - Xc).max(axis=(1, 2))
     gap = collision.sat_gap(x0[:, :4], p, obs).min(axis=(-1, -2))
     assert np.all(st[gap < 0.0] > 1) and np.all(stc[gap < 0.0] > 1)
     assert np.all(st[:4] == 0)                          # the open-road windows
@@ -114,7 +117,7 @@ def test_c4_test_cases_vs_oracle():
     assert blocked.sum() == 6 and np.all(st[blocked] == 3) and np.all(stc[blocked] == 3), (st, stc)
     assert (st[~blocked] <= 1).sum() >= 6 and (stc[~blocked] <= 1).sum() >= 6, (st, stc)
     both = (st <= 1) & (stc <= 1)
-    assert both.sum() >= 5, (st, stc)                     # each side >= 6 of the 8: mostly the same ones
+    assert both.sum() >= 6, (st, stc)
     Xc = co.obca_split(zc, 200, 6)[0]
     same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6       # same local optimum (OBCA is nonconvex)
     assert same[both & (st == 0) & (stc == 0)].all()     # optimal-optimal pairs: identical primal
@@ -141,9 +144,7 @@ def test_c4_replan_subset_vs_oracle():
     assert both.sum() >= 14, (st, stc)
     Xc = co.obca_split(zc, 200, 6)[0]
     same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6
-    # the same local optimum wherever both stop, bar one re-plan that a rounding-level branch of a long run
-    # may carry to a neighbouring optimum (OBCA is nonconvex; both are checked feasible and collision-free below)
-    assert same[both].sum() >= both.sum() - 1, np.abs(X - Xc).max(axis=(1, 2))[both]
+    assert same[both].all(), np.abs(X - Xc).max(axis=(1, 2))[both]   # the same local optimum wherever both stop
     nlp = ObcaNLP(200, 6, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
     for b in np.flatnonzero(ok):
         gv, lbg, ubg = nlp.g(Z[b], x0[b], xg[b])
@@ -164,10 +165,8 @@ def test_c4_full_batch_properties_and_determinism():
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
     blocked = (gs < 0.0) | (gg < 0.0)
     # infeasible by construction: they never converge, and they end as IPOPT's restoration failure (status 3)
-    # instead of running to max_iter -- all but a rounding-dependent straggler (1 of 118 after the round-3
-    # change of FMA contraction, none before)
-    assert np.all(st[blocked] >= 2), np.bincount(st[blocked])
-    assert (st[blocked] == 3).mean() >= 0.97, np.bincount(st[blocked])
+    # instead of running to max_iter
+    assert np.all(st[blocked] == 3), np.bincount(st[blocked])
     assert ok[~blocked].mean() >= 0.85, np.bincount(st[~blocked])
     dyn = X[:, 1:] - (X[:, :-1] + 0.1 * _f(X[:, :-1], U))
     assert np.abs(dyn[ok]).max() <= 1e-8
@@ -176,14 +175,14 @@ def test_c4_full_batch_properties_and_determinism():
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
 
 
-def test_reference_default_plan_matches_oracle():
+def test_default_plan_matches_oracle():
     """The reference's own default OBCA call (trajectory_animation.py:43-52, 77-83, 109): N = 200, dt = 0.1, all 11
     obstacles of obstacles.json, the Hybrid-A*-shaped 8-waypoint guess of tests/golden/make_golden_default_plan.py,
     max_iter 5000.  The kernel reaches the oracle's optimum (the committed fixture): same status, the same primal
     solution to 1e-6, cost 64,914, collision-free with d_min active."""
     from oracle import c_oracle as co
     from ttmpc import collision
-    g = np.load(GOLDEN / "reference_default_plan.npz")
+    g = np.load(GOLDEN / "oracle_default_plan.npz")
     ob = np.load(GOLDEN / "reference_numpy.npz")["obstacles"].reshape(-1, 4)
     N, M = 200, ob.shape[0]
     X, U, Z, st, it, kk = _solver(N, ob).solve(g["x_init"], g["x_goal"], z_guess=g["z_guess"])
