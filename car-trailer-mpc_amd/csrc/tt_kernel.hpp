@@ -77,8 +77,11 @@ struct ObcaArgs {
     double* ws;                     // per-instance workspace, obca_ws_doubles(N, M) each
     unsigned long long* stamps;     // [B][kObcaPhases] cycle sums (diagnostics), or nullptr
 };
+// phase clocks, then event counters (diagnostics, tools/obca_stamps.py / obca_tail.py): factorisations (inertia
+// attempts incl. the SOC and pretend-singular refactorisations), restoration-phase iterations, soft-restoration steps,
+// refinement corrections, second-order corrections, pretend-singular re-solves, line-search trial points
 enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_REF_SWEEP, OPH_REF_REC, OPH_TOTAL,
-       kObcaPhases };
+       OCNT_FACTOR, OCNT_RESTO_IT, OCNT_SOFT, OCNT_CORR, OCNT_SOC, OCNT_PRETEND, OCNT_TRIAL, kObcaPhases };
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
 constexpr int kObcaStageFields = 353;

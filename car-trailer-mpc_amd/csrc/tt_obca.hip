@@ -178,6 +178,10 @@ __device__ __forceinline__ void stamp(LShared& sh, bool on, int ph) {
         sh.t0 = t;
     }
 }
+// diagnostic event counter (thread 0)
+__device__ __forceinline__ void count(LShared& sh, bool on, int ev) {
+    if (on && threadIdx.x == 0) sh.stamp[ev] += 1;
+}
 
 // workgroup reduction of NV values with per-value op; result uniform in every thread, fixed order
 template <int NV>
@@ -2777,6 +2781,7 @@ __device__ __noinline__ int newton_solve(const Ctx& c, LShared& sh, double mu, d
     stamp(sh, on, OPH_UPD);
     __syncthreads();
     if (threadIdx.x == 0) sh.dc = dc;
+    count(sh, on, OCNT_FACTOR);
     __syncthreads();
     const int f = phase_factor(c, sh, mu, dw);
     stamp(sh, on, OPH_FACTOR);
@@ -3509,6 +3514,7 @@ __device__ __noinline__ bool refine(const Ctx& c, LShared& sh, double mu, double
         // without the correction's right-hand side; a second correction re-runs the residual pass with it
         if (it >= 1) phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
         __syncthreads();
+        count(sh, on, OCNT_CORR);
         correction_solve(c, sh, mu, dw, buf);
         phase_nres(c, sh, mu, dw, tau, buf, false, NR_CORR, q);
         stamp(sh, on, OPH_REF_REC);
@@ -3927,6 +3933,7 @@ __device__ __forceinline__ bool pd_solve(const Ctx& c, LShared& sh, Perturb& ph,
     double ratio = 0.0;
     const bool quit = refine(c, sh, mu, ph.dx, tau, buf, rec, &ratio);
     if (!quit || ratio < 1e-5) return true;
+    count(sh, c.a->stamps != nullptr, OCNT_PRETEND);
     if (!ph.singular(mu)) return false;
     if (!factor_loop(c, sh, ph, mu, buf)) return false;
     refine(c, sh, mu, ph.dx, tau, buf, rec, &ratio);
@@ -4119,6 +4126,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             do {
                 double red[13];
                 stamp(sh, ston, OPH_UPD);
+                if (R) count(sh, ston, OCNT_RESTO_IT);
                 phase_lin(cs, sh, red);
                 stamp(sh, ston, OPH_LIN);
                 double dinf = red[0], pinf = red[1], c0 = red[2];
@@ -4233,6 +4241,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                         accepted = rel < 1e-15;
                         for (int ls = 0; !accepted; ++ls) {
                             double tr[3];
+                            count(sh, ston, OCNT_TRIAL);
                             phase_trial(cs, sh, mu, alpha, 0, tr);
                             stamp(sh, ston, OPH_TRIAL);
                             const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
@@ -4253,6 +4262,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                                 for (int p = 0; p < 4; ++p) {
                                     if (p > 0 && th_t > 0.99 * th_old) break;
                                     th_old = th_t;
+                                    count(sh, ston, OCNT_SOC);
                                     phase_soc_resid(cs, sh, a_soc);
                                     __syncthreads();
                                     // the same matrix (iterate and perturbations) with the SOC right-hand side
@@ -4312,6 +4322,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                             acc_soft = fin && pd_t <= SOFT_RESTO_FACTOR * pd_cur;
                         }
                         if (acc_soft) {
+                            count(sh, ston, OCNT_SOFT);
                             __syncthreads();
                             if (tid == 0) add_filter(sh, 0, (1.0 - g_th) * th0, phi0 - g_ph * th0);
                             __syncthreads();

@@ -1310,14 +1310,9 @@ __device__ __forceinline__ void phase_init(const Ctx<BM>& c) {
 template <int BM, int OCC, int NS>
 __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void track_kernel(TrackArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    // Instance b = workgroup b.  An XCD-aware map (contiguous instance ranges per XCD, -DTT_XCD_MAP) was
-    // measured: C2 +0.7 %, C3 -6 % (1.896 -> 2.01 ms, profiles/r02/ab_xcd.txt), so the plain map ships.
-#ifdef TT_XCD_MAP
-    const int wg = blockIdx.x, q8 = a.B >> 3, r8 = a.B & 7, x8 = wg & 7;
-    const int b = x8 * q8 + min(x8, r8) + (wg >> 3);
-#else
+    // Instance b = workgroup b.  An XCD-aware map (contiguous instance ranges per XCD) was measured in round 2:
+    // C2 +0.7 %, C3 -6 % (1.896 -> 2.01 ms, profiles/r02/ab_xcd.txt), so the plain map ships.
     const int b = blockIdx.x;
-#endif
     const int N = NS > 0 ? NS : a.N, S = N + 1;  // NS: horizon fixed at compile time (stage offsets fold)
     Ctx<BM> c;
     c.sm = sm;
@@ -1547,11 +1542,10 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // The BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds.  At N = 20 the large-batch
     // occupancy build is the same stage-unrolled code, so an instance's result never depends on B (or on the
     // sharded path's chunk size): only the build's register budget differs, not one operation.
-#ifndef TT_N20_OCC  // A/B builds only: 1 = round 2's generic occupancy build at N = 20, 2 = no occupancy build
-#define TT_N20_OCC 0
+#ifndef TT_N20_OCC_MIN_B  // A/B builds only: the batch above which N = 20 takes the two-waves-per-SIMD build
+#define TT_N20_OCC_MIN_B 4096
 #endif
-    if (m == kMaskMPC && d && a.N == 20 && a.B > 4096 && TT_N20_OCC == 0) return launch<kMaskMPC | kDiagBit, 2, 20>(a, stream);
-    if (m == kMaskMPC && d && a.N == 20 && a.B > 4096 && TT_N20_OCC == 1) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
+    if (m == kMaskMPC && d && a.N == 20 && a.B > TT_N20_OCC_MIN_B) return launch<kMaskMPC | kDiagBit, 2, 20>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);

@@ -48,7 +48,10 @@ L.ttx_obca_set_stamps(s._h, None)
 cyc = d.cpu().numpy().astype(np.float64)
 names = ["lin", "compl", "factor", "riccati", "forward", "recover(+resid)", "trial", "update/other", "riccati_soft",
          "forward_soft", "ref_sweeps", "ref_recover_resid", "TOTAL"]
+counters = ["factorisations", "resto_iters", "soft_resto", "corrections", "soc", "pretend_singular", "trial_points"]
 per_it = cyc / np.maximum(it, 1)[:, None]
 print(f"{wl} B={B} iters mean {it.mean():.1f} max {it.max()}  status {np.bincount(st, minlength=6).tolist()}")
 for i, n in enumerate(names):
-    print(f"  {n:13s} {per_it[:, i].mean():12.0f} cycles/iter  ({100 * cyc[:, i].sum() / cyc[:, -1].sum():5.1f}%)")
+    print(f"  {n:13s} {per_it[:, i].mean():12.0f} cycles/iter  ({100 * cyc[:, i].sum() / cyc[:, len(names) - 1].sum():5.1f}%)")
+for i, n in enumerate(counters):
+    print(f"  {n:17s} {per_it[:, len(names) + i].mean():8.3f} per iteration")
