@@ -194,8 +194,9 @@ def main():
                     help="comma-separated rocprofv3 --pmc CSVs (FETCH_SIZE, WRITE_SIZE) of this config; "
                          "default: the committed profiles/ pair when the config is the default C2")
     ap.add_argument("--max-iter", type=int, default=5000, help="OBCA configs: IPOPT max_iter (reference: 5000)")
-    ap.add_argument("--chunks", type=int, default=4,
-                    help="c5 with N > 1 ranks: pipelined scatter/solve/gather chunks per rank shard")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="c5: pipelined scatter/solve/gather chunks per rank shard (one rank: chunk copies); "
+                         "0 = auto: up to 4 chunks of >= 4096 instances (the N = 20 two-waves-per-SIMD build)")
     ap.add_argument("--graph", action="store_true", help="sim: replay one captured closed-loop step (hipGraph)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -366,7 +367,13 @@ def main_c5(args):
         dist.init_process_group(backend="nccl", device_id=dev)
     solver = ttmpc.BatchSolver(N, sc.PARAMS, sc.MPC_Q, sc.MPC_R, sc.XLB, sc.XUB, sc.ULB, sc.UUB, device=local)
     stream = torch.cuda.Stream(dev)
-    sb = ShardedBatch(B_total, N, gpu_shard_solver(solver, stream), device=dev, chunks=args.chunks if world > 1 else 1)
+    # chunks apply on one rank too (chunk copies instead of collectives), so e.g. --batch 8192 --chunks 2 times on one
+    # GPU exactly the per-rank launch shape of the 8-rank run.  Auto: at most 4 chunks and none
+    # below 4096 instances -- a 2048-instance launch runs at ~9.7 M solves/s against ~12.6 M at 4096 and ~15 M at
+    # >= 8192 (profiles/r04/occ_by_batch/), more than the transfer overlap of a smaller chunk gains back
+    per_rank = -(-B_total // world)
+    chunks = args.chunks if args.chunks > 0 else max(1, min(4, per_rank // 4096))
+    sb = ShardedBatch(B_total, N, gpu_shard_solver(solver, stream), device=dev, chunks=chunks)
     if rank == 0:
         x0, xr, ur = workload("c5", B_total, N, seed=rank_seed(0))
         sb.pack_inputs(x0, xr, ur)

@@ -1542,10 +1542,10 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // The BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds.  At N = 20 the large-batch
     // occupancy build is the same stage-unrolled code, so an instance's result never depends on B (or on the
     // sharded path's chunk size): only the build's register budget differs, not one operation.
-#ifndef TT_N20_OCC_MIN_B  // A/B builds only: the batch above which N = 20 takes the two-waves-per-SIMD build
-#define TT_N20_OCC_MIN_B 4096
-#endif
-    if (m == kMaskMPC && d && a.N == 20 && a.B > TT_N20_OCC_MIN_B) return launch<kMaskMPC | kDiagBit, 2, 20>(a, stream);
+    // Above B = 2048 (two rounds of one wave per SIMD) the two-waves-per-SIMD build wins: 12.6 vs 10.3 M solves/s at
+    // B = 4096, 12.0 vs 9.8 at 3072, equal at 2048, 3 % slower at 1024 (profiles/r04/occ_by_batch/); round 3 switched
+    // at 4096, so the 4096-instance chunks of the sharded C5 path ran one wave per SIMD.
+    if (m == kMaskMPC && d && a.N == 20 && a.B > 2048) return launch<kMaskMPC | kDiagBit, 2, 20>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);

@@ -118,13 +118,55 @@ def test_c4_test_cases_vs_oracle():
     assert (st[~blocked] <= 1).sum() >= 6 and (stc[~blocked] <= 1).sum() >= 6, (st, stc)
     both = (st <= 1) & (stc <= 1)
     assert both.sum() >= 6, (st, stc)
-    Xc = co.obca_split(zc, 200, 6)[0]
+    Xc, Uc, _, _ = co.obca_split(zc, 200, 6)
     same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6       # same local optimum (OBCA is nonconvex)
-    assert same[both & (st == 0) & (stc == 0)].all()     # optimal-optimal pairs: identical primal
-    assert same[both].sum() >= both.sum() - 1            # an 'acceptable' stop may sit elsewhere
+    assert same[both].sum() >= both.sum() - 1, np.abs(X - Xc).max(axis=(1, 2))
+    # The two runs compute the same iterates while they stay in lockstep (test_obca_lockstep_with_oracle); these runs
+    # last 1,000-5,000 iterations, and once rounding has separated them (after ~50-400 iterations on this workload,
+    # DESIGN.md 5) an optimal pair may end in a different basin of the nonconvex NLP.  Such an end point must then
+    # be a stationary point in its own right: the KKT certificate of oracle/obca_certificate.py (every dual rebuilt
+    # from (X, U) alone, x_goal fitted; multipliers of free sign, the bounded fit takes minutes at N = 200) at
+    # round-off, on both sides -- measured 1.5e-7 relative at the oracle's end point of the pair that separated.
+    from oracle.obca_certificate import certify_plan
+    for b in np.flatnonzero(both & (st == 0) & (stc == 0) & ~same):
+        for XX, UU in ((X[b], U[b]), (Xc[b], Uc[b])):
+            r = certify_plan(XX, UU, obs, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB,
+                             sc.OBCA_UUB, act_tol=1e-4, bounded=False)
+            assert r["stat_rel"] < 1e-6 and np.abs(r["x_goal"] - xg[b]).max() < 2e-2, (b, r["stat_rel"])
     ok = st <= 1
     assert np.abs(X[ok, -1] - xg[ok]).max() <= 1e-2 + 1e-7
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
+
+
+def test_obca_lockstep_with_oracle():
+    """Step-level parity: every instance of the three parity workloads (16 MPC+OBCA windows, the 14 C4 test cases, 16
+    re-plans), GPU and oracle both stopped at max_iter K.  Both run the same restated IPOPT on the same inputs, so
+    their iterates agree to round-off while no decision (filter, inertia, barrier update, restoration) has flipped
+    on a last-bit difference: after 25 iterations every instance agrees to <= 1e-9 (measured <= 9e-11), after 50
+    all but a few (measured 43 / 46; DESIGN.md 5 records where the paths separate)."""
+    from oracle import c_oracle as co
+    from ttmpc import scenarios as sc
+    import json
+    import ttmpc
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    obs6 = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
+    cases = json.loads((GOLDEN / "test_cases.json").read_text())["cases"]
+    p50 = dict(P6, dt=0.05)
+    bnd50 = (sc.XLB, sc.XUB, sc.ULB, sc.UUB)
+    x0w, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 16, 50, seed=0)
+    plans = [sc.obca_case_batch(cases, 14, 200, 6, seed=0), sc.obca_replan_batch(g["state_traj"], 16, 200, 6, seed=0)]
+    for K, need in ((25, 46), (50, 40)):
+        d = []
+        X, *_ = _solver(50, g["obstacles"], ttmpc.TT_VARIANT_TRACK_OBCA, p50, bnd50, max_iter=K).solve(x0w, xref=xr, uref=ur)
+        zc, *_ = co.obca_solve_batch(_oracle(50, g["obstacles"], co.OBCA_TRACK, p50, bnd50, max_iter=K), x0w, xref=xr,
+                                     uref=ur, nthreads=16)
+        d.append(np.abs(X - co.obca_split(zc, 50, 11)[0]).max(axis=(1, 2)))
+        for x0, xg, zg in plans:
+            X, *_ = _solver(200, obs6, max_iter=K).solve(x0, xg, z_guess=zg)
+            zc, *_ = co.obca_solve_batch(_oracle(200, obs6, max_iter=K), x0, xg, z_guess=zg, nthreads=16)
+            d.append(np.abs(X - co.obca_split(zc, 200, 6)[0]).max(axis=(1, 2)))
+        d = np.concatenate(d)
+        assert (d <= 1e-9).sum() >= need, (K, d)
 
 
 def test_c4_replan_subset_vs_oracle():
