@@ -80,7 +80,8 @@ struct ObcaArgs {
 // phase clocks, then event counters (diagnostics, tools/obca_stamps.py / obca_tail.py): factorisations (inertia
 // attempts incl. the SOC and pretend-singular refactorisations), restoration-phase iterations, soft-restoration steps,
 // refinement corrections, second-order corrections, pretend-singular re-solves, line-search trial points
-enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_REF_SWEEP, OPH_REF_REC, OPH_TOTAL,
+enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL, OPH_UPD, OPH_RIC_SOFT, OPH_FWD_SOFT, OPH_REF_SWEEP, OPH_REF_REC,
+       OPH_REF_STAGE, OPH_TOTAL,
        OCNT_FACTOR, OCNT_RESTO_IT, OCNT_SOFT, OCNT_CORR, OCNT_SOC, OCNT_PRETEND, OCNT_TRIAL, kObcaPhases };
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N

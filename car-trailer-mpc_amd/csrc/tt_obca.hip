@@ -3471,10 +3471,13 @@ __device__ __noinline__ void correction_solve(const Ctx& c, LShared& sh, double 
     if (c.lds) {
         stage_vec_inputs(c, c.lds, soft);
         __syncthreads();
+        stamp(sh, on, OPH_REF_STAGE);
         if (threadIdx.x < 64) riccati_vec(c, VecL{(const lds_double*)c.lds}, soft);
         __syncthreads();
+        stamp(sh, on, OPH_REF_SWEEP);
         stage_soft_forward(c, c.lds, soft);
         __syncthreads();
+        stamp(sh, on, OPH_REF_STAGE);
         if (threadIdx.x < 64) {
             if (soft) forward_soft(c, SoftF{(const lds_double*)c.lds}, 2);
             else forward(c, SoftF{(const lds_double*)c.lds}, 2);
@@ -3508,15 +3511,21 @@ __device__ __noinline__ bool refine(const Ctx& c, LShared& sh, double mu, double
     stamp(sh, on, OPH_REC);
     const double bnorm = q[1];
     double ratio = q[0] / (fmin(q[2], 1e6) + bnorm);
-    bool quit = false;
+    bool quit = false, prepped = true;  // the NR_MAIN pass prepared the first correction's right-hand side
     for (int it = 0; !quit && (it < 1 || ratio > 1e-10); ++it) {
-        // one correction is the rule (the oracle's census: > 99.9 % of the solves), so the check after it runs
-        // without the correction's right-hand side; a second correction re-runs the residual pass with it
-        if (it >= 1) phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
+        // One correction is the rule away from the degenerate tail, so the residual pass after the first runs without
+        // the next correction's right-hand side (the prep part); once a second correction was needed, more follow (C4
+        // tail: ~3.8 per solve, profiles/r04/tail/) and every residual pass prepares the next one, instead of a
+        // separate NR_STEP pass per correction (the same expressions on the same inputs: bitwise the same step)
+        if (!prepped) phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
         __syncthreads();
         count(sh, on, OCNT_CORR);
         correction_solve(c, sh, mu, dw, buf);
-        phase_nres(c, sh, mu, dw, tau, buf, false, NR_CORR, q);
+#ifndef OBCA_PREP_FUSE  // A/B only (bitwise check of the fusion): 0 = round 3's separate NR_STEP pass
+#define OBCA_PREP_FUSE 1
+#endif
+        prepped = OBCA_PREP_FUSE && it >= 1;
+        phase_nres(c, sh, mu, dw, tau, buf, prepped, NR_CORR, q);
         stamp(sh, on, OPH_REF_REC);
         const double ratio2 = q[0] / (fmin(q[2], 1e6) + bnorm);
         if (ratio2 > 1e-10 && it + 1 > 1 && (it + 1 > 10 || ratio2 > ratio)) quit = true;

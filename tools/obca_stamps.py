@@ -47,7 +47,7 @@ torch.cuda.synchronize()
 L.ttx_obca_set_stamps(s._h, None)
 cyc = d.cpu().numpy().astype(np.float64)
 names = ["lin", "compl", "factor", "riccati", "forward", "recover(+resid)", "trial", "update/other", "riccati_soft",
-         "forward_soft", "ref_sweeps", "ref_recover_resid", "TOTAL"]
+         "forward_soft", "ref_sweeps", "ref_recover_resid", "ref_staging", "TOTAL"]
 counters = ["factorisations", "resto_iters", "soft_resto", "corrections", "soc", "pretend_singular", "trial_points"]
 per_it = cyc / np.maximum(it, 1)[:, None]
 print(f"{wl} B={B} iters mean {it.mean():.1f} max {it.max()}  status {np.bincount(st, minlength=6).tolist()}")

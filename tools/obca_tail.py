@@ -1,6 +1,6 @@
 """Where an iteration of the C4 max_iter tail goes (diagnostic, GPU box).
 
-    python tools/obca_tail.py [B] [K1] [K2]
+    python tools/obca_tail.py [B] [K1] [K2] [out.npz]
 Runs the bench's C4 batch (B instances, seed 0, the 4 collision-free test cases) twice with the phase clocks and event
 counters on (ttx_obca_set_stamps), stopped at max_iter K1 and K2.  For the instances that run to max_iter in both, the
 difference of the two runs is exactly their iterations K1..K2: per phase the shader cycles per iteration, and per
@@ -33,7 +33,7 @@ L.ttx_obca_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
 L.ttx_obca_set_stamps.restype = C.c_int
 nph = L.ttx_obca_set_stamps(None, None)
 names = ["lin", "compl", "factor", "riccati", "forward", "recover(+resid)", "trial", "update/other", "riccati_soft",
-         "forward_soft", "ref_sweeps", "ref_recover_resid"]
+         "forward_soft", "ref_sweeps", "ref_recover_resid", "ref_staging"]
 counters = ["factorisations", "resto_iters", "soft_resto", "corrections", "soc", "pretend_singular", "trial_points"]
 TOT = len(names)
 
@@ -55,6 +55,8 @@ def run(K):
 
 c1, st1, it1, w1 = run(K1)
 c2, st2, it2, w2 = run(K2)
+if len(sys.argv) > 4:
+    np.savez(sys.argv[4], c1=c1, st1=st1, it1=it1, w1=w1, c2=c2, st2=st2, it2=it2, w2=w2)
 tail = (it1 == K1) & (it2 == K2)
 print(f"C4 B={B}: max_iter {K1}: {w1:.2f} s, status {np.bincount(st1, minlength=6).tolist()};  max_iter {K2}: {w2:.2f} s, "
       f"status {np.bincount(st2, minlength=6).tolist()};  {int(tail.sum())} instances at max_iter in both")
@@ -80,3 +82,18 @@ if tail.any():
     for b in np.flatnonzero(tail):
         r = (c2[b] - c1[b]) / float(K2 - K1)
         print(f"    #{b:3d}: {r[TOT]:10.0f}  {r[TOT + 1]:6.3f}  {r[TOT + 2]:6.3f}")
+
+# the instances that set the K2 launch time: their whole run, per phase (the phases sum to the instance's clock, and the
+# slowest instance's clock / the effective shader clock is the launch time)
+print(f"slowest instances of the max_iter {K2} launch (whole run):")
+order = np.argsort(-c2[:, TOT])[:5]
+for b in order:
+    r = c2[b]
+    print(f"  #{b:3d}: status {st2[b]} iters {it2[b]:5d}  {r[TOT]:.4e} cycles = {r[TOT] / (c2[:, TOT].max() / w2):.2f} s "
+          f"({r[TOT] / max(it2[b], 1) / 1e6:.2f} M cycles/iter; factorisations/iter {r[TOT + 1] / max(it2[b], 1):.2f}, "
+          f"resto iters {r[TOT + 2]:.0f}, corrections/iter {r[TOT + 4] / max(it2[b], 1):.2f}, "
+          f"trial points/iter {r[TOT + 7] / max(it2[b], 1):.2f})")
+b = order[0]
+print(f"  phases of #{b} (cycles per iteration over its {it2[b]} iterations):")
+for i, n in enumerate(names):
+    print(f"    {n:18s} {c2[b, i] / max(it2[b], 1):12.0f}  ({100 * c2[b, i] / c2[b, TOT]:5.1f}%)")
