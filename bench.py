@@ -740,6 +740,7 @@ def main_obca(args):
         "solver": solver_rec,
         "roofline": {"bound": "valu_fp64", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP64_PEAK_TFLOPS, 7), "traffic": traffic, "traffic_source": traffic_src,
+                     "traffic_estimated": traffic is not None,
                      "note": "latency-bound (serial Riccati over N stages per instance, one workgroup per instance); "
                              "flops: SURVEY §8(d) C4 block-arrow formula x per-instance iterations"},
     }
@@ -785,10 +786,10 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 TRAFFIC_COMMIT = "fcd2080"
 
 
-# committed PMC passes of obca_kernel (tools/obca_pmc.sh): HBM bytes per instance-iteration, scaled by a launch's
-# summed IPM iterations for roofline.traffic of the OBCA lines (same N, M; c4all shares c4's kernel shape)
-OBCA_PMC = {"c4": "profiles/r03/final_c844f7e/pmc_c4", "c4all": "profiles/r03/final_c844f7e/pmc_c4",
-            "cobs": "profiles/r03/final_c844f7e/pmc_cobs"}
+# committed PMC passes of obca_kernel (tools/obca_pmc.sh, one short probe per config on the shipped kernel): HBM bytes per
+# instance-iteration, scaled by a launch's summed IPM iterations for roofline.traffic of the OBCA lines -- an estimate
+# (the probe's iteration mix is not the full launch's), flagged as such in the line (traffic_estimated)
+OBCA_PMC = {"c4": "profiles/r04/pmc_c4", "c4all": "profiles/r04/pmc_c4all", "cobs": "profiles/r04/pmc_cobs"}
 
 
 def obca_traffic(cfg, iters_sum):

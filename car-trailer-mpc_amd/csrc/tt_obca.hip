@@ -3517,7 +3517,10 @@ __device__ __noinline__ bool refine(const Ctx& c, LShared& sh, double mu, double
         // the next correction's right-hand side (the prep part); once a second correction was needed, more follow (C4
         // tail: ~3.8 per solve, profiles/r04/tail/) and every residual pass prepares the next one, instead of a
         // separate NR_STEP pass per correction (the same expressions on the same inputs: bitwise the same step)
-        if (!prepped) phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
+        if (!prepped) {
+            phase_nres(c, sh, mu, dw, tau, buf, true, NR_STEP, q);
+            stamp(sh, on, OPH_REF_REC);
+        }
         __syncthreads();
         count(sh, on, OCNT_CORR);
         correction_solve(c, sh, mu, dw, buf);

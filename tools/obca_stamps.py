@@ -53,5 +53,5 @@ per_it = cyc / np.maximum(it, 1)[:, None]
 print(f"{wl} B={B} iters mean {it.mean():.1f} max {it.max()}  status {np.bincount(st, minlength=6).tolist()}")
 for i, n in enumerate(names):
     print(f"  {n:13s} {per_it[:, i].mean():12.0f} cycles/iter  ({100 * cyc[:, i].sum() / cyc[:, len(names) - 1].sum():5.1f}%)")
-for i, n in enumerate(counters):
+for i, n in enumerate(counters[:max(0, nph - len(names))]):  # (an older build has fewer slots)
     print(f"  {n:17s} {per_it[:, len(names) + i].mean():8.3f} per iteration")
