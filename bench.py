@@ -196,7 +196,7 @@ def main():
     ap.add_argument("--max-iter", type=int, default=5000, help="OBCA configs: IPOPT max_iter (reference: 5000)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="c5: pipelined scatter/solve/gather chunks per rank shard (one rank: chunk copies); "
-                         "0 = auto: up to 4 chunks of >= 4096 instances (the N = 20 two-waves-per-SIMD build)")
+                         "0 = auto: one rank 1, else up to 4 chunks of >= 4096 instances (the N = 20 two-wave build)")
     ap.add_argument("--graph", action="store_true", help="sim: replay one captured closed-loop step (hipGraph)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -371,8 +371,10 @@ def main_c5(args):
     # GPU exactly the per-rank launch shape of the 8-rank run.  Auto: at most 4 chunks and none
     # below 4096 instances -- a 2048-instance launch runs at ~9.7 M solves/s against ~12.6 M at 4096 and ~15 M at
     # >= 8192 (profiles/r04/occ_by_batch/), more than the transfer overlap of a smaller chunk gains back
+    # (one rank has no transfers to overlap: one chunk; 65536 x 1 chunk 14.0 M/s, x 4 chunks 13.4 M/s,
+    # profiles/r04/session_b/)
     per_rank = -(-B_total // world)
-    chunks = args.chunks if args.chunks > 0 else max(1, min(4, per_rank // 4096))
+    chunks = args.chunks if args.chunks > 0 else 1 if world == 1 else max(1, min(4, per_rank // 4096))
     sb = ShardedBatch(B_total, N, gpu_shard_solver(solver, stream), device=dev, chunks=chunks)
     if rank == 0:
         x0, xr, ur = workload("c5", B_total, N, seed=rank_seed(0))

@@ -817,88 +817,66 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     return pd;
 }
 
-// ============ forward sweep: dx_{k+1} = A_k dx_k + B du_k + b_k,  du_k = K_k dx_k + kf_k ============
-// Lane q of the first 16-lane row owns one output row: q < 6 dx_{k+1}[q] = dx_k[q] + D[q][.] dx_k + b_k[q] (+ dt du_k
-// for q = 5, 4: B = dt [e5 e4]), q = 6, 7 du_{q-6} = K[q-6][.] dx_k + kf[q-6].  The six dx_k[m] it needs arrive by DPP
-// row_newbcast from lanes m (no LDS round trip on the serial chain), du by two more broadcasts; each lane reads only
-// its own row's coefficients (D row q or K row q-6, zeros from PAD), one stage ahead.  YP (the Newton sweep): lanes
-// 8..13 run the same dot product on row r = q-8 of P_k with p_k as the constant, i.e. y+_k[r] = -(p_k + P_k dx_k)[r],
-// the step's new multipliers, in the same ds_read instructions and FMAs as the sweep (phase_step then skips them).
-// The other 16-lane rows repeat row 0's arithmetic on their own (ignored) values.  b_k = -c_{k+1}: the stored rBH row at stage k, or (BHN,
-// the SOC sweep) the residual rows of stage k+1 themselves -- c_soc lives where its own output dX_soc goes, and
-// stage k+1's residual is read one stage before dx_{k+1} overwrites it.
-template <int L_>
-__device__ __forceinline__ double rowbc(double v) {  // every lane of a 16-lane row receives lane L_ of that row
+// ============ forward sweep: [x^_{k+1}; du_k] = [Phi_k; K^_k] x^_k, Phi = A^ + B^ K^ ============
+// Lane 8g + m owns the term Phi[row(g)][m] x^_k[m] (rows g = 0..5: dx_{k+1}; g = 6, 7: du0, du1).
+// The row sums are three in-row DPP adds (quad xor 1, xor 2, half-mirror); the next stage's x^[m]
+// comes from group m by one ds_bpermute.  crow: residual rows (x^_0 = [-c_0; 1]); bhrow: b^ = -c_{k+1}
+// stored at stage k.
+__device__ __forceinline__ double bperm_d(double v, int src_lane) {
     const long long b = __double_as_longlong(v);
-    return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + L_, 0xF, 0xF, false));
+    const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b & 0xffffffffll));
+    const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-struct FwdOps {
-    double co[6], b;
-};
-#ifndef TT_FWD_YP
-#define TT_FWD_YP 1
-#endif
+
+// NS > 0: the horizon is a compile-time constant and the sweep is fully unrolled, so every stage's LDS
+// offsets fold into the ds_read/ds_write immediates (no per-stage address arithmetic)
 template <int BM, int NS, bool BHN = false>
 __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bhrow, int orow) {
-    const int N = c.N, q = c.lane & 15;
-    constexpr bool YP = !BHN && TT_FWD_YP;
-    const bool yrow = YP && c.lane >= 8 && c.lane < 14;  // y+ rows (first 16-lane row only)
-    int cr[6];
-#pragma unroll
-    for (int m = 0; m < 6; ++m)
-        cr[m] = q < 6 ? (d_idx(q, m) >= 0 ? rAJ + d_idx(q, m) : PAD) : q < 8 ? rK + 6 * (q - 6) + m
-              : (YP && q < 14) ? rPS + sym_idx(q - 8, m) : PAD;
-    const int br = q < 6 ? (BHN ? SR + crow + q : bhrow + q) : q < 8 ? rKF + (q - 6) : (YP && q < 14) ? rPV + (q - 8) : PAD;
-    const double bs = (BHN && q < 6) ? -1.0 : 1.0, dt = c.dt;
-    const bool xrow = q < 6;
-    auto ops = [&](int k, FwdOps& o) __attribute__((always_inline)) {
-#pragma unroll
-        for (int m = 0; m < 6; ++m) o.co[m] = c.r(cr[m], k);
-        o.b = bs * c.r(br, k);
-    };
-    double x = xrow ? -c.r(crow + q, 0) : 0.0;
-    if (c.lane < 6) c.r(orow + c.lane, 0) = x;
-    auto step = [&](int k, const FwdOps& o, FwdOps& nx) __attribute__((always_inline)) {
-        const double d0 = rowbc<0>(x), d1 = rowbc<1>(x), d2 = rowbc<2>(x), d3 = rowbc<3>(x), d4 = rowbc<4>(x),
-                     d5 = rowbc<5>(x);
-        ops(k + 1 < N ? k + 1 : k, nx);  // next stage's coefficients, behind the broadcasts
-        const double base = (xrow ? x : 0.0) + o.b;
-        const double t1 = fma(o.co[0], d0, fma(o.co[2], d2, fma(o.co[4], d4, base)));
-        const double t2 = fma(o.co[1], d1, fma(o.co[3], d3, o.co[5] * d5));
-        const double y = t1 + t2;  // dx_{k+1}[q] without B du (q < 6), du_{q-6} (q = 6, 7)
-        const double du0 = rowbc<6>(y), du1 = rowbc<7>(y);
-        const double nx_ = q == 5 ? fma(dt, du0, y) : q == 4 ? fma(dt, du1, y) : y;
-        if (c.lane < 8) c.r(orow + q, c.lane < 6 ? k + 1 : k) = nx_;
-        if constexpr (YP) {
-            if (yrow) c.r(rYP + q - 8, k) = -y;  // b^_k (rBH = rYP) was read one stage earlier
+    const int N = c.N, g = c.lane >> 3, mm = c.lane & 7;
+    // output row of this lane's group: 0..5 = dx_{k+1}[g], 6/7 = du0/du1 (rows 7/8 of [Phi; K^])
+    const int u = (g == 5 || g == 6) ? 0 : (g == 4 || g == 7) ? 1 : -1;
+    const double fone = (g < 6 && mm == g) ? 1.0 : 0.0;
+    // BHN: b^_k = -c_{k+1} read straight from the residual rows of stage k+1 (row SR + crow + g of stage k)
+    // instead of a stored b^ row (the SOC sweep: c_soc lives where its own output dX_soc goes)
+    const int fas = (g < 6 && mm < 6 && d_idx(g, mm) >= 0) ? rAJ + d_idx(g, mm)
+                  : (g < 6 && mm == 6) ? (BHN ? SR + crow + g : bhrow + g) : PAD;
+    const double fsg = (BHN && g < 6 && mm == 6) ? -1.0 : 1.0;
+    const int fk = (u >= 0 && mm < 6) ? rK + 6 * u + mm : (u >= 0 && mm == 6) ? rKF + u : PAD;
+    const double fkc = u >= 0 ? (g < 6 ? c.dt : 1.0) : 0.0;
+    // x^_0[m] = -c_0[m] (m < 6), 1 (m = 6), 0 (m = 7)
+    double x = mm < 6 ? -c.r(crow + mm, 0) : (mm == 6 ? 1.0 : 0.0);
+    if (c.lane < 6) c.r(orow + c.lane, 0) = -c.r(crow + c.lane, 0);
+    const int src = 8 * (mm < 6 ? mm : 0);  // group holding x_{k+1}[mm]
+    double nph = fone + fsg * c.r(fas, 0) + fkc * c.r(fk, 0);
+    // unrolled builds: one unmasked store per lane and stage.  Lane 8g writes its output (dx_{k+1}[g] or
+    // du_k[g-6]); the other 56 lanes write a row that is dead here -- the Hessian diagonal (rHD, consumed
+    // by the Riccati) in the Newton sweep, the residual c (rCC, consumed by the SOC right-hand side) in
+    // the SOC sweep
+    const int fst = mm == 0 ? (g < 6 ? SR + orow + g : orow + g) : (BHN ? rCC : rHD) + (g % 6);
+    auto step = [&](int k) {
+        const double ph = nph;
+        const int kn = k + 1 < N ? k + 1 : k;
+        nph = fone + fsg * c.r(fas, kn) + fkc * c.r(fk, kn);
+        double y = ph * x;
+        y += dppd<0xB1>(y);   // quad_perm [1,0,3,2]
+        y += dppd<0x4E>(y);   // quad_perm [2,3,0,1]
+        y += dppd<0x141>(y);  // row_half_mirror: the 8-lane group sum, in every lane of the group
+        // rows 0..5 -> dx_{k+1}; groups 6/7 -> du0/du1 at stage k
+        if constexpr (NS > 0) {
+            c.sm[HEAD + k * SR + fst] = y;
+        } else {
+            pstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
+            pstore(c, mm == 0 && g >= 6, orow + g, k, y);
         }
-        x = nx_;
+        const double xn = bperm_d(y, src);
+        x = mm < 6 ? xn : (mm == 6 ? 1.0 : 0.0);
     };
-    FwdOps oa, ob;
-    ops(0, oa);
     if constexpr (NS > 0) {
 #pragma unroll
-        for (int k = 0; k + 1 < NS; k += 2) {
-            step(k, oa, ob);
-            step(k + 1, ob, oa);
-        }
-        if constexpr (NS % 2 == 1) step(NS - 1, oa, ob);
+        for (int k = 0; k < NS; ++k) step(k);
     } else {
-        int k = 0;
-        for (; k + 1 < N; k += 2) {
-            step(k, oa, ob);
-            step(k + 1, ob, oa);
-        }
-        if (k < N) step(k, oa, ob);
-    }
-    if constexpr (YP) {  // y+_N = -(p_N + P_N dx_N)
-        FwdOps o;
-        ops(N, o);
-        const double d0 = rowbc<0>(x), d1 = rowbc<1>(x), d2 = rowbc<2>(x), d3 = rowbc<3>(x), d4 = rowbc<4>(x),
-                     d5 = rowbc<5>(x);
-        const double t1 = fma(o.co[0], d0, fma(o.co[2], d2, fma(o.co[4], d4, o.b)));
-        const double t2 = fma(o.co[1], d1, fma(o.co[3], d3, o.co[5] * d5));
-        if (yrow) c.r(rYP + q - 8, N) = -(t1 + t2);
+        for (int k = 0; k < N; ++k) step(k);
     }
     __syncthreads();
 }
@@ -950,17 +928,16 @@ struct StepInfo {
 
 // ============ new multipliers y+ = -(P dx + p), step bounds, merit slope (stage-parallel) ============
 template <int BM>
-__device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool primal_pieces, bool yp_done = false) {
+__device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool primal_pieces) {
     const int N = c.N;
     double ap = 1.0, az = 1.0, Dg = 0.0, rel = 0.0;
     const int p = c.part();
     for (int k = c.k0(); k <= N; k += c.kst()) {
         double dx[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) dx[i] = yp_done ? 0.0 : c.r(dzr + i, k);
+        for (int i = 0; i < 6; ++i) dx[i] = c.r(dzr + i, k);
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
-            if (yp_done) break;
             if (c.pair && q >= 3) break;
             const int i = c.pair ? 2 * q + p : q;
             double s = c.r(rPV + i, k);
@@ -1436,7 +1413,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             STAMP(PH_RIC);
             phase_forward<BM, NS>(c, rCC, rBH, rDX);
             STAMP(PH_FWD);
-            const StepInfo si = phase_step(c, rDX, true, TT_FWD_YP != 0);
+            const StepInfo si = phase_step(c, rDX, true);
             STAMP(PH_STEP);
             // IPOPT filter line search (Waechter & Biegler 2006, IPOPT defaults) with one second-order
             // correction; theta / phi_mu of the current point come from the linearisation pass

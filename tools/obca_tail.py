@@ -1,7 +1,7 @@
 """Where an iteration of the C4 max_iter tail goes (diagnostic, GPU box).
 
-    python tools/obca_tail.py [B] [K1] [K2] [out.npz]
-Runs the bench's C4 batch (B instances, seed 0, the 4 collision-free test cases) twice with the phase clocks and event
+    python tools/obca_tail.py [B] [K1] [K2] [out.npz] [seed]
+Runs the bench's C4 batch (B instances, bench.py's seed, the 4 collision-free test cases) twice with the phase clocks and event
 counters on (ttx_obca_set_stamps), stopped at max_iter K1 and K2.  For the instances that run to max_iter in both, the
 difference of the two runs is exactly their iterations K1..K2: per phase the shader cycles per iteration, and per
 iteration the factorisations (inertia attempts), restoration iterations, soft-restoration steps, refinement
@@ -27,7 +27,8 @@ K2 = int(sys.argv[3]) if len(sys.argv) > 3 else 5000
 G = REPO / "tests" / "golden"
 obs = sc.obstacles_array(sc.load_obstacles(G / "obstacles.json"))[:6]
 cases = json.loads((G / "test_cases.json").read_text())["cases"]
-x0, xg, zg = sc.obca_case_batch(cases, B, 200, 6, seed=0, obstacles=obs, params=sc.OBCA_PARAMS)
+SEED = int(sys.argv[5]) if len(sys.argv) > 5 else 7  # 7 = bench.py's rank-0 seed (rank_seed(0)): the bench's C4 batch
+x0, xg, zg = sc.obca_case_batch(cases, B, 200, 6, seed=SEED, obstacles=obs, params=sc.OBCA_PARAMS)
 L = ttmpc.lib()
 L.ttx_obca_set_stamps.argtypes = [C.c_void_p, C.c_void_p]
 L.ttx_obca_set_stamps.restype = C.c_int
