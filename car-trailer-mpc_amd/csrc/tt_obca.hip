@@ -36,21 +36,8 @@
 // cross-statement fusion depends on how many uses a product has in the inlined context, so the same block
 // elimination could round differently in phase_factor and in the recovery passes that recompute it
 // (block_refactor); with contraction fixed by the source they are bitwise the same computation.
-#ifndef OBCA_CONTRACT
-#define OBCA_CONTRACT 1
-#endif
-#if OBCA_CONTRACT == 0
-#pragma clang fp contract(off)
-#elif OBCA_CONTRACT == 1
 #pragma clang fp contract(on)
-#else
-#pragma clang fp contract(fast)
-#endif
 
-// A/B switch: phase_factor loads block j+1's inputs during block j (1) or each block's at its start (0)
-#ifndef OBCA_FACTOR_PF
-#define OBCA_FACTOR_PF 1
-#endif
 // A/B switch: the block elimination divides through shared reciprocals (v_rcp_f64 + two Newton steps, <= 1 ulp) and
 // takes 1/sqrt by v_rsq_f64 + Newton (1), or by IEEE division / sqrt (0, the default since round 4: the oracle
 // divides, and the GPU-vs-oracle status agreement is measured closer with it, profiles/r04/parity/)
@@ -218,6 +205,7 @@ __device__ __forceinline__ double inv(double x) {
 #endif
 }
 
+#if OBCA_RCP
 // 1/sqrt(x) by v_rsq_f64 + two Newton steps (x finite, positive, normal)
 __device__ __forceinline__ double frsqrt(double x) {
     double y = __builtin_amdgcn_rsq(x);
@@ -225,6 +213,7 @@ __device__ __forceinline__ double frsqrt(double x) {
     y = y * fma(-hx * y, y, 1.5);
     return y * fma(-hx * y, y, 1.5);
 }
+#endif
 
 // row_newbcast:l (gfx90a+ DPP on a 64-bit move): every lane of a 16-lane row receives lane l of that row
 template <int L_>
@@ -232,13 +221,6 @@ __device__ __forceinline__ double rowbc(double v) {
     const long long b = __double_as_longlong(v);
     return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + L_, 0xF, 0xF, false));
 }
-
-// A/B switch: riccati_vec / forward_soft with lane q owning component q of the vector and the other components
-// broadcast by DPP (1), or every lane carrying the whole vector and reading every operand (0).  Same operations in
-// the same order either way (bitwise identical).
-#ifndef OBCA_VEC_DPP
-#define OBCA_VEC_DPP 1
-#endif
 
 // sum of logs as log(prod of mantissas) + (sum of exponents) ln 2
 struct LogSum {
@@ -430,11 +412,8 @@ typedef __attribute__((address_space(3))) double lds_double;  // LDS-qualified: 
 // per-thread LDS slab of the block phases: the 48 doubles of Yl, Zl, G (field stride T, conflict-free).  Kept in
 // registers they were what the block elimination spilled to scratch, and every scratch reload waited behind
 // the factor-record stores (one in-order vmcnt); ds_ reads wait on lgkmcnt only.
-// A/B switch: W_{x lam} of the block (16 doubles) in the slab too (1) or in registers (0)
-#ifndef OBCA_HXL_SLAB
-#define OBCA_HXL_SLAB 1
-#endif
-constexpr int kSlab = OBCA_HXL_SLAB ? 64 : 48;
+// W_{x lam} of the block (16 doubles) lives in the slab too (rows 48-63)
+constexpr int kSlab = 64;
 struct Blk {
     lds_double* m;                   // this thread's slab (Yl 0-15 | Zl 16-31 | G 32-47)
     __device__ __forceinline__ lds_double& Yl(int a, int r) const { return m[(a * 4 + r) * T]; }  // L^-1 Jw_lam'  [a][r]
@@ -446,13 +425,7 @@ struct Blk {
     double jw0[8], ca, sa, an, cn;   // Jw row 0 + the rotation/normal data of rows 1..3
     double hl, hw;
     double hxx22, hxx23, hxx33;
-#if OBCA_HXL_SLAB
     __device__ __forceinline__ lds_double& H(int q, int a) const { return m[(48 + q * 4 + a) * T]; }  // W_{x lam} [q][a]
-#else
-    double hxl[4][4];                // W_{x lam}: rows X,Y,theta,psi
-    __device__ __forceinline__ double& H(int q, int a) { return hxl[q][a]; }
-    __device__ __forceinline__ double H(int q, int a) const { return hxl[q][a]; }
-#endif
     double haa, hac, hcc;            // the lam-lam Hessian y4 T'H4T (LL before the elimination), see hll
     // elimination
     double idm[4];                   // 1 / (Sigma_mu + dw) (mu block is diagonal)
@@ -1020,24 +993,17 @@ __device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, d
         const Trig tr = stage_trig(x);
         // only the stage contributions leave this pass: the recovery passes recompute the elimination
         // (block_refactor), so a failed inertia attempt costs the block reads and no stores
-        BlkIn cur;
-#if OBCA_FACTOR_PF
+        BlkIn cur;  // block j+1's inputs are loaded during block j
         load_blk_in(c, rs, 0, k, cur);
-#endif
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4];
-#if !OBCA_FACTOR_PF
-            load_blk_in(c, rs, j, k, cur);
-#endif
             const int f = block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
             if (f == F_ZERO) fail[0] = 1.0;
             if (f == F_MANY) fail[1] = 1.0;
             if (f == F_FEW) fail[2] = 1.0;
-#if OBCA_FACTOR_PF
             if (j + 1 < c.nbk) load_blk_in(c, rs, j + 1, k, cur);
-#endif
         }
         double Qs[21], qv[6];
         const double sc = (k == N && plan) ? a.tfac : 1.0;
@@ -1391,7 +1357,23 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
 // ======== phase: forward sweep (wave 0) into step buffer buf ========
 // dx_0 = -c_0; du_k = K_k dx_k + kff_k; dx_{k+1} = A_k dx_k + B du_k - c_{k+1}; y+_k = -(P_k dx_k + p_k).
 // The 6-vector recursion is carried redundantly by every lane (wave-uniform registers: no readlane /
-// broadcast on the serial chain); lanes 0..5 then write row r of the stage outputs off the chain.
+// broadcast on the serial chain); lanes 0..5 then write row r of the stage outputs off the chain.  The chain's
+// operands of stage k+1 (K, kff, the D nonzeros, c_{k+2}: broadcast LDS reads) are loaded during stage k, so no
+// stage waits for its own LDS reads (the same operations on the same values as loading them in place).
+struct FwdOps {
+    double kf0, kf1, K[12], aj[9], e[6];
+};
+template <class Src>
+__device__ __forceinline__ void fwd_ops(const Src& src, int k, FwdOps& o) {
+    o.kf0 = src.KF(0, k);
+    o.kf1 = src.KF(1, k);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) o.K[q] = src.K(q, k);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) o.aj[q] = src.AJ(q, k);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) o.e[q] = src.CR(q, k + 1);
+}
 template <class Src>
 __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
     const WsView vw = ws_view(c);
@@ -1401,7 +1383,7 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
     double dx[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) dx[q] = -src.CR(q, 0);
-    for (int k = 0;; ++k) {
+    auto out = [&](int k) __attribute__((always_inline)) {
         if (lane < 6) {
             double t = src.PV(r, k), dxr = dx[0];
 #pragma unroll
@@ -1411,22 +1393,20 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
             vw.S(S_YCP + 6 * buf + r, k) = -t;
             vw.S(S_DX + 6 * buf + r, k) = dxr;
         }
-        if (k == N) break;
-        double du0 = src.KF(0, k), du1 = src.KF(1, k);
+    };
+    auto chain = [&](int k, const FwdOps& o) __attribute__((always_inline)) {
+        double du0 = o.kf0, du1 = o.kf1;
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
-            du0 = fma(src.K(q, k), dx[q], du0);
-            du1 = fma(src.K(6 + q, k), dx[q], du1);
+            du0 = fma(o.K[q], dx[q], du0);
+            du1 = fma(o.K[6 + q], dx[q], du1);
         }
         if (lane == 0) {
             vw.S(S_DU + 2 * buf, k) = du0;
             vw.S(S_DU + 2 * buf + 1, k) = du1;
         }
-        double aj[9], e[6];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) aj[q] = src.AJ(q, k);
-#pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k + 1);
+        const double* aj = o.aj;
+        const double* e = o.e;
         double nx[6];
         nx[0] = (dx[0] - e[0]) + fma(aj[0], dx[2], aj[1] * dx[5]);
         nx[1] = (dx[1] - e[1]) + fma(aj[2], dx[2], aj[3] * dx[5]);
@@ -1436,7 +1416,25 @@ __device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
         nx[5] = (dx[5] - e[5]) + dt * du0;
 #pragma unroll
         for (int q = 0; q < 6; ++q) dx[q] = nx[q];
+    };
+    // two stages per trip, ping-pong operand sets (no register copies between stages)
+    FwdOps oa, ob;
+    int k = 0;
+    if (N > 0) fwd_ops(src, 0, oa);
+    for (; k + 1 < N; k += 2) {
+        fwd_ops(src, k + 1, ob);
+        out(k);
+        chain(k, oa);
+        if (k + 2 < N) fwd_ops(src, k + 2, oa);
+        out(k + 1);
+        chain(k + 1, ob);
     }
+    if (k < N) {
+        out(k);
+        chain(k, oa);
+        ++k;
+    }
+    out(N);
 }
 
 // ======== restoration phase: Riccati sweep with soft dynamics rows (wave 0) ========
@@ -1702,53 +1700,69 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf)
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
-#if OBCA_VEC_DPP
     // lanes 0..5 own dx[q] (q = lane); the 6-vectors the rows need (dx, P dx + p) arrive by DPP row_newbcast, so each
     // lane reads only its own rows of P and Y.  Same operations in the same order as the redundant form (bitwise).
+    // The stage's operands are read one stage ahead of their use (ping-pong operand sets).
     const int q = lane < 6 ? lane : 0;
+    struct Ops {
+        double pv, p[6], y[6], kf0, kf1, K[12], aj[9], e;
+    };
+    auto load = [&](int k, Ops& o) __attribute__((always_inline)) {
+        o.pv = src.PV(q, k);
+#pragma unroll
+        for (int l = 0; l < 6; ++l) { o.p[l] = src.P(sy6(q, l), k); o.y[l] = src.Y(sy6(q, l), k); }
+        if (k < N) {
+            o.kf0 = src.KF(0, k);
+            o.kf1 = src.KF(1, k);
+#pragma unroll
+            for (int l = 0; l < 12; ++l) o.K[l] = src.K(l, k);
+#pragma unroll
+            for (int l = 0; l < 9; ++l) o.aj[l] = src.AJ(l, k);
+            o.e = src.CR(q, k + 1);
+        }
+    };
     double dq = -src.CR(q, 0);
-    for (int k = 0;; ++k) {
+    // one stage; returns false after the terminal stage
+    auto stage = [&](int k, const Ops& o) __attribute__((always_inline)) -> bool {
         double d[6];
         d[0] = rowbc<0>(dq); d[1] = rowbc<1>(dq); d[2] = rowbc<2>(dq);
         d[3] = rowbc<3>(dq); d[4] = rowbc<4>(dq); d[5] = rowbc<5>(dq);
-        double bq = src.PV(q, k);
+        double bq = o.pv;
 #pragma unroll
-        for (int l = 0; l < 6; ++l) bq = fma(src.P(sy6(q, l), k), d[l], bq);
+        for (int l = 0; l < 6; ++l) bq = fma(o.p[l], d[l], bq);
         double bv[6];
         bv[0] = rowbc<0>(bq); bv[1] = rowbc<1>(bq); bv[2] = rowbc<2>(bq);
         bv[3] = rowbc<3>(bq); bv[4] = rowbc<4>(bq); bv[5] = rowbc<5>(bq);
         {
             double t = 0.0;
 #pragma unroll
-            for (int l = 0; l < 6; ++l) t = fma(src.Y(sy6(q, l), k), bv[l], t);
+            for (int l = 0; l < 6; ++l) t = fma(o.y[l], bv[l], t);
             dq -= t;
         }
         d[0] = rowbc<0>(dq); d[1] = rowbc<1>(dq); d[2] = rowbc<2>(dq);
         d[3] = rowbc<3>(dq); d[4] = rowbc<4>(dq); d[5] = rowbc<5>(dq);
         {
-            double t = src.PV(q, k);
+            double t = o.pv;
 #pragma unroll
-            for (int l = 0; l < 6; ++l) t = fma(src.P(sy6(q, l), k), d[l], t);
+            for (int l = 0; l < 6; ++l) t = fma(o.p[l], d[l], t);
             if (lane < 6) {
                 vw.S(S_YCP + 6 * buf + q, k) = -t;
                 vw.S(S_DX + 6 * buf + q, k) = dq;
             }
         }
-        if (k == N) break;
-        double du0 = src.KF(0, k), du1 = src.KF(1, k);
+        if (k == N) return false;
+        double du0 = o.kf0, du1 = o.kf1;
 #pragma unroll
         for (int l = 0; l < 6; ++l) {
-            du0 = fma(src.K(l, k), d[l], du0);
-            du1 = fma(src.K(6 + l, k), d[l], du1);
+            du0 = fma(o.K[l], d[l], du0);
+            du1 = fma(o.K[6 + l], d[l], du1);
         }
         if (lane == 0) {
             vw.S(S_DU + 2 * buf, k) = du0;
             vw.S(S_DU + 2 * buf + 1, k) = du1;
         }
-        double aj[9];
-#pragma unroll
-        for (int l = 0; l < 9; ++l) aj[l] = src.AJ(l, k);
-        const double eq = src.CR(q, k + 1);
+        const double* aj = o.aj;
+        const double eq = o.e;
         const double n0 = (d[0] - eq) + fma(aj[0], d[2], aj[1] * d[5]);
         const double n1 = (d[1] - eq) + fma(aj[2], d[2], aj[3] * d[5]);
         const double n2 = (d[2] - eq) + fma(aj[4], d[4], aj[5] * d[5]);
@@ -1756,64 +1770,16 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf)
         const double n4 = (d[4] - eq) + dt * du1;
         const double n5 = (d[5] - eq) + dt * du0;
         dq = q == 0 ? n0 : q == 1 ? n1 : q == 2 ? n2 : q == 3 ? n3 : q == 4 ? n4 : n5;
+        return true;
+    };
+    Ops oa, ob;
+    load(0, oa);
+    for (int k = 0;; k += 2) {
+        if (k + 1 <= N) load(k + 1, ob);
+        if (!stage(k, oa)) break;
+        if (k + 2 <= N) load(k + 2, oa);
+        if (!stage(k + 1, ob)) break;
     }
-#else
-    const int r = lane < 6 ? lane : 0;
-    double dx[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) dx[q] = -src.CR(q, 0);
-    for (int k = 0;; ++k) {
-        double b[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            double t = src.PV(q, k);
-#pragma unroll
-            for (int l = 0; l < 6; ++l) t = fma(src.P(sy6(q, l), k), dx[l], t);
-            b[q] = t;
-        }
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            double t = 0.0;
-#pragma unroll
-            for (int l = 0; l < 6; ++l) t = fma(src.Y(sy6(q, l), k), b[l], t);
-            dx[q] -= t;
-        }
-        if (lane < 6) {
-            double t = src.PV(r, k), dxr = dx[0];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) t = fma(src.P(sy6(r, q), k), dx[q], t);
-#pragma unroll
-            for (int q = 1; q < 6; ++q) dxr = r == q ? dx[q] : dxr;
-            vw.S(S_YCP + 6 * buf + r, k) = -t;
-            vw.S(S_DX + 6 * buf + r, k) = dxr;
-        }
-        if (k == N) break;
-        double du0 = src.KF(0, k), du1 = src.KF(1, k);
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            du0 = fma(src.K(q, k), dx[q], du0);
-            du1 = fma(src.K(6 + q, k), dx[q], du1);
-        }
-        if (lane == 0) {
-            vw.S(S_DU + 2 * buf, k) = du0;
-            vw.S(S_DU + 2 * buf + 1, k) = du1;
-        }
-        double aj[9], e[6];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) aj[q] = src.AJ(q, k);
-#pragma unroll
-        for (int q = 0; q < 6; ++q) e[q] = src.CR(q, k + 1);
-        double nx[6];
-        nx[0] = (dx[0] - e[0]) + fma(aj[0], dx[2], aj[1] * dx[5]);
-        nx[1] = (dx[1] - e[1]) + fma(aj[2], dx[2], aj[3] * dx[5]);
-        nx[2] = (dx[2] - e[2]) + fma(aj[4], dx[4], aj[5] * dx[5]);
-        nx[3] = (dx[3] - e[3]) + fma(aj[6], dx[3], fma(aj[7], dx[4], aj[8] * dx[5]));
-        nx[4] = (dx[4] - e[4]) + dt * du1;
-        nx[5] = (dx[5] - e[5]) + dt * du0;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) dx[q] = nx[q];
-    }
-#endif
 }
 
 // elastic-pair step of one row from its new multiplier: dp = (y+ - g_p)/D_p, dn = (-y+ - g_n)/D_n, plus
@@ -2925,100 +2891,76 @@ __device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft
         for (int i = 0; i < 9; ++i) r[65 + i] = aj[i];
     }
 }
+// operands of one stage of the vector sweep (lane q's row), loaded one stage ahead of its use
+struct VecOps {
+    double w, py[6], rv0, rv1, gi0, gi1, gi2, qv, k0, k1, dj[9];
+};
+template <class Src>
+__device__ __forceinline__ void vec_ops(const Src& src, int k, int q, bool soft, VecOps& o) {
+    const int km = k - 1;
+    o.w = src.W(q, k);
+#pragma unroll
+    for (int l = 0; l < 6; ++l) o.py[l] = soft ? src.PY(q, l, k) : 0.0;
+    o.rv0 = src.RV(0, km);
+    o.rv1 = src.RV(1, km);
+    o.gi0 = src.GI(0, km);
+    o.gi1 = src.GI(1, km);
+    o.gi2 = src.GI(2, km);
+    o.qv = src.QV(q, km);
+    o.k0 = src.K(q, km);
+    o.k1 = src.K(6 + q, km);
+#pragma unroll
+    for (int e = 0; e < 9; ++e) o.dj[e] = src.AJ(e, km);
+}
+// lanes 0..5 hold p[q] (q = lane); the serial chain per stage is sv -> (soft: 6 broadcasts, 6 FMAs) -> 6 broadcasts of
+// p' -> np, with only the lane's own row of PY, K, QV and W read from LDS, one stage ahead (ping-pong operand sets)
 template <class Src>
 __device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft) {
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
-#if OBCA_VEC_DPP
-    // lanes 0..5 hold p[q] (q = lane); the serial chain per stage is sv -> (soft: 6 broadcasts, 6 FMAs) -> 6
-    // broadcasts of p' -> np, with only the lane's own row of PY, K, QV and W read from LDS
     const int q = lane < 6 ? lane : 0;
     double pq = src.QV(q, N);
     if (lane < 6) vw.S(S_PV + q, N) = pq;
-    for (int k = N; k >= 1; --k) {
+    auto stage = [&](int k, const VecOps& o) __attribute__((always_inline)) {
         const int km = k - 1;
-        const double sv = pq - src.W(q, k);
+        const double sv = pq - o.w;
         double pp = sv;
         if (soft) {
             double t = sv;
-            t = fma(-src.PY(q, 0, k), rowbc<0>(sv), t);
-            t = fma(-src.PY(q, 1, k), rowbc<1>(sv), t);
-            t = fma(-src.PY(q, 2, k), rowbc<2>(sv), t);
-            t = fma(-src.PY(q, 3, k), rowbc<3>(sv), t);
-            t = fma(-src.PY(q, 4, k), rowbc<4>(sv), t);
-            t = fma(-src.PY(q, 5, k), rowbc<5>(sv), t);
+            t = fma(-o.py[0], rowbc<0>(sv), t);
+            t = fma(-o.py[1], rowbc<1>(sv), t);
+            t = fma(-o.py[2], rowbc<2>(sv), t);
+            t = fma(-o.py[3], rowbc<3>(sv), t);
+            t = fma(-o.py[4], rowbc<4>(sv), t);
+            t = fma(-o.py[5], rowbc<5>(sv), t);
             pp = t;
         }
         const double pp0 = rowbc<0>(pp), pp1 = rowbc<1>(pp), pp2 = rowbc<2>(pp), pp3 = rowbc<3>(pp);
         const double pp4 = rowbc<4>(pp), pp5 = rowbc<5>(pp);
-        const double g0 = fma(dt, pp5, src.RV(0, km)), g1 = fma(dt, pp4, src.RV(1, km));
-        const double gi0 = src.GI(0, km), gi1 = src.GI(1, km), gi2 = src.GI(2, km);
-        const double kf0 = -fma(gi0, g0, gi1 * g1), kf1 = -fma(gi1, g0, gi2 * g1);
-        double np = src.QV(q, km) + pp + fma(src.K(q, km), g0, src.K(6 + q, km) * g1);
+        const double g0 = fma(dt, pp5, o.rv0), g1 = fma(dt, pp4, o.rv1);
+        const double kf0 = -fma(o.gi0, g0, o.gi1 * g1), kf1 = -fma(o.gi1, g0, o.gi2 * g1);
+        double np = o.qv + pp + fma(o.k0, g0, o.k1 * g1);
         // D' p' (D: 0:(0,2) 1:(0,5) 2:(1,2) 3:(1,5) 4:(2,4) 5:(2,5) 6:(3,3) 7:(3,4) 8:(3,5)): the lane's own row
-        double dj[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) dj[e] = src.AJ(e, km);
         // (row 3 as the contracted np[3] += dj[6] * pp[3] of the redundant version: bitwise the same)
+        const double* dj = o.dj;
         const double t2 = fma(dj[0], pp0, dj[2] * pp1), t4 = fma(dj[4], pp2, dj[7] * pp3);
         const double t5 = fma(dj[1], pp0, fma(dj[3], pp1, fma(dj[5], pp2, dj[8] * pp3)));
         np = q == 2 ? np + t2 : q == 3 ? fma(dj[6], pp3, np) : q == 4 ? np + t4 : q == 5 ? np + t5 : np;
         if (lane < 6) vw.S(S_PV + q, km) = np;
         if (lane == 0) { vw.S(S_KF, km) = kf0; vw.S(S_KF + 1, km) = kf1; }
         pq = np;
-    }
-#else
-    const int r = lane < 6 ? lane : 0;
-    auto pick = [&](const double* v) {
-        double t = v[0];
-#pragma unroll
-        for (int q = 1; q < 6; ++q) t = r == q ? v[q] : t;
-        return t;
     };
-    double p[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) p[q] = src.QV(q, N);
-    if (lane < 6) vw.S(S_PV + r, N) = pick(p);
-    for (int k = N; k >= 1; --k) {
-        const int km = k - 1;
-        double sv[6], pp[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) sv[q] = p[q] - src.W(q, k);
-        if (soft) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                double t = sv[i];
-#pragma unroll
-                for (int l = 0; l < 6; ++l) t = fma(-src.PY(i, l, k), sv[l], t);
-                pp[i] = t;
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 6; ++q) pp[q] = sv[q];
-        }
-        const double g0 = fma(dt, pp[5], src.RV(0, km)), g1 = fma(dt, pp[4], src.RV(1, km));
-        const double gi0 = src.GI(0, km), gi1 = src.GI(1, km), gi2 = src.GI(2, km);
-        const double kf0 = -fma(gi0, g0, gi1 * g1), kf1 = -fma(gi1, g0, gi2 * g1);
-        double dj[9], kk[12];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) dj[q] = src.AJ(q, km);
-#pragma unroll
-        for (int q = 0; q < 12; ++q) kk[q] = src.K(q, km);
-        double np[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) np[q] = src.QV(q, km) + pp[q] + fma(kk[q], g0, kk[6 + q] * g1);
-        // D' p' (D: 0:(0,2) 1:(0,5) 2:(1,2) 3:(1,5) 4:(2,4) 5:(2,5) 6:(3,3) 7:(3,4) 8:(3,5))
-        np[2] += fma(dj[0], pp[0], dj[2] * pp[1]);
-        np[3] += dj[6] * pp[3];
-        np[4] += fma(dj[4], pp[2], dj[7] * pp[3]);
-        np[5] += fma(dj[1], pp[0], fma(dj[3], pp[1], fma(dj[5], pp[2], dj[8] * pp[3])));
-        if (lane < 6) vw.S(S_PV + r, km) = pick(np);
-        if (lane == 0) { vw.S(S_KF, km) = kf0; vw.S(S_KF + 1, km) = kf1; }
-#pragma unroll
-        for (int q = 0; q < 6; ++q) p[q] = np[q];
+    VecOps oa, ob;
+    int k = N;
+    if (k >= 1) vec_ops(src, k, q, soft, oa);
+    for (; k - 1 >= 1; k -= 2) {
+        vec_ops(src, k - 1, q, soft, ob);
+        stage(k, oa);
+        if (k - 2 >= 1) vec_ops(src, k - 2, q, soft, oa);
+        stage(k - 1, ob);
     }
-#endif
+    if (k >= 1) stage(k, oa);
 }
 
 // ---- residuals of the un-condensed Newton rows at the step in buffer buf (+ the correction's right-hand side) ----
