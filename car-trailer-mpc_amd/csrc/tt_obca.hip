@@ -2990,7 +2990,6 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         const bool st = k < N;
         double x[6], dx[6], yp[6], ypn[6] = {0, 0, 0, 0, 0, 0}, dj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, wd[7] = {0, 0, 0, 0, 0, 0, 0};
-        double u[2] = {0.0, 0.0}, du[2] = {0.0, 0.0};
         load_x(c, k, x);
 #pragma unroll
         for (int i = 0; i < 6; ++i) { dx[i] = vw.S(S_DX + 6 * buf + i, k); yp[i] = vw.S(S_YCP + 6 * buf + i, k); }
@@ -3001,8 +3000,6 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
             for (int i = 0; i < 9; ++i) dj[i] = vw.S(S_AJ + i, k);
 #pragma unroll
             for (int i = 0; i < 7; ++i) wd[i] = vw.S(S_WD + i, k);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) { u[i] = vw.S(S_U + i, k); du[i] = vw.S(S_DU + 2 * buf + i, k); }
         }
         // ---- x rows (without the block terms, added below) ----
         double rx[6];
@@ -3045,89 +3042,6 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         rx[3] -= dj[6] * ypn[3];
         rx[4] -= dj[4] * ypn[2] + dj[7] * ypn[3];
         rx[5] -= dj[1] * ypn[0] + dj[3] * ypn[1] + dj[5] * ypn[2] + dj[8] * ypn[3];
-        // ---- u rows ----
-        double ru[2] = {0.0, 0.0};
-        if (st)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const double uv = u[i], d = du[i];
-                double g = vw.S(S_GU + i, k), sg = dw + (rs ? zeta * vw.S(S_DRU + i, k) : 0.0);
-                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(uv)));
-                if (c.hlu(i)) {
-                    const double is = inv(uv - c.ul[i]), z = vw.S(S_ZLU + i, k);
-                    g -= mu * is;
-                    sg += z * is;
-                    ftb_lo(uv, c.ul[i], d, tau, ap);
-                    dual(z, mu * is - z - z * is * d);
-                }
-                if (c.huu(i)) {
-                    const double is = inv(c.uu[i] - uv), z = vw.S(S_ZUU + i, k);
-                    g += mu * is;
-                    sg += z * is;
-                    ftb_hi(uv, c.uu[i], d, tau, ap);
-                    dual(z, mu * is - z + z * is * d);
-                }
-                Dm += g * d;
-                double t = Bc(g) + sg * d - dt * ypn[i == 0 ? 5 : 4];
-                if (!rs) t += (i == 0 ? 2.0 * a.R[0] * du[0] + (a.R[1] + a.R[2]) * du[1]
-                                      : (a.R[1] + a.R[2]) * du[0] + 2.0 * a.R[3] * du[1]);
-                ru[i] = R(t);
-            }
-        // ---- dynamics rows of stage k: c_k (+ delta_c y_k) + dx_k - A_{k-1} dx_{k-1} - B du_{k-1} (- dp + dn)
-        // (- delta_c y+_k) ----
-        double rc[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const double cr = vw.S(S_CR + i, k);
-            rc[i] = Bc(dc > 0.0 ? fma(dc, (double)vw.S(S_YC + i, k), cr) : cr) + dx[i];
-        }
-        if (k > 0) {
-            double dxp[6], ajp[9];
-#pragma unroll
-            for (int i = 0; i < 6; ++i) dxp[i] = vw.S(S_DX + 6 * buf + i, k - 1);
-#pragma unroll
-            for (int i = 0; i < 9; ++i) ajp[i] = vw.S(S_AJ + i, k - 1);
-            const double dup0 = vw.S(S_DU + 2 * buf, k - 1), dup1 = vw.S(S_DU + 2 * buf + 1, k - 1);
-            rc[0] -= dxp[0] + fma(ajp[0], dxp[2], ajp[1] * dxp[5]);
-            rc[1] -= dxp[1] + fma(ajp[2], dxp[2], ajp[3] * dxp[5]);
-            rc[2] -= dxp[2] + fma(ajp[4], dxp[4], ajp[5] * dxp[5]);
-            rc[3] -= dxp[3] + fma(ajp[6], dxp[3], fma(ajp[7], dxp[4], ajp[8] * dxp[5]));
-            rc[4] -= dxp[4] + dt * dup1;
-            rc[5] -= dxp[5] + dt * dup0;
-        }
-        double rpc[6] = {0, 0, 0, 0, 0, 0}, rnc[6] = {0, 0, 0, 0, 0, 0}, gpnc[6] = {0, 0, 0, 0, 0, 0};
-        if (rs)
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const double p = vw.S(S_PR + i, k), n = vw.S(S_NR + i, k), zp = vw.S(S_ZP + i, k), zn = vw.S(S_ZN + i, k);
-                const double ip = inv(p), in_ = inv(n);
-                const double Dp = zp * ip + dw, Dn = zn * in_ + dw, gp = RHO - mu * ip, gn = RHO - mu * in_;
-                double dp, dn;
-                if (mode == NR_MAIN) {  // the pair's step from the new multiplier (phase_recover's pn_step)
-                    dp = (yp[i] - gp) / Dp;
-                    dn = (-yp[i] - gn) / Dn;
-                    vw.S(S_DP + 6 * buf + i, k) = dp;
-                    vw.S(S_DN + 6 * buf + i, k) = dn;
-                } else {
-                    dp = vw.S(S_DP + 6 * buf + i, k);
-                    dn = vw.S(S_DN + 6 * buf + i, k);
-                }
-                rc[i] += -dp + dn;
-                rpc[i] = R(Bc(gp) + Dp * dp - yp[i]);
-                rnc[i] = R(Bc(gn) + Dn * dn + yp[i]);
-                gpnc[i] = rpc[i] / Dp - rnc[i] / Dn;
-                ftb_lo(p, 0.0, dp, tau, ap);
-                ftb_lo(n, 0.0, dn, tau, ap);
-                dual(zp, mu * ip - zp - zp * ip * dp);
-                dual(zn, mu * in_ - zn - zn * in_ * dn);
-                Dm += gp * dp + gn * dn;
-                rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
-            }
-        if (dc > 0.0)
-#pragma unroll
-            for (int i = 0; i < 6; ++i) rc[i] -= dc * yp[i];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) R(rc[i]);
         // ---- OBCA blocks ----
         double q4[4] = {0, 0, 0, 0};
         const Trig tr = stage_trig(x);
@@ -3289,6 +3203,96 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
                 }
             }
         }
+        // ---- u rows (after the blocks: their operands are re-read rather than kept live across the block loop) ----
+        double yq[6], yn4 = 0.0, yn5 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) yq[i] = vw.S(S_YCP + 6 * buf + i, k);
+        if (st) { yn4 = vw.S(S_YCP + 6 * buf + 4, k + 1); yn5 = vw.S(S_YCP + 6 * buf + 5, k + 1); }
+        double ru[2] = {0.0, 0.0}, u[2] = {0.0, 0.0}, du[2] = {0.0, 0.0};
+        if (st)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { u[i] = vw.S(S_U + i, k); du[i] = vw.S(S_DU + 2 * buf + i, k); }
+        if (st)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const double uv = u[i], d = du[i];
+                double g = vw.S(S_GU + i, k), sg = dw + (rs ? zeta * vw.S(S_DRU + i, k) : 0.0);
+                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(uv)));
+                if (c.hlu(i)) {
+                    const double is = inv(uv - c.ul[i]), z = vw.S(S_ZLU + i, k);
+                    g -= mu * is;
+                    sg += z * is;
+                    ftb_lo(uv, c.ul[i], d, tau, ap);
+                    dual(z, mu * is - z - z * is * d);
+                }
+                if (c.huu(i)) {
+                    const double is = inv(c.uu[i] - uv), z = vw.S(S_ZUU + i, k);
+                    g += mu * is;
+                    sg += z * is;
+                    ftb_hi(uv, c.uu[i], d, tau, ap);
+                    dual(z, mu * is - z + z * is * d);
+                }
+                Dm += g * d;
+                double t = Bc(g) + sg * d - dt * (i == 0 ? yn5 : yn4);
+                if (!rs) t += (i == 0 ? 2.0 * a.R[0] * du[0] + (a.R[1] + a.R[2]) * du[1]
+                                      : (a.R[1] + a.R[2]) * du[0] + 2.0 * a.R[3] * du[1]);
+                ru[i] = R(t);
+            }
+        // ---- dynamics rows of stage k: c_k (+ delta_c y_k) + dx_k - A_{k-1} dx_{k-1} - B du_{k-1} (- dp + dn)
+        // (- delta_c y+_k) ----
+        double rc[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const double cr = vw.S(S_CR + i, k);
+            rc[i] = Bc(dc > 0.0 ? fma(dc, (double)vw.S(S_YC + i, k), cr) : cr) + dx[i];
+        }
+        if (k > 0) {
+            double dxp[6], ajp[9];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dxp[i] = vw.S(S_DX + 6 * buf + i, k - 1);
+#pragma unroll
+            for (int i = 0; i < 9; ++i) ajp[i] = vw.S(S_AJ + i, k - 1);
+            const double dup0 = vw.S(S_DU + 2 * buf, k - 1), dup1 = vw.S(S_DU + 2 * buf + 1, k - 1);
+            rc[0] -= dxp[0] + fma(ajp[0], dxp[2], ajp[1] * dxp[5]);
+            rc[1] -= dxp[1] + fma(ajp[2], dxp[2], ajp[3] * dxp[5]);
+            rc[2] -= dxp[2] + fma(ajp[4], dxp[4], ajp[5] * dxp[5]);
+            rc[3] -= dxp[3] + fma(ajp[6], dxp[3], fma(ajp[7], dxp[4], ajp[8] * dxp[5]));
+            rc[4] -= dxp[4] + dt * dup1;
+            rc[5] -= dxp[5] + dt * dup0;
+        }
+        double rpc[6] = {0, 0, 0, 0, 0, 0}, rnc[6] = {0, 0, 0, 0, 0, 0}, gpnc[6] = {0, 0, 0, 0, 0, 0};
+        if (rs)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double p = vw.S(S_PR + i, k), n = vw.S(S_NR + i, k), zp = vw.S(S_ZP + i, k), zn = vw.S(S_ZN + i, k);
+                const double ip = inv(p), in_ = inv(n);
+                const double Dp = zp * ip + dw, Dn = zn * in_ + dw, gp = RHO - mu * ip, gn = RHO - mu * in_;
+                double dp, dn;
+                if (mode == NR_MAIN) {  // the pair's step from the new multiplier (phase_recover's pn_step)
+                    dp = (yq[i] - gp) / Dp;
+                    dn = (-yq[i] - gn) / Dn;
+                    vw.S(S_DP + 6 * buf + i, k) = dp;
+                    vw.S(S_DN + 6 * buf + i, k) = dn;
+                } else {
+                    dp = vw.S(S_DP + 6 * buf + i, k);
+                    dn = vw.S(S_DN + 6 * buf + i, k);
+                }
+                rc[i] += -dp + dn;
+                rpc[i] = R(Bc(gp) + Dp * dp - yq[i]);
+                rnc[i] = R(Bc(gn) + Dn * dn + yq[i]);
+                gpnc[i] = rpc[i] / Dp - rnc[i] / Dn;
+                ftb_lo(p, 0.0, dp, tau, ap);
+                ftb_lo(n, 0.0, dn, tau, ap);
+                dual(zp, mu * ip - zp - zp * ip * dp);
+                dual(zn, mu * in_ - zn - zn * in_ * dn);
+                Dm += gp * dp + gn * dn;
+                rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
+            }
+        if (dc > 0.0)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) rc[i] -= dc * yq[i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) R(rc[i]);
         // ---- final rows (plan mode, stage N) ----
         double qf[6] = {0, 0, 0, 0, 0, 0};
         if (k == N && plan)
