@@ -993,17 +993,18 @@ __device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, d
         const Trig tr = stage_trig(x);
         // only the stage contributions leave this pass: the recovery passes recompute the elimination
         // (block_refactor), so a failed inertia attempt costs the block reads and no stores
-        BlkIn cur;  // block j+1's inputs are loaded during block j
-        load_blk_in(c, rs, 0, k, cur);
+        // (each block's inputs are loaded at its start: loading block j+1's during block j measured 3.8 % slower
+        // once the pass spills, profiles/r04/factor_nopf/)
         for (int j = 0; j < c.nbk; ++j) {
             Blk bk;
             bk.m = c.slab + threadIdx.x;
             double fw[8], zf[8], t4[4];
+            BlkIn cur;
+            load_blk_in(c, rs, j, k, cur);
             const int f = block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
             if (f == F_ZERO) fail[0] = 1.0;
             if (f == F_MANY) fail[1] = 1.0;
             if (f == F_FEW) fail[2] = 1.0;
-            if (j + 1 < c.nbk) load_blk_in(c, rs, j + 1, k, cur);
         }
         double Qs[21], qv[6];
         const double sc = (k == N && plan) ? a.tfac : 1.0;
