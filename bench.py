@@ -279,14 +279,16 @@ def main():
     traffic = None
     traffic_src = None
     csvs = [p for p in args.traffic_csv.split(",") if p]
-    prof = REPO / "profiles" / "r02" / f"track_{TRAFFIC_COMMIT}"
+    src_note = ""
     if not csvs and (args.config, B, N) in (("c2", 1024, 20), ("c3", 8192, 40)):
-        csvs = [str(prof / f"{pas}_{args.config}_counter_collection.csv") for pas in ("fetch", "write")]
+        d = REPO / TRACK_PMC[args.config]
+        csvs = [str(d / pas / f"{pas}_counter_collection.csv") for pas in ("fetch", "write")]
+        src_note = f" (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of this bench config; HBM bytes per " \
+                   f"launch; {TRACK_PMC_SOURCE})"
     if csvs and all(Path(p).exists() for p in csvs):
         traffic = read_traffic(csvs)
         traffic_src = ", ".join(str(Path(p).relative_to(REPO)) if str(p).startswith(str(REPO)) else p for p in csvs) + \
-            f" (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes of this bench config at commit " \
-            f"{TRAFFIC_COMMIT}; HBM bytes per launch; profiles/r02/track_{TRAFFIC_COMMIT}/SOURCE.txt)"
+            src_note
     out = {
         "metric": "MPC solves/sec (N=20, nx=6, nu=2; BASELINE label says nx=5, the reference model has 6 states)"
         if N == 20 else f"MPC solves/sec (N={N}, nx=6, nu=2)",
@@ -783,15 +785,16 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
                       f"threads on {ncores} visible host cores; oracle/c/tt_obca.c (same restated IPOPT)"}
 
 
-# commit whose rocprofv3 PMC passes the default C2 / C3 lines quote as roofline.traffic (the kernel has not
-# changed since; re-profile with tools/gpu_track_prof.sh after a kernel change)
-TRAFFIC_COMMIT = "fcd2080"
+# rocprofv3 PMC passes (tools/hbm_passes.sh) that the default C2 / C3 lines quote as roofline.traffic: the kernel
+# the bench runs; re-profile after a tracking-kernel change
+TRACK_PMC = {"c2": "profiles/r04/final/pmc_c2", "c3": "profiles/r04/final/pmc_c3"}
+TRACK_PMC_SOURCE = "profiles/r04/final/SOURCE.txt"
 
 
 # committed PMC passes of obca_kernel (tools/obca_pmc.sh, one short probe per config on the shipped kernel): HBM bytes per
 # instance-iteration, scaled by a launch's summed IPM iterations for roofline.traffic of the OBCA lines -- an estimate
 # (the probe's iteration mix is not the full launch's), flagged as such in the line (traffic_estimated)
-OBCA_PMC = {"c4": "profiles/r04/pmc_c4", "c4all": "profiles/r04/pmc_c4all", "cobs": "profiles/r04/pmc_cobs"}
+OBCA_PMC = {"c4": "profiles/r04/final/pmc_c4", "c4all": "profiles/r04/final/pmc_c4all", "cobs": "profiles/r04/final/pmc_cobs"}
 
 
 def obca_traffic(cfg, iters_sum):
