@@ -38,12 +38,6 @@
 // (block_refactor); with contraction fixed by the source they are bitwise the same computation.
 #pragma clang fp contract(on)
 
-// A/B switch: the block elimination divides through shared reciprocals (v_rcp_f64 + two Newton steps, <= 1 ulp) and
-// takes 1/sqrt by v_rsq_f64 + Newton (1), or by IEEE division / sqrt (0, the default since round 4: the oracle
-// divides, and the GPU-vs-oracle status agreement is measured closer with it, profiles/r04/parity/)
-#ifndef OBCA_RCP
-#define OBCA_RCP 0
-#endif
 
 namespace ttmpc {
 namespace {
@@ -196,24 +190,12 @@ __device__ __forceinline__ double frcp(double x) {
     return fma(r, e, r);
 }
 
-// 1/x for the barrier terms: frcp (OBCA_RCP) or IEEE division
+// 1/x for the barrier terms: IEEE division (the oracle divides; round 3's shared reciprocals cost the GPU-vs-oracle
+// agreement and were removed in round 4)
 __device__ __forceinline__ double inv(double x) {
-#if OBCA_RCP
-    return frcp(x);
-#else
     return 1.0 / x;
-#endif
 }
 
-#if OBCA_RCP
-// 1/sqrt(x) by v_rsq_f64 + two Newton steps (x finite, positive, normal)
-__device__ __forceinline__ double frsqrt(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    const double hx = 0.5 * x;
-    y = y * fma(-hx * y, y, 1.5);
-    return y * fma(-hx * y, y, 1.5);
-}
-#endif
 
 // row_newbcast:l (gfx90a+ DPP on a 64-bit move): every lane of a 16-lane row receives lane l of that row
 template <int L_>
@@ -470,11 +452,7 @@ __device__ __forceinline__ int schol4(double* L, bool pd) {
         }
         const double sj = s > 0.0 ? 1.0 : -1.0;
         neg += s < 0.0 ? 1 : 0;
-#if OBCA_RCP
-        const double ir = frsqrt(fabs(s));
-#else
         const double ir = frcp(sqrt(fabs(s)));
-#endif
         L[lo4(j, j)] = sj * ir;
 #pragma unroll
         for (int i = j + 1; i < 4; ++i) {
@@ -535,11 +513,7 @@ __device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& 
     k.d[2] = (w[1] - w[3]) - g.sa * aa + g.ca * cc;
     k.d[3] = nr - 1.0;
     nr = fmax(nr, 1e-12);
-#if OBCA_RCP
-    const double inr = frcp(nr);
-#else
     const double inr = 1.0 / nr;
-#endif
     k.e2 = -g.sa * aa + g.ca * cc;
     k.e3 = -g.ca * aa - g.sa * cc;
     k.angp = g.angp;
@@ -563,17 +537,10 @@ __device__ __forceinline__ void blk_lin(LArgs& a, const double* xk, const Trig& 
     k.H(3, 0) = -y1 * g.dpp0 + g.angp * r0; k.H(3, 1) = -y1 * g.dpp1 + g.angp * r1;
     k.H(3, 2) = y1 * g.dpp0 - g.angp * r0;  k.H(3, 3) = y1 * g.dpp1 - g.angp * r1;
     // lam-lam block y4 T'H4T (into LL, before the diagonal is added)
-#if OBCA_RCP
-    const double in3 = inr * inr * inr;
-    k.haa = y4 * cc * cc * in3;
-    k.hac = -y4 * aa * cc * in3;
-    k.hcc = y4 * aa * aa * in3;
-#else
     const double n3 = nr * nr * nr;
     k.haa = y4 * cc * cc / n3;
     k.hac = -y4 * aa * cc / n3;
     k.hcc = y4 * aa * aa / n3;
-#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -817,18 +784,10 @@ struct PN {
 };
 __device__ __forceinline__ PN pn_terms(bool lsq, double p, double n, double zp, double zn, double mu, double dw) {
     PN t;
-#if OBCA_RCP
-    const double ip = frcp(p), in_ = frcp(n);
-    t.Dp = lsq ? 1.0 : zp * ip + dw;
-    t.Dn = lsq ? 1.0 : zn * in_ + dw;
-    t.gp = RHO - (lsq ? zp : mu * ip);
-    t.gn = RHO - (lsq ? zn : mu * in_);
-#else
     t.Dp = lsq ? 1.0 : zp / p + dw;
     t.Dn = lsq ? 1.0 : zn / n + dw;
     t.gp = RHO - (lsq ? zp : mu / p);
     t.gn = RHO - (lsq ? zn : mu / n);
-#endif
     return t;
 }
 
@@ -915,35 +874,13 @@ __device__ __forceinline__ int block_setup(const Ctx& c, const LShared& sh, cons
             hw = sh.zeta * in.drw[e];
             gw = hw * (in.w[e] - in.wr[e]);
         }
-#if OBCA_RCP
-        const double isl = frcp(sl);
-        sw[e] = lsq ? 1.0 : zw * isl + hw;
-        fw[e] = lsq ? gw - zw : gw - mu * isl;
-#else
         sw[e] = lsq ? 1.0 : zw / sl + hw;
         fw[e] = lsq ? gw - zw : gw - mu / sl;
-#endif
     }
     blk_lin(*c.a, x, tr, j, in.w, in.y, bk);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const double s = in.s[r], vl = in.vl[r], vu = in.vu[r];
-#if OBCA_RCP
-        // 1 / (rU - s) and 1 / (s - rL) shared by the row's Sigma and barrier gradient
-        const double iu = frcp(c.rU(r) - s), il = c.hrl(r) ? frcp(s - c.rL(r)) : 0.0;
-        const double sg = c.hrl(r) ? vu * iu + vl * il : vu * iu, gr = c.hrl(r) ? mu * iu - mu * il : mu * iu;
-        bk.D[r] = lsq ? 1.0 : sg + dw;
-        const double iD = frcp(bk.D[r]);
-        bk.E[r] = iD + dc;
-        const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : gr;
-        rd[r] = (dc > 0.0 ? fma(dc, in.y[r], in.dr[r]) : in.dr[r]) + gs * iD;
-        if (rs) {
-            const PN t = pn_terms(lsq, in.pr[r], in.nr[r], in.zp[r], in.zn[r], mu, dw);
-            const double ip = frcp(t.Dp), in_ = frcp(t.Dn);
-            bk.E[r] += ip + in_;
-            rd[r] += t.gp * ip - t.gn * in_;
-        }
-#else
         bk.D[r] = lsq ? 1.0 : sig_row(c, r, s, vl, vu) + dw;
         bk.E[r] = 1.0 / bk.D[r] + dc;
         const double gs = lsq ? (c.hrl(r) ? -vl : 0.0) + vu : grad_row(c, r, s, mu);
@@ -953,7 +890,6 @@ __device__ __forceinline__ int block_setup(const Ctx& c, const LShared& sh, cons
             bk.E[r] += 1.0 / t.Dp + 1.0 / t.Dn;
             rd[r] += t.gp / t.Dp - t.gn / t.Dn;
         }
-#endif
     }
     const int f = blk_factor(bk, sw, dw, C4, c.pd);
     if (f != F_OK) return f;
@@ -1300,10 +1236,11 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
         const double H0i = dt * hi.y, H1i = dt * hi.x, H0j = dt * a45.y, H1j = dt * a45.x;
         const double K0j = -fma(Gi00, H0j, Gi01 * H1j), K1j = -fma(Gi01, H0j, Gi11 * H1j);
         const double Pk = cur.qt + atpa + fma(H0i, K0j, H1i * K1j);
-        // ---- vector recursion: p' from lanes 48..53 to every lane (scalar registers)
+        // ---- vector recursion: p' from lanes 48..53 to the lanes of their 16-lane row (DPP row_newbcast; lanes 48..53
+        // and lane 48's KF / G^-1 stores are its only readers)
         double ppl[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, 48 + q);
+        ppl[0] = rowbc<0>(pp); ppl[1] = rowbc<1>(pp); ppl[2] = rowbc<2>(pp);
+        ppl[3] = rowbc<3>(pp); ppl[4] = rowbc<4>(pp); ppl[5] = rowbc<5>(pp);
         const double g0 = fma(dt, ppl[5], cur.rv0), g1 = fma(dt, ppl[4], cur.rv1);
         const double kf0 = -fma(Gi00, g0, Gi01 * g1), kf1 = -fma(Gi01, g0, Gi11 * g1);
         double cr0, cr1, cr2, cr3;
@@ -1330,7 +1267,7 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) 
             src.setPV(r, k, pnew);
             if (keep) { vw.S(S_K + r, k) = K0; vw.S(S_K + 6 + r, k) = K1; }
         }
-        if (lane == 0) {
+        if (lane == 48) {
             src.setKF(0, k, kf0);
             src.setKF(1, k, kf1);
             if (c.refine) { vw.S(S_GI, k) = Gi00; vw.S(S_GI + 1, k) = Gi01; vw.S(S_GI + 2, k) = Gi11; }
@@ -1534,11 +1471,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
             const double piv = readlane_d(mv, 7 * p);
             if (!fail && !(piv >= 2.2250738585072014e-308)) fcode = pivot_fail(piv, readlane_d(m0, 7 * p));
             const double aip = __shfl(mv, 6 * i + p), apj = __shfl(mv, 6 * p + j);
-#if OBCA_RCP
-            const double ip = frcp(piv);
-#else
             const double ip = 1.0 / piv;
-#endif
             const double nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : mv - aip * apj * ip;
             fail = fail || !(piv >= 2.2250738585072014e-308);
             mv = act ? nv : 0.0;
@@ -1558,9 +1491,10 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
             for (int l = 0; l < 6; ++l) t = fma(Pt[8 * i + l], Yt[8 * l + j], t);
             Tt[tij] = t;  // P Y
         }
+        // p of lanes 48..53 to the lanes of their row (DPP row_newbcast: the vector lanes are its only readers)
         double pl[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) pl[q] = readlane_d(pv, 48 + q);
+        pl[0] = rowbc<0>(pv); pl[1] = rowbc<1>(pv); pl[2] = rowbc<2>(pv);
+        pl[3] = rowbc<3>(pv); pl[4] = rowbc<4>(pv); pl[5] = rowbc<5>(pv);
         lds_order();
         double nP, npv = pv;
         {
@@ -1594,11 +1528,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
         const int gc = g2_code(G00, G11, det);
         if (!fail) fcode = gc;
         fail = fail || gc != F_OK;
-#if OBCA_RCP
-        const double idet = frcp(det);
-#else
         const double idet = 1.0 / det;
-#endif
         const double Gi00 = G11 * idet, Gi01 = -G01 * idet, Gi11 = G00 * idet;
         double Pk;
         {  // P_kk[ii][jj] = Q~ + (A'PA)[ii][jj] + H'K
@@ -1610,8 +1540,8 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
             Pk = o.qt + atpa + fma(H0i, K0j, H1i * K1j);
         }
         double ppl[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) ppl[q] = readlane_d(pp, 48 + q);
+        ppl[0] = rowbc<0>(pp); ppl[1] = rowbc<1>(pp); ppl[2] = rowbc<2>(pp);
+        ppl[3] = rowbc<3>(pp); ppl[4] = rowbc<4>(pp); ppl[5] = rowbc<5>(pp);
         const double g0 = fma(dt, ppl[5], o.rv0), g1 = fma(dt, ppl[4], o.rv1);
         const double kf0 = -fma(Gi00, g0, Gi01 * g1), kf1 = -fma(Gi01, g0, Gi11 * g1);
         double pnew;
@@ -1630,7 +1560,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& 
                 out.setPV(r, kk, pnew);
             }
         }
-        if (lane == 0) {
+        if (lane == 48) {
             out.setKF(0, kk, kf0);
             out.setKF(1, kk, kf1);
             if (c.refine) { vw.S(S_GI, kk) = Gi00; vw.S(S_GI + 1, kk) = Gi01; vw.S(S_GI + 2, kk) = Gi11; }
