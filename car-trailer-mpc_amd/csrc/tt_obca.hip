@@ -3401,10 +3401,7 @@ __device__ __noinline__ bool refine(const Ctx& c, LShared& sh, double mu, double
         __syncthreads();
         count(sh, on, OCNT_CORR);
         correction_solve(c, sh, mu, dw, buf);
-#ifndef OBCA_PREP_FUSE  // A/B only (bitwise check of the fusion): 0 = round 3's separate NR_STEP pass
-#define OBCA_PREP_FUSE 1
-#endif
-        prepped = OBCA_PREP_FUSE && it >= 1;
+        prepped = it >= 1;
         phase_nres(c, sh, mu, dw, tau, buf, prepped, NR_CORR, q);
         stamp(sh, on, OPH_REF_REC);
         const double ratio2 = q[0] / (fmin(q[2], 1e6) + bnorm);
