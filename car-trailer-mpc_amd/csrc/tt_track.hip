@@ -95,7 +95,6 @@ __device__ __forceinline__ double wred(double v, Op op) {
     return op(op(readlane_d(v, 0), readlane_d(v, 16)), op(readlane_d(v, 32), readlane_d(v, 48)));
 }
 __device__ __forceinline__ double wsum(double v) { return wred(v, OpSum()); }
-__device__ __forceinline__ double wmax(double v) { return wred(v, OpMax()); }
 __device__ __forceinline__ double wmin(double v) { return wred(v, OpMin()); }
 
 // Two or four reductions with one op at once.  The first log2(Q) butterfly stages (quad xor 1, xor 2)
