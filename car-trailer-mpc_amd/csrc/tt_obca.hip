@@ -1111,9 +1111,10 @@ __device__ __forceinline__ void stage_copy(const Ctx& c, double* A, Val value) {
                 v[u] = value(f, k);
             }
         }
+        lds_double* L = (lds_double*)A;  // ds_write, not flat stores (which would also queue on vmcnt)
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (d[u] >= 0) A[d[u]] = v[u];
+            if (d[u] >= 0) L[d[u]] = v[u];
     }
 }
 __device__ __noinline__ void stage_inputs(const Ctx& c, double* A) {
@@ -1174,7 +1175,7 @@ __device__ __forceinline__ void dcol(const double* dj, const ColMask& m, double&
 __device__ __forceinline__ double2 ldd2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 
 template <class Src>
-__device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src& src) {
+__device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src src) {
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt, dt2 = dt * dt;
@@ -1313,7 +1314,7 @@ __device__ __forceinline__ void fwd_ops(const Src& src, int k, FwdOps& o) {
     for (int q = 0; q < 6; ++q) o.e[q] = src.CR(q, k + 1);
 }
 template <class Src>
-__device__ __noinline__ void forward(const Ctx& c, const Src& src, int buf) {
+__device__ __noinline__ void forward(const Ctx& c, const Src src, int buf) {
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
@@ -1437,7 +1438,7 @@ __device__ __forceinline__ void soft_ops(const Src& src, int k, int i, int j, in
 }
 
 template <class Src>
-__device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src& src) {
+__device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src src) {
     const WsView vw = ws_view(c);
     const GSrc out{c};
     const int lane = threadIdx.x, N = c.N;
@@ -1627,7 +1628,7 @@ __device__ __noinline__ void stage_soft_forward(const Ctx& c, double* A, bool so
     });
 }
 template <class Src>
-__device__ __noinline__ void forward_soft(const Ctx& c, const Src& src, int buf) {
+__device__ __noinline__ void forward_soft(const Ctx& c, const Src src, int buf) {
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
@@ -2369,12 +2370,15 @@ __device__ __forceinline__ void compl_stage(const Ctx& c, const LShared& sh, int
 }
 
 template <bool RS_>
-__device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red)[13]) {
+__device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red_out)[13]) {
     LArgs& a = *c.a;
     const int N = c.N;
     const bool plan = c.plan();
     constexpr bool rs = RS_;
     const double zeta = sh.zeta;
+    // the sums accumulate in registers (the caller's array is memory that every workspace store may alias: kept there,
+    // each update was a flat load and store behind the pass's workspace stores)
+    double red[13];
 #pragma unroll
     for (int i = 0; i < 13; ++i) red[i] = 0.0;
 
@@ -2649,6 +2653,8 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
     }
     const int ops[13] = {R_MAX, R_MAX, R_MAX, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_SUM, R_MAX};
     wg_reduce(sh, red, ops);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) red_out[i] = red[i];
 }
 
 // one instantiation per problem (original / restoration phase): the original problem's skips every restoration
@@ -2846,7 +2852,7 @@ __device__ __forceinline__ void vec_ops(const Src& src, int k, int q, bool soft,
 // lanes 0..5 hold p[q] (q = lane); the serial chain per stage is sv -> (soft: 6 broadcasts, 6 FMAs) -> 6 broadcasts of
 // p' -> np, with only the lane's own row of PY, K, QV and W read from LDS, one stage ahead (ping-pong operand sets)
 template <class Src>
-__device__ __noinline__ void riccati_vec(const Ctx& c, const Src& src, bool soft) {
+__device__ __noinline__ void riccati_vec(const Ctx& c, const Src src, bool soft) {
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
