@@ -1892,6 +1892,9 @@ __device__ __noinline__ void phase_trial_t(const Ctx& c, LShared& sh, double mu,
         if (k < N)
 #pragma unroll
             for (int i = 0; i < 2; ++i) u[i] = c.S(S_U + i, k) + alpha * c.S(S_DU + 2 * buf + i, k);
+        // the tracking / plan cost first: its target loads are issued before any of the pass's stores (a load behind a
+        // store waits for it)
+        const double scost = rs ? 0.0 : stage_cost(c, k, x, u);
         LogSum ls;
         bool ok = true;
         double Fr = 0.0, prox = 0.0;  // restoration objective of this stage: rho sum(p + n), D_R-weighted distances
@@ -2026,7 +2029,7 @@ __device__ __noinline__ void phase_trial_t(const Ctx& c, LShared& sh, double mu,
                 ls.add(sl);
                 ls.add(su);
             }
-        F += rs ? RHO * Fr + 0.5 * sh.zeta * prox : stage_cost(c, k, x, u);
+        F += rs ? RHO * Fr + 0.5 * sh.zeta * prox : scost;
         if (!ok) bad = 1.0;
         else logs += ls.value();
     }
@@ -2392,6 +2395,8 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
         double objR = 0.0;  // restoration objective of this stage
         load_x(c, k, x);
         if (k < N) { u[0] = c.S(S_U, k); u[1] = c.S(S_U + 1, k); }
+        // the stage cost before any of the pass's stores (its target loads would wait for them)
+        const double cost = stage_cost(c, k, x, u);
         if (rs) {
             double prox = 0.0;
 #pragma unroll
@@ -2644,7 +2649,6 @@ __device__ __noinline__ void phase_lin_t(const Ctx& c, LShared& sh, double (&red
 #pragma unroll
             for (int i = 0; i < 7; ++i) c.S(S_WD + i, k) = wd[i];
         }
-        const double cost = stage_cost(c, k, x, u);
         red[6] += rs ? objR : cost;
         red[7] += lsum.value();
         red[10] += cost;
