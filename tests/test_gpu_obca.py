@@ -162,6 +162,23 @@ def test_obca_lockstep_with_oracle():
         assert (d <= 1e-9).sum() >= need, (K, d)
 
 
+def test_hbm_source_sweeps_lockstep():
+    """N = 230: the serial sweeps' stage records no longer fit the dynamic LDS (kObcaLdsMax), so the Riccati, forward,
+    soft and correction sweeps read their operands straight from the HBM workspace (the GSrc / SoftG / VecG / SoftFG
+    sources) -- a path no other test reaches.  Lockstep with the oracle at max_iter 25, as the census above."""
+    from oracle import c_oracle as co
+    from ttmpc import scenarios as sc
+    import json
+    obs6 = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
+    cases = json.loads((GOLDEN / "test_cases.json").read_text())["cases"]
+    N, B = 230, 8
+    x0, xg, zg = sc.obca_case_batch(cases, B, N, 6, seed=3, obstacles=obs6)
+    X, U, Z, st, it, kk = _solver(N, obs6, max_iter=25).solve(x0, xg, z_guess=zg)
+    zc, stc, itc, kkc = co.obca_solve_batch(_oracle(N, obs6, max_iter=25), x0, xg, z_guess=zg, nthreads=16)
+    d = np.abs(X - co.obca_split(zc, N, 6)[0]).max(axis=(1, 2))
+    assert np.all(np.isfinite(X)) and (d <= 1e-9).sum() >= B - 1, d
+
+
 def test_c4_replan_subset_vs_oracle():
     """Re-plans around the reference's committed plan (8 Hybrid-A*-style waypoints), reference duals."""
     from oracle import c_oracle as co
