@@ -1050,7 +1050,6 @@ __device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, d
 // staged by all four waves before the sweep (LSrc: region A = sweep inputs, region B = its outputs).
 // CR is the effective dynamics-row residual S_CE.
 struct GSrc {
-    static constexpr bool kLds = false;
     const Ctx& c;
     __device__ double QT(int i, int k) const { return c.S(S_QT + i, k); }
     __device__ double QV(int i, int k) const { return c.S(S_QV + i, k); }
@@ -1066,11 +1065,11 @@ struct GSrc {
     __device__ void setPV(int i, int k, double v) const { c.S(S_PV + i, k) = v; }
     __device__ void setK(int i, int k, double v) const { c.S(S_K + i, k) = v; }
     __device__ void setKF(int i, int k, double v) const { c.S(S_KF + i, k) = v; }
+    __device__ void setGI(int i, int k, double v) const { c.S(S_GI + i, k) = v; }
 };
-// region A per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CR 6  (47);  region B: P 21 | PV 6 | K 12 | KF 2 (41)
-constexpr int LA = 47, LB = 41;
+// region A per stage: QT 21 | QV 6 | RT 3 | RV 2 | AJ 9 | CR 6  (47);  region B: P 21 | PV 6 | K 12 | KF 2 | G^-1 3 (44)
+constexpr int LA = 47, LB = 44;
 struct LSrc {
-    static constexpr bool kLds = true;
     const lds_double* A;
     lds_double* B;
     __device__ double QT(int i, int k) const { return A[k * LA + i]; }
@@ -1087,6 +1086,8 @@ struct LSrc {
     __device__ void setPV(int i, int k, double v) const { B[k * LB + 21 + i] = v; }
     __device__ void setK(int i, int k, double v) const { B[k * LB + 27 + i] = v; }
     __device__ void setKF(int i, int k, double v) const { B[k * LB + 39 + i] = v; }
+    __device__ double GI(int i, int k) const { return B[k * LB + 41 + i]; }
+    __device__ void setGI(int i, int k, double v) const { B[k * LB + 41 + i] = v; }
 };
 __host__ __device__ inline size_t obca_lds_bytes(int N) { return (size_t)(LA + LB) * (N + 1) * 8; }  // >= the soft records (53, 77)
 constexpr size_t kObcaLdsMax = 150 * 1024;  // dynamic LDS budget for the staged sweeps (+ static Shared)
@@ -1176,7 +1177,6 @@ __device__ __forceinline__ double2 ldd2(const double* p) { return *reinterpret_c
 
 template <class Src>
 __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src src) {
-    const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt, dt2 = dt * dt;
     const bool act = lane < 36, vec = lane >= 48 && lane < 54;
@@ -1187,13 +1187,12 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src src) {
     // the two tiles as LDS-addressed arrays (ds_read / ds_write, not flat accesses through `sh`)
     __shared__ __attribute__((aligned(16))) double P[48];   // P_{k+1}, row-major, row stride 8
     __shared__ __attribute__((aligned(16))) double PT[48];  // PA transposed: PT[8 j + r] = PA[r][j]
-    // with refinement the factorisation (P, K, G^-1) also goes to the HBM workspace: the correction solves reuse it
-    const bool keep = Src::kLds && c.refine;
+    // with refinement the factorisation (P, K, G^-1) also goes to the HBM workspace for the correction solves: from the
+    // LDS record by keep_factors (waves 1-3, during the forward sweep), so the serial sweep issues no HBM stores
     if (act) {
         const double q = src.QT(sij, N);
         P[8 * i + j] = q;
         if (i <= j) src.setP(sij, N, q);
-        if (keep && i <= j) vw.S(S_P + sij, N) = q;
     }
     double pv = vec ? src.QV(r, N) : 0.0;
     if (vec) src.setPV(r, N, pv);
@@ -1258,7 +1257,6 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src src) {
         if (act) {
             P[8 * i + j] = Pk;
             if (i <= j) src.setP(sij, k, Pk);
-            if (keep && i <= j) vw.S(S_P + sij, k) = Pk;
         }
         if (vec) {
             const double H0 = dt * hi.y, H1 = dt * hi.x;
@@ -1266,12 +1264,11 @@ __device__ __noinline__ void riccati(const Ctx& c, LShared& sh, const Src src) {
             src.setK(r, k, K0);
             src.setK(6 + r, k, K1);
             src.setPV(r, k, pnew);
-            if (keep) { vw.S(S_K + r, k) = K0; vw.S(S_K + 6 + r, k) = K1; }
         }
         if (lane == 48) {
             src.setKF(0, k, kf0);
             src.setKF(1, k, kf1);
-            if (c.refine) { vw.S(S_GI, k) = Gi00; vw.S(S_GI + 1, k) = Gi01; vw.S(S_GI + 2, k) = Gi11; }
+            if (c.refine) { src.setGI(0, k, Gi00); src.setGI(1, k, Gi01); src.setGI(2, k, Gi11); }
         }
         pv = pnew;
         asm volatile("" ::: "memory");
@@ -2683,6 +2680,23 @@ __device__ __noinline__ double2 phase_compl(const Ctx& c, LShared& sh, double mu
 // Returns false when the Riccati/blocks are not positive definite.
 // One factorisation + condensed solve with the perturbations (dw, dc) into step buffer buf: F_OK, or the outcome of the
 // failed factorisation (F_MANY / F_ZERO / F_FEW) for the perturbation handler.
+// the Riccati factors of the LDS record (region B) to the HBM workspace (S_P, S_K, S_GI) for the refinement's correction
+// solves: threads 64..255, field-major (consecutive k on consecutive lanes: coalesced stores), while wave 0 runs the
+// forward sweep on the same (read-only) record
+__device__ __noinline__ void keep_factors(const Ctx& c, const LSrc src) {
+    const WsView vw = ws_view(c);
+    const int NP = c.NP, N = c.N, nt = T - 64;
+    constexpr int NF = 21 + 12 + 3;
+    for (int idx = (int)threadIdx.x - 64; idx < NF * NP; idx += nt) {
+        const int f = idx / NP, k = idx - f * NP;
+        if (f < 21) vw.S(S_P + f, k) = src.P(f, k);
+        else if (k < N) {
+            if (f < 33) vw.S(S_K + f - 21, k) = src.K(f - 21, k);
+            else vw.S(S_GI + f - 33, k) = src.GI(f - 33, k);
+        }
+    }
+}
+
 __device__ __noinline__ int newton_solve(const Ctx& c, LShared& sh, double mu, double dw, double dc, int buf) {
     const bool on = c.a->stamps != nullptr;
     stamp(sh, on, OPH_UPD);
@@ -2724,6 +2738,7 @@ __device__ __noinline__ int newton_solve(const Ctx& c, LShared& sh, double mu, d
         stamp(sh, on, OPH_RIC);
         if (sh.flag) return sh.flag;
         if (threadIdx.x < 64) forward(c, src, buf);
+        else if (c.refine) keep_factors(c, src);
     } else {
         const GSrc src{c};
         if (threadIdx.x < 64) riccati(c, sh, src);
