@@ -612,7 +612,7 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
 // transposed into the PA tile, so both are contiguous b128 reads).  The 16x16 f64 MFMA was measured
 // at ~185 cycles per srcC-chained link on gfx950 and runs no faster than the VALU for f64, so the
 // whole recursion stays on the VALU with ~300 cycles of dependent latency per stage.
-constexpr int hPF = 128, hPT = 192;  // P tile [8i + j] and transposed PA tile [8j + i] (64 doubles each)
+constexpr int hPF = 128, hPT = 192;  // P tile (i, j) and transposed PA tile (j, i), 64 doubles each, rows 4..7 XOR-swizzled
 
 // branch-free predicated LDS store: invalid lanes write their own dump slot
 template <int BM>
@@ -735,9 +735,15 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
     double* PF = c.sm + hPF;
     double* PT = c.sm + hPT;
+    // Both tiles swizzle rows 4..7 by XOR 4 on the column (halves swapped): a b128 read of one chunk of every row then
+    // touches 32 distinct banks (rows i and i+4 sit 64 doubles = 128 banks apart, i.e. on the same banks, unswizzled),
+    // the even pairs stay aligned, and a row is still a permutation of its 8 slots (the per-lane writes stay
+    // conflict-free).  Element (r, cidx) of a tile is at 8 r + (cidx ^ (r & 4)).
+    const int sw_i = i & 4, sw_j = j & 4;
+    const int pf_own = 8 * i + (j ^ sw_i);  // this lane's P^ entry
     // terminal P^_N = H^_N (no dynamics): padded lanes hold exact zeros
     double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
-    PF[c.lane] = Pij;
+    PF[pf_own] = Pij;
     asm volatile("" ::: "memory");
     pstore(c, m.ps >= 0, m.ps, N, Pij);
     // inertia flag accumulated without branching: a failed stage only poisons the (discarded) factors
@@ -753,9 +759,9 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     // after a tile read so that waiting for the tile never waits for the prefetch)
     auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
         // row i of P^_{k+1} and the reduced input Hessian entries (uniform)
-        const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
-        const double2 p5 = ld2(PF + 44);  // P[5][4], P[5][5]
-        const double p44 = PF[36];
+        const double2 r01v = ld2(PF + 8 * i + sw_i), r23v = ld2(PF + 8 * i + (2 ^ sw_i)), r45v = ld2(PF + 8 * i + (4 ^ sw_i));
+        const double2 p5 = ld2(PF + 40);  // P[5][4], P[5][5] (row 5: columns 4, 5 at slots 0, 1)
+        const double p44 = PF[32];        // P[4][4] (row 4: column 4 at slot 0)
         __builtin_amdgcn_sched_barrier(0);
         ep_ops_a(c, m, kn, nx);  // next stage's operands, first half
         __builtin_amdgcn_sched_barrier(0);
@@ -770,11 +776,11 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         pa = fma(r45v.x, o.dj[4], pa);
         pb = fma(r45v.y, o.dj[5], pb);
         const double PAij = pa + pb;
-        PT[8 * j + i] = PAij;
+        PT[8 * j + (i ^ sw_j)] = PAij;
         asm volatile("" ::: "memory");  // the tile is read by other lanes: keep program order
         // column j of PA (rows 0..5; rows 4, 5 also give G[.][j]) and G[.][i]
-        const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
-        const double2 gi = ld2(PT + 8 * i + 4);  // PA[4][i], PA[5][i]
+        const double2 c01 = ld2(PT + 8 * j + sw_j), c23 = ld2(PT + 8 * j + (2 ^ sw_j)), c45 = ld2(PT + 8 * j + (4 ^ sw_j));
+        const double2 gi = ld2(PT + 8 * i + (4 ^ sw_i));  // PA[4][i], PA[5][i]
         // next stage's operands, second half: issued behind the tile reads (LDS serves a wave in order)
         __builtin_amdgcn_sched_barrier(0);
         ep_ops_b(c, m, kn, dw, nx);
@@ -790,7 +796,7 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
         const double m0 = fma(i00, g0j, i01 * g1j), m1 = fma(i01, g0j, i11 * g1j);
         Pij = F - fma(g0i, m0, g1i * m1);
-        PF[c.lane] = Pij;
+        PF[pf_own] = Pij;
         asm volatile("" ::: "memory");
         // factorisation rows for the forward sweep, the step and the SOC
         c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
