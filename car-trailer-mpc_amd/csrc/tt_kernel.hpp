@@ -29,7 +29,10 @@ enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC
        kNumPhases };
 
 // LDS: fixed head + rows per stage (doubles); see tt_track.hip for the map.
-constexpr int kRowsPerStage = 117;  // 116 used + 1 zero pad (odd stride: conflict-free b64)
+// 116 used + 1 zero pad + 1 unused.  The even stride (= 2 mod 4, 944 B) keeps every stage record 16-B aligned and makes
+// the lane-pair phases' reads conflict-free (lanes 2k, 2k+1 -> rows R, R+1 of stage k); bitwise the same as 117, C2
+// -2.5 %, C3 -1.7 % (profiles/r04/stride118/).
+constexpr int kRowsPerStage = 118;
 constexpr int kTrackFilter = 16;  // filter line search entries (theta, phi) kept in the LDS head
 constexpr int kHead = 256;  // 64 head values + 32 dump slots + 2x16 filter entries + two 8x8 Riccati tiles
 constexpr int kScratch = kHead;

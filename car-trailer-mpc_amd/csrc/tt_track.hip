@@ -62,7 +62,7 @@ static_assert(HEAD >= SR, "stage -1 of the Riccati prefetch addresses head words
 // rows
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rDX = 30, rYP = 38, rAJ = 44, rGF = 53, rCC = 61, rK = 67;
 constexpr int rKF = 79, rPS = 81, rPV = 102, rDXS = 108, PAD = 116;
-static_assert(PAD + 1 == kRowsPerStage, "stage record");
+static_assert(PAD + 2 == kRowsPerStage, "stage record (one unused row keeps the stride even)");
 // second lives (see the LDS map): curvature, Sigma, dB from the linearisation to the Riccati sweep; the
 // Riccati operands diag(Sigma) + diag(W), Sigma_u and b^ = -c_{k+1} (stage k); the trial residual c
 constexpr int rWC = rDX, rSG = rPS, rDB = rPS + 8, rHD = rDXS, rSGU = rDXS + 6, rBH = rYP, rCT = rDXS;

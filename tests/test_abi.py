@@ -37,7 +37,7 @@ def test_introspection_without_gpu():
     from ttmpc import lib
     L = lib()
     assert L.tt_max_horizon() >= 60
-    assert L.tt_lds_bytes(20) == 8 * (117 * 21 + 256)
+    assert L.tt_lds_bytes(20) == 8 * (118 * 21 + 256)
     assert 4 * L.tt_lds_bytes(40) <= 160 * 1024   # C3: four N = 40 instances per CU
     assert b"gfx950" in L.tt_version()
 

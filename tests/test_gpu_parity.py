@@ -222,7 +222,7 @@ def test_reference_call_surface():
 
 
 def test_max_horizon_matches_oracle():
-    """The largest horizon whose instance fits one CU's LDS (tt_max_horizon: 117-double stage records)."""
+    """The largest horizon whose instance fits one CU's LDS (tt_max_horizon: 118-double stage records)."""
     import ttmpc
     from ttmpc.scenarios import synthetic_batch
     N = ttmpc.lib().tt_max_horizon()

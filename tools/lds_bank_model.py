@@ -2,7 +2,7 @@
 instruction, one extra LDS cycle per extra distinct address on a bank within a group).  Prints the extra cycles of
 each access of one stage (operand reads, factor-row store) and of the P / PA tile accesses.  Mirrors the row layout
 of car-trailer-mpc_amd/csrc/tt_track.hip; update both together."""
-HEAD,SR=256,117
+HEAD,SR=256,118
 rX,rY,rZL,rZU,rDX,rYP,rAJ,rGF,rCC,rK=0,8,14,22,30,38,44,53,61,67
 rKF,rPS,rPV,rDXS,PAD=79,81,102,108,116
 rWC,rSG,rDB,rHD,rSGU,rBH=rDX,rPS,rPS+8,rDXS,rDXS+6,rYP
