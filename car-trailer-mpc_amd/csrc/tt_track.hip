@@ -25,18 +25,18 @@
 //
 // LDS map (doubles).  Head (fixed offsets, immediate addressing): Qw(36) Rw(4) x_init(6) lb(8)
 // ub(8) pad(2) dump(32: per-lane sink for branch-free predicated stores), filter, Riccati tiles.  Stage
-// k row r at sm[kHead + k*117 + r]; the odd stride keeps lane-per-stage ds_read_b64 bank-conflict-free:
+// k row r at sm[kHead + k*118 + r]; the even stride keeps every record 16-B aligned (see tt_kernel.hpp):
 //   0-5 X | 6-7 U | 8-13 Y (eq. multipliers, IPOPT sign) | 14-21 zL | 22-29 zU | 30-37 dX,dU
-//   38-43 Y+ | 44-52 dt*J (9 nnz) | 53-60 grad F (+ mu dB from ric_prep on) | 61-66 c | 67-78 K
-//   79-80 k_ff | 81-101 P_k (upper) | 102-107 p_k | 108-115 dX,dU (soc) | 116 zero pad
+//   38-43 Y+ | 44-52 dt*J (9 nnz) | 53 zero pad | 54-61 grad F (+ mu dB from ric_prep on) | 62-67 c | 68-79 K
+//   80-81 k_ff | 82-102 P_k (upper) | 103 spare | 104-109 p_k | 110-117 dX,dU (soc)
 // The reference window (Xref, Uref) is read from HBM (L2-resident, stage-parallel phases only).  Rows with
 // a second life (their first owner is dead over that span of the iteration):
 //   linearise .. Riccati   30-36 curvature W (7 nnz)          [dX is produced by the forward sweep]
-//   linearise .. ric_prep  81-88 Sigma = zL/sL + zU/sU, 89-96 dB = 1/sU - 1/sL   [P_k: Riccati]
-//   ric_prep .. Riccati    108-113 diag(Sigma) + diag(W), 114-115 Sigma_u      [dX_soc: SOC]
+//   linearise .. ric_prep  82-89 Sigma = zL/sL + zU/sU, 90-97 dB = 1/sU - 1/sL   [P_k: Riccati]
+//   ric_prep .. Riccati    110-115 diag(Sigma) + diag(W), 116-117 Sigma_u      [dX_soc: SOC]
 //                          38-43 b^ = -c_{k+1}                                  [Y+: step]
-//   trial .. SOC forward   108-113 c(trial) / c_soc                             [dX_soc: SOC forward]
-// 117 rows keep four N = 40 instances (40.4 KB each) on one CU (C3).
+//   trial .. SOC forward   110-115 c(trial) / c_soc                             [dX_soc: SOC forward]
+// 118 rows keep four N = 40 instances (40.8 KB each) on one CU (C3).
 //
 // Bound pattern: template parameter BM (bit v = finite lower bound on variable v, bit 8+v = finite
 // upper bound; v = 0..5 states, 6..7 inputs) so the common patterns compile to straight-line code;
@@ -60,9 +60,11 @@ static_assert(hFTH + kTrackFilter == hFPH && hFPH + kTrackFilter <= 128, "filter
 static_assert(HEAD >= SR, "stage -1 of the Riccati prefetch addresses head words");
 // (128..255: the P and transposed-PA tiles of the Riccati sweep, see phase_riccati)
 // rows
-constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rDX = 30, rYP = 38, rAJ = 44, rGF = 53, rCC = 61, rK = 67;
-constexpr int rKF = 79, rPS = 81, rPV = 102, rDXS = 108, PAD = 116;
-static_assert(PAD + 2 == kRowsPerStage, "stage record (one unused row keeps the stride even)");
+// every multi-row block starts on an even row (the two odd-sized blocks, dt*J and P, are each followed by a single
+// row: the zero pad and the spare), so with the even stride its row pairs are 16-B aligned ds_read_b128 / ds_write_b128
+constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rDX = 30, rYP = 38, rAJ = 44, PAD = 53, rGF = 54, rCC = 62, rK = 68;
+constexpr int rKF = 80, rPS = 82, rPV = 104, rDXS = 110;
+static_assert(rDXS + 8 == kRowsPerStage, "stage record");
 // second lives (see the LDS map): curvature, Sigma, dB from the linearisation to the Riccati sweep; the
 // Riccati operands diag(Sigma) + diag(W), Sigma_u and b^ = -c_{k+1} (stage k); the trial residual c
 constexpr int rWC = rDX, rSG = rPS, rDB = rPS + 8, rHD = rDXS, rSGU = rDXS + 6, rBH = rYP, rCT = rDXS;
@@ -1541,7 +1543,7 @@ bool diagonal_weights(const TrackArgs& a) {
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     const int m = bound_mask(a);
     const bool d = diagonal_weights(a);
-    // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 31 with the 117-double
+    // Two waves per SIMD only pay where LDS lets more than 4 waves share a CU (N <= 31 with the 118-double
     // stage record); at N = 40 four waves share a CU and the occupancy build's spills would be pure cost.
     const bool occ_room = 5 * lds_bytes(a.N) <= kMaxLdsBytes;
     // The BASELINE horizons (C2 N = 20, C3 N = 40) get stage-unrolled builds.  At N = 20 the large-batch

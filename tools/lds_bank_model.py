@@ -3,8 +3,8 @@ instruction, one extra LDS cycle per extra distinct address on a bank within a g
 each access of one stage (operand reads, factor-row store) and of the P / PA tile accesses.  Mirrors the row layout
 of car-trailer-mpc_amd/csrc/tt_track.hip; update both together."""
 HEAD,SR=256,118
-rX,rY,rZL,rZU,rDX,rYP,rAJ,rGF,rCC,rK=0,8,14,22,30,38,44,53,61,67
-rKF,rPS,rPV,rDXS,PAD=79,81,102,108,116
+rX,rY,rZL,rZU,rDX,rYP,rAJ,rGF,rCC,rK=0,8,14,22,30,38,44,54,62,68
+rKF,rPS,rPV,rDXS,PAD=80,82,104,110,53
 rWC,rSG,rDB,rHD,rSGU,rBH=rDX,rPS,rPS+8,rDXS,rDXS+6,rYP
 def sym(i,j): return i*6-(i*(i-1))//2+(j-i) if i<=j else sym(j,i)
 D={(0,2):0,(0,5):1,(1,2):2,(1,5):3,(2,4):4,(2,5):5,(3,3):6,(3,4):7,(3,5):8}
