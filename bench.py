@@ -196,7 +196,7 @@ def main():
     ap.add_argument("--max-iter", type=int, default=5000, help="OBCA configs: IPOPT max_iter (reference: 5000)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="c5: pipelined scatter/solve/gather chunks per rank shard (one rank: chunk copies); "
-                         "0 = auto: one rank 1, else up to 4 chunks of >= 4096 instances (the N = 20 two-wave build)")
+                         "0 = auto: 1 (one launch per rank shard, the measured fastest shape)")
     ap.add_argument("--graph", action="store_true", help="sim: replay one captured closed-loop step (hipGraph)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -324,6 +324,12 @@ def main():
         out["p99_latency_ms"] = round(p99, 4)
     if args.cpu_budget > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.config, B, N, rank_seed(rank), args.cpu_budget)
+        if "p50_latency_ms" in out:
+            # B = 1 latency against one CPU core solving the same NLP (the reference solves one instance per call on
+            # one core): the oracle's mean per-solve time on one core of the same sample
+            c1 = 1e3 / out["cpu_baseline"]["value_1core"]
+            out["latency_vs_cpu_1core"] = {"p50_latency_ms": out["p50_latency_ms"], "cpu_1core_ms_per_solve": round(c1, 4),
+                                           "ratio": round(c1 / out["p50_latency_ms"], 3)}
     print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
@@ -370,13 +376,13 @@ def main_c5(args):
     solver = ttmpc.BatchSolver(N, sc.PARAMS, sc.MPC_Q, sc.MPC_R, sc.XLB, sc.XUB, sc.ULB, sc.UUB, device=local)
     stream = torch.cuda.Stream(dev)
     # chunks apply on one rank too (chunk copies instead of collectives), so e.g. --batch 8192 --chunks 2 times on one
-    # GPU exactly the per-rank launch shape of the 8-rank run.  Auto: at most 4 chunks and none
-    # below 4096 instances -- a 2048-instance launch runs at ~9.7 M solves/s against ~12.6 M at 4096 and ~15 M at
-    # >= 8192 (profiles/r04/occ_by_batch/), more than the transfer overlap of a smaller chunk gains back
-    # (one rank has no transfers to overlap: one chunk; 65536 x 1 chunk 14.0 M/s, x 4 chunks 13.4 M/s,
-    # profiles/r04/session_b/)
-    per_rank = -(-B_total // world)
-    chunks = args.chunks if args.chunks > 0 else 1 if world == 1 else max(1, min(4, per_rank // 4096))
+    # GPU exactly the per-rank launch shape of a chunked 8-rank run.  Auto = ONE chunk per rank shard: measured through
+    # the sharded path on one GPU at the 8-rank shard size of 8,192 instances, 1 chunk 11.54 M solves/s, 2 chunks
+    # 10.20 M, 4 chunks 8.31 M (profiles/r04/session_b/bench_c5_8192x{1,2,4}.json): a smaller launch loses more
+    # occupancy (the two-wave N = 20 build needs >= 4096 instances to pay, profiles/r04/occ_by_batch/) than the
+    # overlap of an ~11 MB scatter (~0.07 ms over xGMI) can win back.  --chunks > 1 stays available for an RCCL run
+    # that shows overlap paying.
+    chunks = args.chunks if args.chunks > 0 else 1
     sb = ShardedBatch(B_total, N, gpu_shard_solver(solver, stream), device=dev, chunks=chunks)
     if rank == 0:
         x0, xr, ur = workload("c5", B_total, N, seed=rank_seed(0))

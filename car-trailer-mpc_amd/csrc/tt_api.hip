@@ -386,6 +386,14 @@ int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_x
 int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xgoal, const double* d_xref,
                                const double* d_uref, const double* d_z_guess, double* d_x_out, double* d_u_out,
                                double* d_z_out, int* d_status, int* d_iters, double* d_kkt_res, void* stream) {
+    return tt_obca_solve_batch_iterate_device(handle, B, d_x0, d_xgoal, d_xref, d_uref, d_z_guess, d_x_out, d_u_out,
+                                              d_z_out, d_status, d_iters, d_kkt_res, nullptr, stream);
+}
+
+int tt_obca_solve_batch_iterate_device(void* handle, int B, const double* d_x0, const double* d_xgoal,
+                                       const double* d_xref, const double* d_uref, const double* d_z_guess,
+                                       double* d_x_out, double* d_u_out, double* d_z_out, int* d_status, int* d_iters,
+                                       double* d_kkt_res, double* d_iterate_out, void* stream) {
     Handle* h = static_cast<Handle*>(handle);
     if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
     if (!is_obca(h->cfg)) return fail(h, -EINVAL, "handle is not an OBCA variant%s");
@@ -440,6 +448,7 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
     a.status = d_status;
     a.iters = d_iters;
     a.kkt = d_kkt_res;
+    a.itout = d_iterate_out;
     a.ws = h->d_ows;
     a.stamps = h->obca_stamps;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -451,6 +460,13 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
 int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
                         const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
                         int* status, int* iters, double* kkt_res) {
+    return tt_obca_solve_batch_iterate(handle, B, x0, xgoal, xref, uref, z_guess, x_out, u_out, z_out, status, iters,
+                                       kkt_res, nullptr);
+}
+
+int tt_obca_solve_batch_iterate(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
+                                const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
+                                int* status, int* iters, double* kkt_res, double* iterate_out) {
     Handle* h = static_cast<Handle*>(handle);
     if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
     if (!is_obca(h->cfg)) return fail(h, -EINVAL, "handle is not an OBCA variant%s");
@@ -479,13 +495,22 @@ int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgo
     }
     if (z_guess) H2D(h->d_ozg, z_guess, b * nz * 8);
     if (e != hipSuccess) return hip_fail(h, e, "H2D copy");
-    rc = tt_obca_solve_batch_device(h, B, h->d_x0, plan ? h->d_oxg : nullptr, plan ? nullptr : h->d_xref,
-                                    plan ? nullptr : h->d_uref, z_guess ? h->d_ozg : nullptr, h->d_xo, h->d_uo,
-                                    z_out ? h->d_ozo : nullptr, h->d_st, h->d_it, h->d_kkt, s);
+    // the diagnostic iterate export gets a buffer of its own for this call (it is not a hot-path output)
+    const size_t it_bytes = b * ttmpc::obca_iterate_len(h->cfg.N, h->cfg.M) * 8;
+    double* d_itout = nullptr;
+    if (iterate_out) {
+        e = hipMalloc((void**)&d_itout, it_bytes);
+        if (e != hipSuccess) return fail(h, -ENOMEM, "iterate export allocation failed for B=%s", std::to_string(B).c_str());
+    }
+    rc = tt_obca_solve_batch_iterate_device(h, B, h->d_x0, plan ? h->d_oxg : nullptr, plan ? nullptr : h->d_xref,
+                                            plan ? nullptr : h->d_uref, z_guess ? h->d_ozg : nullptr, h->d_xo, h->d_uo,
+                                            z_out ? h->d_ozo : nullptr, h->d_st, h->d_it, h->d_kkt, d_itout, s);
     if (rc) {
         (void)hipStreamSynchronize(s);
+        if (d_itout) (void)hipFree(d_itout);
         return rc;
     }
+    if (iterate_out) D2H(iterate_out, d_itout, it_bytes);
     if (x_out) D2H(x_out, h->d_xo, b * (N + 1) * 6 * 8);
     if (u_out) D2H(u_out, h->d_uo, b * N * 2 * 8);
     if (z_out) D2H(z_out, h->d_ozo, b * nz * 8);
@@ -495,6 +520,10 @@ int tt_obca_solve_batch(void* handle, int B, const double* x0, const double* xgo
 #undef H2D
 #undef D2H
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (d_itout) {
+        if (e != hipSuccess) (void)hipStreamSynchronize(s);
+        (void)hipFree(d_itout);
+    }
     if (e != hipSuccess) return hip_fail(h, e, "OBCA solve");
     return 0;
 }
@@ -538,6 +567,9 @@ int tt_lds_bytes(int N) { return ttmpc::lds_bytes(N); }
 int tt_max_horizon(void) { return ttmpc::max_horizon(); }
 const char* tt_version(void) { return "ttmpc 0.2 (gfx950: wave-per-instance Riccati IPM; workgroup-per-instance OBCA IPM)"; }
 long long tt_obca_n(int N, int M) { return (N < 1 || M < 1) ? -EINVAL : (long long)ttmpc::obca_n(N, M); }
+long long tt_obca_iterate_len(int N, int M) {
+    return (N < 1 || M < 1) ? -EINVAL : (long long)ttmpc::obca_iterate_len(N, M);
+}
 long long tt_obca_workspace_bytes(int N, int M) {
     return (N < 1 || M < 1) ? -EINVAL : (long long)(8 * ttmpc::obca_ws_doubles(N, M));
 }

@@ -4,6 +4,11 @@
 
 namespace ttmpc {
 
+// IPOPT's convergence test (OptimalityErrorConvergenceCheck, defaults): besides the scaled error E_0 <= tol, the
+// unscaled dual infeasibility, constraint violation and complementarity must be below these (acceptable: the second set)
+constexpr double kDualInfTol = 1.0, kConstrViolTol = 1e-4, kComplInfTol = 1e-4;
+constexpr double kAccDualInfTol = 1e10, kAccConstrViolTol = 1e-2, kAccComplInfTol = 1e-2;
+
 // Everything one launch needs; passed by value as the kernel argument (< 1 KB).
 struct TrackArgs {
     int N, B, max_iter, acc_iter;
@@ -77,6 +82,7 @@ struct ObcaArgs {
     int* status;                    // [B]
     int* iters;                     // [B] or nullptr
     double* kkt;                    // [B] or nullptr
+    double* itout;                  // [B][obca_iterate_len] final primal-dual iterate (diagnostic export) or nullptr
     double* ws;                     // per-instance workspace, obca_ws_doubles(N, M) each
     unsigned long long* stamps;     // [B][kObcaPhases] cycle sums (diagnostics), or nullptr
 };
@@ -94,6 +100,8 @@ __host__ __device__ inline size_t obca_ws_doubles(int N, int M) {
     return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
 }
 __host__ __device__ inline size_t obca_n(int N, int M) { return (size_t)N * (8 + 16 * M) + 6 + 16 * M; }
+// diagnostic export of the final iterate (include/ttmpc.h tt_obca_iterate_len): 30 per stage, 32 per block, 24 final rows
+__host__ __device__ inline size_t obca_iterate_len(int N, int M) { return (size_t)(30 + 64 * M) * (N + 1) + 24; }
 
 hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream);
 

@@ -627,6 +627,7 @@ __device__ __forceinline__ int blk_factor(Blk& k, const double* sig_w, double dw
     const int negT = schol4(k.LT, pd);
     // Haynsworth: the block has IPOPT's inertia (8, 4, 0) iff negT == negA; negT > negA leaves it with too few negative
     // eigenvalues (its rows need delta_c), negT < negA with too many (negative curvature: delta_x)
+    // (pd mode: A was positive definite, so a negative T pivot, -2, means too few negative eigenvalues)
     if (negT < 0) return negT == -1 ? F_ZERO : F_MANY;
     if (negT != negA) return negT > negA ? F_FEW : F_MANY;
     double Wm[4][4];  // LT^-1 G
@@ -4028,6 +4029,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         int in_soft = 0, soft_cnt = 0, first_resto = 0, resto_iter0 = 0, have_acc = 0;
         double th_resto0 = 0.0;
         const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, smax = 100.0;
+        const double mu_min = fmin(a.tol, kComplInfTol) / (kappa_eps + 1.0);  // MonotoneMuUpdate's barrier floor
         const double g_th = 1e-5, g_ph = 1e-8, s_ph = 2.3, s_th = 1.1, delta = 1.0, eta_ph = 1e-8, g_al = 0.05;
         const double tolc = 10.0 * EPS;
         for (iter = 0;; ++iter) {
@@ -4045,16 +4047,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 const double nbd = n_bounds + (R ? 2.0 * n_rows : 0.0);
                 double sd = fmax(smax, red[3] / (n_rows + nbd)) / smax, sc = fmax(smax, red[4] / nbd) / smax;
                 E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
+                // IPOPT's OptimalityErrorConvergenceCheck: E_0 and the UNSCALED dual infeasibility, constraint violation
+                // and complementarity (pinf bounds the NLP's constraint violation from above, oracle/c/tt_obca.c)
+                const bool conv = E0 <= a.tol && dinf <= kDualInfTol && pinf <= kConstrViolTol && c0 <= kComplInfTol;
+                const bool accp = E0 <= a.acc_tol && dinf <= kAccDualInfTol && pinf <= kAccConstrViolTol &&
+                                  c0 <= kAccComplInfTol;
                 if (!R) {
-                    if (E0 <= a.tol) { status = 0; done = true; break; }
-                    if (E0 <= a.acc_tol) {
+                    if (conv) { status = 0; done = true; break; }
+                    if (accp) {
                         phase_acc(cs, false);
                         have_acc = 1;
                         if (++stt.acc >= a.acc_iter) { status = 1; done = true; break; }
                     } else {
                         stt.acc = 0;
                     }
-                    if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; done = true; break; }
+                    if (iter >= a.max_iter) { status = accp ? 1 : 2; done = true; break; }
                 } else {
                     // restoration convergence: original infeasibility down to kappa_resto of its value at entry and
                     // the point acceptable to the augmented original filter
@@ -4068,8 +4075,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                         break;
                     }
                     first_resto = 0;
-                    if (E0 <= a.acc_tol) ++stt.acc; else stt.acc = 0;
-                    if (E0 <= a.tol || stt.acc >= a.acc_iter) {
+                    if (accp) ++stt.acc; else stt.acc = 0;
+                    if (conv || stt.acc >= a.acc_iter) {
                         // IPOPT's RestoConvergenceCheck: the ORIGINAL problem's primal infeasibility (max norm) against
                         // resto_failure_feasibility_threshold (default 1e2 tol)
                         if (red[12] <= 1e2 * a.tol) {  // feasible but filter-unacceptable
@@ -4089,7 +4096,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     if (iter >= a.max_iter) { status = 2; done = true; break; }
                 }
                 // ---- barrier update (monotone, Fiacco-McCormick); the filter is reset on every change ----
-                while (stt.mu > a.tol / 10.0 * 1.0000001) {
+                while (stt.mu > mu_min * 1.0000001) {
                     // E_mu = max(dual, primal, complementarity): when the first two already exceed kappa_eps mu the
                     // test fails whatever the complementarity is (fmax(a, b) >= a for a non-NaN a), so its pass is
                     // skipped -- the usual case away from convergence; the decision is the same as with it
@@ -4098,7 +4105,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     const double2 cm = phase_compl(cs, sh, stt.mu);
                     stamp(sh, ston, OPH_COMPL);
                     if (!(fmax(e_dp, cm.x / sc) <= kappa_eps * stt.mu)) break;
-                    stt.mu = fmax(a.tol / 10.0, fmin(kappa_mu * stt.mu, pow(stt.mu, theta_mu)));
+                    stt.mu = fmax(mu_min, fmin(kappa_mu * stt.mu, pow(stt.mu, theta_mu)));
                     stt.tau = fmax(0.99, 1.0 - stt.mu);
                     __syncthreads();
                     if (tid == 0) {
@@ -4329,6 +4336,44 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                     z[o + ob * 8 + 4 * bd + e] = c.B(B_W + e, j, k);
                     z[o + 8 * a.M + ob * 8 + 4 * bd + e] = c.B(B_W + 4 + e, j, k);
                 }
+            }
+        }
+    }
+    if (a.itout) {
+        // the final primal-dual iterate, for an independent evaluation of IPOPT's optimality error at the GPU's point
+        // (tests/test_gpu_obca.py; oracle/c/tt_obca.c pack_iterate has the same layout)
+        double* it = a.itout + (size_t)c.b * obca_iterate_len(N, a.M);
+        for (int k = tid; k <= N; k += T) {
+            double* q = it + 30 * (size_t)k;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                q[i] = c.S(S_X + i, k); q[8 + i] = c.S(S_ZLX + i, k); q[14 + i] = c.S(S_ZUX + i, k);
+                q[24 + i] = c.S(S_YC + i, k);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                q[6 + i] = k < N ? c.S(S_U + i, k) : 0.0;
+                q[20 + i] = k < N ? c.S(S_ZLU + i, k) : 0.0;
+                q[22 + i] = k < N ? c.S(S_ZUU + i, k) : 0.0;
+            }
+            double* bq = it + 30 * (size_t)(N + 1) + 32 * (size_t)k * NBK;
+            for (int j = 0; j < NBK; ++j) {
+                double* qb = bq + 32 * j;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) { qb[e] = c.B(B_W + e, j, k); qb[8 + e] = c.B(B_ZW + e, j, k); }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    qb[16 + r] = c.B(B_S + r, j, k); qb[20 + r] = c.B(B_VL + r, j, k); qb[24 + r] = c.B(B_VU + r, j, k);
+                    qb[28 + r] = c.B(B_YD + r, j, k);
+                }
+            }
+        }
+        if (tid == 0) {
+            double* f = it + 30 * (size_t)(N + 1) + 32 * (size_t)(N + 1) * NBK;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                f[i] = plan ? sh.sf[i] : 0.0; f[6 + i] = plan ? sh.vLf[i] : 0.0; f[12 + i] = plan ? sh.vUf[i] : 0.0;
+                f[18 + i] = plan ? sh.ydf[i] : 0.0;
             }
         }
     }

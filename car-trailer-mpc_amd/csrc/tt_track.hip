@@ -1376,7 +1376,8 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
         int acc_count = 0, nf = 0;
         // launch constants of the optimality-error scaling and the barrier floor: no IEEE division per iteration
         const double inv_m = 1.0 / (double)(6 * (N + 1) + nb), inv_nb = nb ? 1.0 / (double)nb : 0.0;
-        const double mu_floor = a.tol / 10.0, mu_floor_test = mu_floor * 1.0000001;
+        // IPOPT's barrier floor (MonotoneMuUpdate::CalcNewMuAndTau): min(tol, compl_inf_tol) / (barrier_tol_factor + 1)
+        const double mu_floor = fmin(a.tol, kComplInfTol) / 11.0, mu_floor_test = mu_floor * 1.0000001;
         for (iter = 0;; ++iter) {
             const Lin e = phase_linearize(c);
             STAMP(PH_LIN);
@@ -1385,14 +1386,20 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             const double isd = 100.0 * frcp(fmax(100.0, (e.sy + e.sz) * inv_m));
             const double isc = nb ? 100.0 * frcp(fmax(100.0, e.sz * inv_nb)) : 1.0;
             const double dsc = e.dinf * isd;
-            E0 = fmax(fmax(dsc, e.pinf), e.c0() * isc);
-            if (E0 <= a.tol) { status = 0; break; }
-            if (E0 <= a.acc_tol) {
+            const double c0 = e.c0();
+            E0 = fmax(fmax(dsc, e.pinf), c0 * isc);
+            // IPOPT's OptimalityErrorConvergenceCheck: the scaled error and the UNSCALED dual infeasibility,
+            // constraint violation (dynamics rows only: max |c| = pinf) and complementarity max |z s|
+            const bool conv = E0 <= a.tol && e.dinf <= kDualInfTol && e.pinf <= kConstrViolTol && c0 <= kComplInfTol;
+            const bool accp = E0 <= a.acc_tol && e.dinf <= kAccDualInfTol && e.pinf <= kAccConstrViolTol &&
+                              c0 <= kAccComplInfTol;
+            if (conv) { status = 0; break; }
+            if (accp) {
                 if (++acc_count >= a.acc_iter) { status = 1; break; }
             } else {
                 acc_count = 0;
             }
-            if (iter >= a.max_iter) { status = E0 <= a.acc_tol ? 1 : 2; break; }
+            if (iter >= a.max_iter) { status = accp ? 1 : 2; break; }
             // barrier parameter (monotone Fiacco-McCormick)
             double cmu = e.cmu(c.mu);
             for (;;) {

@@ -84,6 +84,13 @@ def lib():
     L.tt_obca_solve_batch.restype = C.c_int
     L.tt_obca_solve_batch_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 12
     L.tt_obca_solve_batch_device.restype = C.c_int
+    L.tt_obca_solve_batch_iterate.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip,
+                                              _dp, _dp]
+    L.tt_obca_solve_batch_iterate.restype = C.c_int
+    L.tt_obca_solve_batch_iterate_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 13
+    L.tt_obca_solve_batch_iterate_device.restype = C.c_int
+    L.tt_obca_iterate_len.argtypes = [C.c_int, C.c_int]
+    L.tt_obca_iterate_len.restype = C.c_longlong
     L.tt_obca_n.argtypes = [C.c_int, C.c_int]
     L.tt_obca_n.restype = C.c_longlong
     L.tt_obca_workspace_bytes.argtypes = [C.c_int, C.c_int]
@@ -123,7 +130,8 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ("tt_create", "tt_solve_batch", "tt_solve_batch_device", "tt_plan_batch", "tt_obca_solve_batch",
-                    "tt_obca_solve_batch_device", "tt_obca_n", "tt_obca_workspace_bytes", "tt_destroy",
+                    "tt_obca_solve_batch_device", "tt_obca_solve_batch_iterate", "tt_obca_solve_batch_iterate_device",
+                    "tt_obca_iterate_len", "tt_obca_n", "tt_obca_workspace_bytes", "tt_destroy",
                     "tt_last_error", "tt_lds_bytes", "tt_max_horizon", "tt_version", "tt_sim_window_device",
                     "tt_collision_device", "tt_plant_update_device", "tt_warm_start_device",
                     "tt_record_solution_device", "tt_interpolate_device", "tt_lqr_score_device",
@@ -268,8 +276,9 @@ class ObcaSolver:
     __del__ = BatchSolver.__del__
     _err = BatchSolver._err
 
-    def solve(self, x0, x_goal=None, xref=None, uref=None, z_guess=None):
-        """Host arrays -> (X (B,N+1,6), U (B,N,2), z (B,n), status, iters, kkt)."""
+    def solve(self, x0, x_goal=None, xref=None, uref=None, z_guess=None, iterate=False):
+        """Host arrays -> (X (B,N+1,6), U (B,N,2), z (B,n), status, iters, kkt); with ``iterate=True`` also the final
+        primal-dual iterate (B, tt_obca_iterate_len) of the diagnostic export (include/ttmpc.h) as a 7th element."""
         N, n = self.N, self.n
         x0 = _f64(x0)
         B = x0.shape[0] if x0.ndim == 2 else 1
@@ -284,6 +293,14 @@ class ObcaSolver:
         st = np.empty(B, dtype=np.int32)
         it = np.empty(B, dtype=np.int32)
         kk = np.empty(B)
+        if iterate:
+            I = np.empty((B, int(self._L.tt_obca_iterate_len(N, self.M))))
+            rc = self._L.tt_obca_solve_batch_iterate(self._h, B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg),
+                                                     _ptr(X), _ptr(U), _ptr(Z), st.ctypes.data_as(_ip),
+                                                     it.ctypes.data_as(_ip), _ptr(kk), _ptr(I))
+            if rc != 0:
+                self._err(rc, "tt_obca_solve_batch_iterate")
+            return X, U, Z, st, it, kk, I
         rc = self._L.tt_obca_solve_batch(self._h, B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg), _ptr(X),
                                          _ptr(U), _ptr(Z), st.ctypes.data_as(_ip), it.ctypes.data_as(_ip), _ptr(kk))
         if rc != 0:

@@ -109,6 +109,25 @@ int tt_obca_solve_batch_device(void* handle, int B, const double* d_x0, const do
 /* decision-vector length n of the OBCA variants, and device workspace bytes one instance needs */
 long long tt_obca_n(int N, int M);
 long long tt_obca_workspace_bytes(int N, int M);
+/* Diagnostic variants of the two calls above that also export each instance's FINAL PRIMAL-DUAL ITERATE, so that
+ * IPOPT's optimality error can be re-evaluated independently at the returned point (tests; the reference's IPOPT keeps
+ * these multipliers internal -- CasADi returns only their lam_x / lam_g combinations).  iterate_out [B][L],
+ * L = tt_obca_iterate_len(N, M) = 30(N+1) + 64M(N+1) + 24 doubles:
+ *   per stage k = 0..N (30): x 6, u 2, z_L(x) 6, z_U(x) 6, z_L(u) 2, z_U(u) 2, y of the 6 dynamics rows
+ *                            (u, z_L(u), z_U(u) are 0 at k = N);
+ *   per OBCA block (k, j), j = 2 obstacle + body, in k-major order (32): mu|lam 8, their bound multipliers 8,
+ *                            the 4 rows' slacks s, slack-bound multipliers v_L, v_U and row multipliers y_d;
+ *   final-box rows (24, plan variant; zeros otherwise): slacks, v_L, v_U, y of x_N - x_goal.
+ * The multipliers are IPOPT's internal ones (bound multipliers >= 0 of the relaxed bounds; rows of the slack form
+ * d(x) - s = 0). */
+long long tt_obca_iterate_len(int N, int M);
+int tt_obca_solve_batch_iterate(void* handle, int B, const double* x0, const double* xgoal, const double* xref,
+                                const double* uref, const double* z_guess, double* x_out, double* u_out, double* z_out,
+                                int* status, int* iters, double* kkt_res, double* iterate_out);
+int tt_obca_solve_batch_iterate_device(void* handle, int B, const double* d_x0, const double* d_xgoal,
+                                       const double* d_xref, const double* d_uref, const double* d_z_guess,
+                                       double* d_x_out, double* d_u_out, double* d_z_out, int* d_status, int* d_iters,
+                                       double* d_kkt_res, double* d_iterate_out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Closed-loop simulation step, device pointers, asynchronous on `stream`.

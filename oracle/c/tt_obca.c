@@ -73,6 +73,15 @@
 #define WD_TRIAL_MAX 3           /* watchdog_trial_iter_max */
 #define KAPPA_D 1e-5            /* kappa_d: linear damping of variables with one finite bound */
 #define MAX_SOFT_RESTO 10
+/* IPOPT's OptimalityErrorConvergenceCheck defaults (dual_inf_tol, constr_viol_tol, compl_inf_tol and the acceptable
+ * ones) and MonotoneMuUpdate's barrier floor min(tol, compl_inf_tol) / (barrier_tol_factor + 1) */
+#define DUAL_INF_TOL 1.0
+#define CONSTR_VIOL_TOL 1e-4
+#define COMPL_INF_TOL 1e-4
+#define ACC_DUAL_INF_TOL 1e10
+#define ACC_CONSTR_VIOL_TOL 1e-2
+#define ACC_COMPL_INF_TOL 1e-2
+#define BARRIER_TOL_FACTOR 10.0
 
 static int isfree(double b) { return !isfinite(b) || fabs(b) >= 1e19; }
 
@@ -791,6 +800,8 @@ static int block_factor(ws_t* W, int bi, double dw, double dc, double* Q) {
          * eigenvalues", which it treats as a singular matrix); negT < negA: too many (negative curvature) */
         else if (negT != negA) { ++g_cen[negT > negA ? 1 : 2]; return negT > negA ? F_FEW : F_MANY; }
     } else {
+        /* pd mode: A is positive definite here (negA = 0), so a negative pivot of T leaves the block with too FEW
+         * negative eigenvalues by Haynsworth (IPOPT: singular -> delta_c), not too many */
         const int f = chol(LT, 4);
         if (f != 0) return f;
         for (int r = 0; r < 4; ++r) ST[r] = 1.0;
@@ -1450,7 +1461,19 @@ static double ftb_dual(const ws_t* W, double tau) {
 
 /* scaled optimality error at the current iterate (IPOPT eq. (5)) of the current system (original or
  * restoration NLP); also the 1-norm primal-dual system error at mu (soft restoration test) */
-typedef struct { double E0, Emu, dinf, pinf, pderr; int finite; } opterr_t;
+typedef struct { double E0, Emu, dinf, pinf, c0, sd, sc, pderr; int finite; } opterr_t;
+
+/* IPOPT's convergence tests on an evaluated error (OptimalityErrorConvergenceCheck::CheckConvergence and
+ * CurrentIsAcceptable): the scaled error E_0 and the UNSCALED dual infeasibility, constraint violation and
+ * complementarity max |z s|.  The constraint violation of the NLP (max |c| and the violation of d(x) against its
+ * bounds) is at most pinf = max(|c|, |d(x) - s|) because every slack s lies inside the (relaxed) bounds, and pinf
+ * <= E_0, so with tol <= constr_viol_tol that test can only pass where the E_0 test does; pinf stands in for it. */
+static int converged(const opterr_t* o, double tol) {
+    return o->E0 <= tol && o->dinf <= DUAL_INF_TOL && o->pinf <= CONSTR_VIOL_TOL && o->c0 <= COMPL_INF_TOL;
+}
+static int acceptable_pt(const opterr_t* o, double acc_tol) {
+    return o->E0 <= acc_tol && o->dinf <= ACC_DUAL_INF_TOL && o->pinf <= ACC_CONSTR_VIOL_TOL && o->c0 <= ACC_COMPL_INF_TOL;
+}
 
 static opterr_t opt_error(ws_t* W, double mu) {
     const tto_obca_problem* P = W->P;
@@ -1536,6 +1559,9 @@ static opterr_t opt_error(ws_t* W, double mu) {
     o.Emu = fmax(fmax(dinf / sd, pinf), cmu / sc);
     o.dinf = dinf;
     o.pinf = pinf;
+    o.c0 = c0;
+    o.sd = sd;
+    o.sc = sc;
     o.pderr = d1 + p1 + cm1;
     if (W->dbg & 2) {
         double my_ = 0, mz = 0, mzw = 0, mv = 0;
@@ -2553,20 +2579,65 @@ static void orig_th_phi(ws_t* W, double mu, double* th, double* ph, double* pmax
     *ph = bad ? INFINITY : cost_eval(W, W->x, W->u) + b;
 }
 
-static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const double* xref, const double* uref,
-                     const double* zg, double* zout, int* iters_out, double* kkt_out) {
-    const tto_obca_problem* P = W->P;
+/* The primal-dual iterate in the layout of the kernel's diagnostic export (include/ttmpc.h tt_obca_iterate_len):
+ * per stage k (30): x 6, u 2, zLx 6, zUx 6, zLu 2, zUu 2, yc 6 (u, zLu, zUu zero at k = N); per block bi = k nbk + j
+ * (32): w 8, zw 8, s 4, vL 4, vU 4, yd 4; then the final-box rows (24): sf 6, vLf 6, vUf 6, ydf 6 (zero in track mode). */
+static void pack_iterate(const ws_t* W, double* it) {
     const int N = W->N;
-    W->xinit = xinit; W->xgoal = xgoal; W->xref = xref; W->uref = uref;
-    memset(g_cen, 0, sizeof(g_cen));
-    W->R = M_ORIG;
-    W->lsq = 0;
-    W->have_acc = 0;
-    W->kd = (P->opts & TTO_OPT_KAPPA_D) ? KAPPA_D : 0.0;
-    W->dbg = (getenv("TTO_DEBUG") ? 1 : 0) | (getenv("TTO_DEBUG2") ? 2 : 0) | (getenv("TTO_CHECK") ? 4 : 0);
-    const int dbg = W->dbg & 1;
-    const int use_resto = !(P->opts & TTO_OPT_NO_RESTO), use_soft = !(P->opts & TTO_OPT_NO_SOFT_RESTO);
-    /* weights, bounds (bound_relax_factor 1e-8 on every finite bound) */
+    for (int k = 0; k <= N; ++k) {
+        double* q = it + 30 * (size_t)k;
+        for (int i = 0; i < 6; ++i) {
+            q[i] = W->x[6 * k + i]; q[8 + i] = W->zLx[6 * k + i]; q[14 + i] = W->zUx[6 * k + i]; q[24 + i] = W->yc[6 * k + i];
+        }
+        for (int i = 0; i < 2; ++i) {
+            q[6 + i] = k < N ? W->u[2 * k + i] : 0.0;
+            q[20 + i] = k < N ? W->zLu[2 * k + i] : 0.0;
+            q[22 + i] = k < N ? W->zUu[2 * k + i] : 0.0;
+        }
+    }
+    double* bq = it + 30 * ((size_t)N + 1);
+    for (int bi = 0; bi < W->nb; ++bi) {
+        double* q = bq + 32 * (size_t)bi;
+        for (int e = 0; e < 8; ++e) { q[e] = W->w[8 * bi + e]; q[8 + e] = W->zw[8 * bi + e]; }
+        for (int r = 0; r < 4; ++r) {
+            q[16 + r] = W->s[4 * bi + r]; q[20 + r] = W->vL[4 * bi + r]; q[24 + r] = W->vU[4 * bi + r];
+            q[28 + r] = W->yd[4 * bi + r];
+        }
+    }
+    double* f = bq + 32 * (size_t)W->nb;
+    for (int i = 0; i < 6; ++i) {
+        const int pl = W->mode == TTO_OBCA_PLAN;
+        f[i] = pl ? W->sf[i] : 0.0; f[6 + i] = pl ? W->vLf[i] : 0.0; f[12 + i] = pl ? W->vUf[i] : 0.0;
+        f[18 + i] = pl ? W->ydf[i] : 0.0;
+    }
+}
+
+static void unpack_iterate(ws_t* W, const double* it) {
+    const int N = W->N;
+    for (int k = 0; k <= N; ++k) {
+        const double* q = it + 30 * (size_t)k;
+        for (int i = 0; i < 6; ++i) {
+            W->x[6 * k + i] = q[i]; W->zLx[6 * k + i] = q[8 + i]; W->zUx[6 * k + i] = q[14 + i]; W->yc[6 * k + i] = q[24 + i];
+        }
+        if (k < N)
+            for (int i = 0; i < 2; ++i) { W->u[2 * k + i] = q[6 + i]; W->zLu[2 * k + i] = q[20 + i]; W->zUu[2 * k + i] = q[22 + i]; }
+    }
+    const double* bq = it + 30 * ((size_t)N + 1);
+    for (int bi = 0; bi < W->nb; ++bi) {
+        const double* q = bq + 32 * (size_t)bi;
+        for (int e = 0; e < 8; ++e) { W->w[8 * bi + e] = q[e]; W->zw[8 * bi + e] = q[8 + e]; }
+        for (int r = 0; r < 4; ++r) {
+            W->s[4 * bi + r] = q[16 + r]; W->vL[4 * bi + r] = q[20 + r]; W->vU[4 * bi + r] = q[24 + r];
+            W->yd[4 * bi + r] = q[28 + r];
+        }
+    }
+    const double* f = bq + 32 * (size_t)W->nb;
+    for (int i = 0; i < 6; ++i) { W->sf[i] = f[i]; W->vLf[i] = f[6 + i]; W->vUf[i] = f[12 + i]; W->ydf[i] = f[18 + i]; }
+}
+
+/* weights, bounds (bound_relax_factor 1e-8 on every finite bound), row bounds */
+static void setup_bounds(ws_t* W) {
+    const tto_obca_problem* P = W->P;
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) W->Qc[i * 6 + j] = 0.5 * (P->Q[i * 6 + j] + P->Q[j * 6 + i]);
     for (int i = 0; i < 2; ++i)
@@ -2590,6 +2661,22 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     W->hrL[3] = 0; W->hrU[3] = 1; W->rU[3] = RELAX;
     W->rL[0] = W->rL[3] = -INFINITY;
     W->fL = -P->fin_tol - RELAX; W->fU = P->fin_tol + RELAX;
+}
+
+static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const double* xref, const double* uref,
+                     const double* zg, double* zout, int* iters_out, double* kkt_out, double* it_out) {
+    const tto_obca_problem* P = W->P;
+    const int N = W->N;
+    W->xinit = xinit; W->xgoal = xgoal; W->xref = xref; W->uref = uref;
+    memset(g_cen, 0, sizeof(g_cen));
+    W->R = M_ORIG;
+    W->lsq = 0;
+    W->have_acc = 0;
+    W->kd = (P->opts & TTO_OPT_KAPPA_D) ? KAPPA_D : 0.0;
+    W->dbg = (getenv("TTO_DEBUG") ? 1 : 0) | (getenv("TTO_DEBUG2") ? 2 : 0) | (getenv("TTO_CHECK") ? 4 : 0);
+    const int dbg = W->dbg & 1;
+    const int use_resto = !(P->opts & TTO_OPT_NO_RESTO), use_soft = !(P->opts & TTO_OPT_NO_SOFT_RESTO);
+    setup_bounds(W);
 
     if (zg) unpack(W, zg); else { default_guess(W, zout); unpack(W, zout); }
     if (P->dual_init)
@@ -2601,6 +2688,7 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         if (!isfinite(xinit[i]) || (W->hxl[i] && xinit[i] < W->xl[i]) || (W->hxu[i] && xinit[i] > W->xu[i])) status = 3;
     if (status == 3) {
         pack(W, zout);
+        if (it_out) memset(it_out, 0, tto_obca_iterate_len(N, P->M) * sizeof(double));
         if (iters_out) *iters_out = 0;
         if (kkt_out) *kkt_out = INFINITY;
         return 3;
@@ -2647,7 +2735,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     ipm_state_t SO, SR;
     ipm_reset(&SO, 0.1);
     ipm_reset(&SR, 0.1);
-    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
+    const double kappa_eps = BARRIER_TOL_FACTOR, kappa_mu = 0.2, theta_mu = 1.5;
+    const double mu_min = fmin(P->tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0);
     int in_soft = 0, soft_cnt = 0, first_resto = 0, n_resto = 0, n_soft = 0, fallback = 0, resto_iter0 = 0;
     double th_resto0 = 0.0;
     for (iter = 0;; ++iter) {
@@ -2659,8 +2748,9 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         if (W->R == M_ORIG) {
             if (dbg) fprintf(stderr, "it %4d E0 %.3e dinf %.3e pinf %.3e mu %.2e f %.6e\n", iter, E0, oe.dinf, oe.pinf,
                              S->mu, cost_eval(W, W->x, W->u));
-            if (E0 <= P->tol) { status = 0; break; }
-            if (E0 <= P->acc_tol) {
+            const int accp = acceptable_pt(&oe, P->acc_tol);
+            if (converged(&oe, P->tol)) { status = 0; break; }
+            if (accp) {
                 memcpy(W->xacc, W->x, 6 * ((size_t)N + 1) * 8);
                 memcpy(W->uacc, W->u, 2 * (size_t)N * 8);
                 memcpy(W->wacc, W->w, 8 * (size_t)W->nb * 8);
@@ -2669,7 +2759,7 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
             } else {
                 S->acc_count = 0;
             }
-            if (iter >= P->max_iter) { status = E0 <= P->acc_tol ? 1 : 2; break; }
+            if (iter >= P->max_iter) { status = accp ? 1 : 2; break; }
         } else {
             /* restoration convergence (RestoConvergenceCheck): original infeasibility reduced to kappa_resto of
              * its value at entry and the point acceptable to the augmented original filter */
@@ -2684,8 +2774,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
                 continue;
             }
             first_resto = 0;
-            if (E0 <= P->acc_tol) ++S->acc_count; else S->acc_count = 0;
-            if (E0 <= P->tol || S->acc_count >= P->acc_iter) {
+            if (acceptable_pt(&oe, P->acc_tol)) ++S->acc_count; else S->acc_count = 0;
+            if (converged(&oe, P->tol) || S->acc_count >= P->acc_iter) {
                 /* the restoration NLP converged (or converged to an acceptable point) without reaching a point
                  * acceptable to the original problem: IPOPT (RestoConvergenceCheck) compares the ORIGINAL problem's
                  * primal infeasibility (max norm) with resto_failure_feasibility_threshold (default 1e2 tol) */
@@ -2701,8 +2791,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
             if (iter >= P->max_iter) { status = 2; break; }
         }
         /* barrier update (monotone, Fiacco-McCormick); the filter is reset on every change */
-        while (oe.Emu <= kappa_eps * S->mu && S->mu > P->tol / 10.0 * 1.0000001) {
-            S->mu = fmax(P->tol / 10.0, fmin(kappa_mu * S->mu, pow(S->mu, theta_mu)));
+        while (oe.Emu <= kappa_eps * S->mu && S->mu > mu_min * 1.0000001) {
+            S->mu = fmax(mu_min, fmin(kappa_mu * S->mu, pow(S->mu, theta_mu)));
             S->tau = fmax(0.99, 1.0 - S->mu);
             S->F.n = 0;
             if (W->R == M_RESTO) { W->zeta = sqrt(S->mu); obj_grad(W); }
@@ -2817,6 +2907,7 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
         fprintf(stderr, "CENSUS status %d iters %d fact %ld blocks_ok %ld few %ld many %ld zero %ld ref>1e-10 %ld ref>1e-5 %ld pretend %ld\n",
                 status, iter, g_cen[0], g_cen[4], g_cen[1], g_cen[2], g_cen[3], g_cen[5], g_cen[6], g_cen[7]);
     pack(W, zout);
+    if (it_out) pack_iterate(W, it_out);
     if (iters_out) *iters_out = iter;
     if (kkt_out) *kkt_out = E0;
     return status;
@@ -2829,7 +2920,7 @@ int tto_obca_solve(const tto_obca_problem* P, const double* x_init, const double
     if (P->mode == TTO_OBCA_TRACK && (!xref || !uref)) return -1;
     ws_t W;
     if (ws_init(&W, P) != 0) return -1;
-    const int st = solve_one(&W, x_init, x_goal, xref, uref, z_guess, z_out, iters, kkt);
+    const int st = solve_one(&W, x_init, x_goal, xref, uref, z_guess, z_out, iters, kkt, NULL);
     free(W.mem);
     return st;
 }
@@ -2837,6 +2928,12 @@ int tto_obca_solve(const tto_obca_problem* P, const double* x_init, const double
 int tto_obca_solve_batch(const tto_obca_problem* P, int B, const double* x_init, const double* x_goal,
                          const double* xref, const double* uref, const double* z_guess, double* z_out,
                          int* status, int* iters, double* kkt, int nthreads) {
+    return tto_obca_solve_batch_it(P, B, x_init, x_goal, xref, uref, z_guess, z_out, status, iters, kkt, NULL, nthreads);
+}
+
+int tto_obca_solve_batch_it(const tto_obca_problem* P, int B, const double* x_init, const double* x_goal,
+                            const double* xref, const double* uref, const double* z_guess, double* z_out,
+                            int* status, int* iters, double* kkt, double* it_out, int nthreads) {
     if (P->N < 1 || P->M < 1 || P->M > TTO_MAXM || B < 0) return -1;
     const int N = P->N;
     const size_t n = (size_t)N * (8 + 16 * P->M) + 6 + 16 * P->M;
@@ -2857,7 +2954,8 @@ int tto_obca_solve_batch(const tto_obca_problem* P, int B, const double* x_init,
             double e = 0.0;
             status[b] = solve_one(&W, x_init + 6 * (size_t)b, x_goal ? x_goal + 6 * (size_t)b : NULL,
                                   xref ? xref + (size_t)b * 6 * (N + 1) : NULL, uref ? uref + (size_t)b * 2 * N : NULL,
-                                  z_guess ? z_guess + (size_t)b * n : NULL, z_out + (size_t)b * n, &it, &e);
+                                  z_guess ? z_guess + (size_t)b * n : NULL, z_out + (size_t)b * n, &it, &e,
+                                  it_out ? it_out + (size_t)b * tto_obca_iterate_len(N, P->M) : NULL);
             if (iters) iters[b] = it;
             if (kkt) kkt[b] = e;
         }
@@ -2872,4 +2970,29 @@ int tto_obca_solve_batch(const tto_obca_problem* P, int B, const double* x_init,
 void tto_obca_block_lin(const tto_obca_problem* P, const double* xk, int j, const double* wv, const double* y,
                         double* d, double* Jx, double* Jw, double* Hxx, double* Hxw, double* Hww) {
     blk_lin(P, xk, j, wv, y, d, Jx, Jw, Hxx, Hxw, Hww);
+}
+
+long long tto_obca_iterate_len(int N, int M) { return 30LL * (N + 1) + 64LL * M * (N + 1) + 24; }
+
+/* IPOPT's optimality error at a GIVEN primal-dual point (the GPU's returned iterate, or the oracle's own), in the
+ * original problem: out = {E_0 (scaled, IPOPT eq. (5)), unscaled dual infeasibility, primal infeasibility (max norm of
+ * the dynamics / slack / final rows), complementarity max |z s|, s_d, s_c, converged (IPOPT's test at P->tol),
+ * acceptable}.  The point must be strictly interior (the slacks inside their relaxed bounds); returns -1 if not. */
+int tto_obca_eval_iterate(const tto_obca_problem* P, const double* x_init, const double* x_goal, const double* xref,
+                          const double* uref, const double* it, double* out) {
+    if (P->N < 1 || P->M < 1 || P->M > TTO_MAXM) return -1;
+    ws_t W;
+    if (ws_init(&W, P) != 0) return -1;
+    W.xinit = x_init; W.xgoal = x_goal; W.xref = xref; W.uref = uref;
+    W.R = M_ORIG;
+    setup_bounds(&W);
+    unpack_iterate(&W, it);
+    int bad = 0;
+    (void)barrier(&W, W.x, W.u, W.w, W.s, W.sf, NULL, NULL, 1.0, &bad);
+    linearise(&W);
+    const opterr_t o = opt_error(&W, 0.0);
+    out[0] = o.E0; out[1] = o.dinf; out[2] = o.pinf; out[3] = o.c0; out[4] = o.sd; out[5] = o.sc;
+    out[6] = converged(&o, P->tol); out[7] = acceptable_pt(&o, P->acc_tol);
+    free(W.mem);
+    return bad ? -1 : 0;
 }

@@ -74,6 +74,18 @@ int tto_obca_solve_batch(const tto_obca_problem* P, int B, const double* x_init,
                          const double* xref, const double* uref, const double* z_guess, double* z_out,
                          int* status, int* iters, double* kkt, int nthreads);
 
+/* Same, plus the final primal-dual iterate of every instance (it_out [B][tto_obca_iterate_len], or NULL) in the layout
+ * of the GPU library's diagnostic export (tt_obca_solve_batch_iterate in include/ttmpc.h). */
+int tto_obca_solve_batch_it(const tto_obca_problem* P, int B, const double* x_init, const double* x_goal,
+                            const double* xref, const double* uref, const double* z_guess, double* z_out,
+                            int* status, int* iters, double* kkt, double* it_out, int nthreads);
+long long tto_obca_iterate_len(int N, int M);
+/* IPOPT's optimality error (scaled E_0; unscaled dual infeasibility, primal infeasibility, complementarity; s_d, s_c;
+ * the converged / acceptable verdicts of IPOPT's convergence check) at a given primal-dual iterate -- an independent
+ * evaluation of the GPU's end point.  out[8]. */
+int tto_obca_eval_iterate(const tto_obca_problem* P, const double* x_init, const double* x_goal, const double* xref,
+                          const double* uref, const double* it, double* out);
+
 #ifdef __cplusplus
 }
 #endif

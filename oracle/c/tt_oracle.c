@@ -10,8 +10,11 @@
  * Algorithm (restatement of IPOPT's primal-dual barrier method as configured by
  * mpc_control.py:35-39 -- tol 1e-8, acceptable 1e-6 x15, monotone mu, tau = max(.99, 1-mu),
  * bound_relax_factor 1e-8, bound_push/frac 1e-2, kappa_eps 10, kappa_mu .2, theta_mu 1.5,
- * kappa_sigma 1e10, exact Lagrangian Hessian).  Globalisation: l1-merit backtracking with one
- * second-order correction (IPOPT uses a filter; only the iterate path differs, not the KKT point).
+ * kappa_sigma 1e10, exact Lagrangian Hessian).  Globalisation: IPOPT's filter line search with one
+ * second-order correction.  Termination: IPOPT's OptimalityErrorConvergenceCheck -- the scaled error E_0 <= tol
+ * AND the unscaled dual infeasibility <= dual_inf_tol (1), constraint violation <= constr_viol_tol (1e-4) and
+ * complementarity <= compl_inf_tol (1e-4); "acceptable" with acceptable_tol and 1e10 / 1e-2 / 1e-2.  Barrier floor
+ * of MonotoneMuUpdate::CalcNewMuAndTau: min(tol, compl_inf_tol) / (barrier_tol_factor + 1).
  * Linear algebra: full (n+m) KKT in banded storage (half-bandwidth 13 for the stage-interleaved
  * ordering [y_k, x_k, u_k]), LU with partial pivoting (LAPACK dgbtf2/dgbtrs restated), inertia-free
  * curvature test for the Hessian regularisation.
@@ -25,6 +28,14 @@
 #include <string.h>
 
 #define TTO_MAX_FILTER 16 /* = kTrackFilter of the GPU kernel */
+/* IPOPT defaults of the convergence check (OptimalityErrorConvergenceCheck) and of the barrier floor */
+#define DUAL_INF_TOL 1.0
+#define CONSTR_VIOL_TOL 1e-4
+#define COMPL_INF_TOL 1e-4
+#define ACC_DUAL_INF_TOL 1e10
+#define ACC_CONSTR_VIOL_TOL 1e-2
+#define ACC_COMPL_INF_TOL 1e-2
+#define BARRIER_TOL_FACTOR 10.0
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -324,6 +335,7 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
     const double kappa1 = 1e-2, kappa2 = 1e-2, smax = 100.0, kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5;
     const double kappa_sigma = 1e10, eta = 1e-4;
     const double tol = P->tol, acc_tol = P->acc_tol;
+    const double mu_min = fmin(tol, COMPL_INF_TOL) / (BARRIER_TOL_FACTOR + 1.0); /* MonotoneMuUpdate floor */
     /* weights: Qw = diag(wq) Qs diag(wq) (mpc_control_fuzzy.py:23-24); Qs = sym(Q) */
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) {
@@ -424,18 +436,22 @@ static int solve_one(const tto_problem* P, ws_t* w, const double* xinit, const d
         if (getenv("TTO_DEBUG"))
             fprintf(stderr, "it %3d E0 %.3e dinf %.3e pinf %.3e c0 %.3e mu %.2e sd %.2e nu %.2e\n", iter, E0, dinf, pinf, c0,
                     mu, sd, nu);
-        if (E0 <= tol) { status = 0; break; }
-        if (E0 <= acc_tol) {
+        /* IPOPT's convergence test: the scaled error and the unscaled dual infeasibility, constraint violation
+         * (the dynamics rows: max |c| = pinf) and complementarity max |z s| = c0 */
+        const int conv = E0 <= tol && dinf <= DUAL_INF_TOL && pinf <= CONSTR_VIOL_TOL && c0 <= COMPL_INF_TOL;
+        const int accp = E0 <= acc_tol && dinf <= ACC_DUAL_INF_TOL && pinf <= ACC_CONSTR_VIOL_TOL && c0 <= ACC_COMPL_INF_TOL;
+        if (conv) { status = 0; break; }
+        if (accp) {
             if (++acc_count >= P->acc_iter) { status = 1; break; }
         } else {
             acc_count = 0;
         }
-        if (iter >= P->max_iter) { status = E0 <= acc_tol ? 1 : 2; break; }
+        if (iter >= P->max_iter) { status = accp ? 1 : 2; break; }
         /* ---- barrier parameter update (monotone, Fiacco-McCormick) ---- */
         for (;;) {
             double Emu = fmax(fmax(dinf / sd, pinf), cmu / sc);
-            if (Emu <= kappa_eps * mu && mu > tol / 10.0 * 1.0000001) {
-                mu = fmax(tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
+            if (Emu <= kappa_eps * mu && mu > mu_min * 1.0000001) {
+                mu = fmax(mu_min, fmin(kappa_mu * mu, pow(mu, theta_mu)));
                 tau = fmax(0.99, 1.0 - mu);
                 nf = 0; /* IPOPT resets the filter on every barrier update */
                 cmu = 0.0;

@@ -152,16 +152,31 @@ def obca_n(N, M):
     return N * (8 + 16 * M) + 6 + 16 * M
 
 
-def obca_solve_batch(P, x0, x_goal=None, xref=None, uref=None, z_guess=None, nthreads=0):
-    """-> (z (B,n), status, iters, kkt).  plan mode needs x_goal (B,6); track mode xref/uref."""
+def _obca_lib():
     L = lib()
     if not hasattr(L, "_obca_ready"):
         dp = C.POINTER(C.c_double)
         ip = C.POINTER(C.c_int)
-        L.tto_obca_solve_batch.argtypes = [C.POINTER(TTOObcaProblem), C.c_int, dp, dp, dp, dp, dp, dp, ip, ip, dp,
-                                           C.c_int]
-        L.tto_obca_solve_batch.restype = C.c_int
+        L.tto_obca_solve_batch_it.argtypes = [C.POINTER(TTOObcaProblem), C.c_int, dp, dp, dp, dp, dp, dp, ip, ip, dp,
+                                              dp, C.c_int]
+        L.tto_obca_solve_batch_it.restype = C.c_int
+        L.tto_obca_iterate_len.argtypes = [C.c_int, C.c_int]
+        L.tto_obca_iterate_len.restype = C.c_longlong
+        L.tto_obca_eval_iterate.argtypes = [C.POINTER(TTOObcaProblem), dp, dp, dp, dp, dp, dp]
+        L.tto_obca_eval_iterate.restype = C.c_int
         L._obca_ready = True
+    return L
+
+
+def obca_iterate_len(N, M):
+    """Length of the primal-dual iterate export (include/ttmpc.h tt_obca_iterate_len; tt_obca.c pack_iterate)."""
+    return 30 * (N + 1) + 64 * M * (N + 1) + 24
+
+
+def obca_solve_batch(P, x0, x_goal=None, xref=None, uref=None, z_guess=None, nthreads=0, iterate=False):
+    """-> (z (B,n), status, iters, kkt) [+ the final primal-dual iterates (B, obca_iterate_len) with iterate=True].
+    plan mode needs x_goal (B,6); track mode xref/uref."""
+    L = _obca_lib()
     N, M = P.N, P.M
     n = obca_n(N, M)
     x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, 6)
@@ -175,12 +190,41 @@ def obca_solve_batch(P, x0, x_goal=None, xref=None, uref=None, z_guess=None, nth
     st = np.zeros(B, dtype=np.int32)
     it = np.zeros(B, dtype=np.int32)
     kk = np.zeros(B)
-    rc = L.tto_obca_solve_batch(C.byref(P), B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg), _ptr(z),
-                                st.ctypes.data_as(C.POINTER(C.c_int)), it.ctypes.data_as(C.POINTER(C.c_int)),
-                                _ptr(kk), int(nthreads))
+    I = np.zeros((B, obca_iterate_len(N, M))) if iterate else None
+    rc = L.tto_obca_solve_batch_it(C.byref(P), B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg), _ptr(z),
+                                   st.ctypes.data_as(C.POINTER(C.c_int)), it.ctypes.data_as(C.POINTER(C.c_int)),
+                                   _ptr(kk), _ptr(I), int(nthreads))
     if rc != 0:
         raise RuntimeError(f"tto_obca_solve_batch failed: {rc}")
-    return z, st, it, kk
+    return (z, st, it, kk, I) if iterate else (z, st, it, kk)
+
+
+def obca_eval_iterate(P, x0, iterate, x_goal=None, xref=None, uref=None):
+    """IPOPT's optimality error at a given primal-dual point (tto_obca_eval_iterate), one instance per row:
+    -> dict of arrays E0 (scaled, IPOPT eq. (5)), dinf (unscaled dual infeasibility), pinf, compl (max |z s|), sd, sc,
+    converged / acceptable (IPOPT's convergence check at P.tol / P.acc_tol), interior (the slacks inside the bounds)."""
+    L = _obca_lib()
+    N = P.N
+    x0 = np.ascontiguousarray(x0, dtype=np.float64).reshape(-1, 6)
+    B = x0.shape[0]
+    I = np.ascontiguousarray(iterate, dtype=np.float64).reshape(B, obca_iterate_len(N, P.M))
+    cv = lambda a, shp: None if a is None else np.ascontiguousarray(a, dtype=np.float64).reshape(shp)  # noqa: E731
+    xg, xr, ur = cv(x_goal, (B, 6)), cv(xref, (B, N + 1, 6)), cv(uref, (B, N, 2))
+    out = np.zeros((B, 8))
+    ok = np.zeros(B, dtype=bool)
+    for b in range(B):
+        o = np.zeros(8)
+        rc = L.tto_obca_eval_iterate(C.byref(P), _ptr(x0[b]), None if xg is None else _ptr(xg[b]),
+                                     None if xr is None else _ptr(xr[b]), None if ur is None else _ptr(ur[b]),
+                                     _ptr(I[b]), _ptr(o))
+        out[b] = o
+        ok[b] = rc == 0
+    keys = ("E0", "dinf", "pinf", "compl", "sd", "sc")
+    r = {k: out[:, i] for i, k in enumerate(keys)}
+    r["converged"] = out[:, 6] != 0
+    r["acceptable"] = out[:, 7] != 0
+    r["interior"] = ok
+    return r
 
 
 def obca_split(z, N, M):

@@ -36,15 +36,34 @@ def _oracle(N, obs, mode=0, params=P6, bounds=None, **kw):
     return co.make_obca_problem(N, params, sc.OBCA_Q, sc.OBCA_R, *b, obs, mode=mode, **kw)
 
 
+def _ipopt_check_at_gpu_points(P, x0, I, st, kk, **inputs):
+    """Independent check of the GPU's own end points: for every instance the kernel reports optimal
+    (status 0), the ORACLE evaluates IPOPT's optimality error at the GPU's returned primal-dual iterate (the diagnostic
+    export tt_obca_solve_batch_iterate; oracle/c/tt_obca.c tto_obca_eval_iterate): the point must be interior and pass
+    IPOPT's full convergence test there -- scaled E_0 <= tol AND the unscaled dual infeasibility <= dual_inf_tol (1),
+    complementarity <= compl_inf_tol (1e-4) -- and the oracle's E_0 must agree with the one the kernel reported."""
+    from oracle import c_oracle as co
+    opt = np.flatnonzero(st == 0)
+    if opt.size == 0:
+        return None
+    r = co.obca_eval_iterate(P, x0[opt], I[opt], **{k: None if v is None else v[opt] for k, v in inputs.items()})
+    assert r["interior"].all(), opt[~r["interior"]]
+    assert r["converged"].all(), [(int(b), float(e), float(d), float(c), float(sd)) for b, e, d, c, sd, ok in
+                                  zip(opt, r["E0"], r["dinf"], r["compl"], r["sd"], r["converged"]) if not ok]
+    assert np.all(np.abs(r["E0"] - kk[opt]) <= 1e-9), np.abs(r["E0"] - kk[opt]).max()
+    return r
+
+
 def test_toy_plan_matches_oracle_and_is_kkt():
     from oracle import c_oracle as co
     from oracle.obca_nlp import ObcaNLP
     from ttmpc import collision
     from ttmpc import scenarios as sc
     N, M, obs, x0, xg, zg = toy_plan()
-    X, U, Z, st, it, kk = _solver(N, obs).solve(x0, xg, z_guess=zg)
+    X, U, Z, st, it, kk, I = _solver(N, obs).solve(x0, xg, z_guess=zg, iterate=True)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(N, obs), x0, xg, z_guess=zg)
     assert np.array_equal(st, stc) and np.all(st == 0)
+    _ipopt_check_at_gpu_points(_oracle(N, obs), x0, I, st, kk, x_goal=xg)
     nlp = ObcaNLP(N, M, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
     for b in range(len(x0)):  # same local optimum (primal; the OBCA duals are not unique)
         (Xg, Ug, _, _), (Xo, Uo, _, _) = nlp.split(Z[b]), nlp.split(zc[b])
@@ -72,8 +91,10 @@ def test_mpc_obca_windows_match_oracle():
     x0, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 16, 50, seed=0)
     p = dict(P6, dt=0.05)
     bnd = (sc.XLB, sc.XUB, sc.ULB, sc.UUB)
-    X, U, Z, st, it, kk = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0, xref=xr, uref=ur)
+    X, U, Z, st, it, kk, I = _solver(50, obs, ttmpc.TT_VARIANT_TRACK_OBCA, p, bnd).solve(x0, xref=xr, uref=ur,
+                                                                                       iterate=True)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0, xref=xr, uref=ur, nthreads=16)
+    _ipopt_check_at_gpu_points(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0, I, st, kk, xref=xr, uref=ur)
     assert np.array_equal(st, stc), (st, stc)           # identical statuses on all 16 windows
     both = (st <= 1) & (stc <= 1)
     assert both.sum() >= 9, (st, stc)
@@ -107,8 +128,11 @@ def test_c4_test_cases_vs_oracle():
     from ttmpc import collision
     from ttmpc import scenarios as sc
     obs, x0, xg, zg = _c4_cases(14)
-    X, U, Z, st, it, kk = _solver(200, obs).solve(x0, xg, z_guess=zg)
+    X, U, Z, st, it, kk, I = _solver(200, obs).solve(x0, xg, z_guess=zg, iterate=True)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs), x0, xg, z_guess=zg, nthreads=16)
+    # every GPU-optimal end point -- in particular where the two runs end at different points or only the GPU
+    # converges -- passes IPOPT's full convergence test as the oracle evaluates it at the GPU's primal-dual point
+    _ipopt_check_at_gpu_points(_oracle(200, obs), x0, I, st, kk, x_goal=xg)
     assert (st == stc).sum() >= 12, (st, stc)
     gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
@@ -188,8 +212,9 @@ def test_c4_replan_subset_vs_oracle():
     g = np.load(GOLDEN / "reference_numpy.npz")
     obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
     x0, xg, zg = sc.obca_replan_batch(g["state_traj"], 16, 200, 6, seed=0)
-    X, U, Z, st, it, kk = _solver(200, obs).solve(x0, xg, z_guess=zg)
+    X, U, Z, st, it, kk, I = _solver(200, obs).solve(x0, xg, z_guess=zg, iterate=True)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(200, obs), x0, xg, z_guess=zg, nthreads=16)
+    _ipopt_check_at_gpu_points(_oracle(200, obs), x0, I, st, kk, x_goal=xg)
     ok = st <= 1
     assert ok.sum() >= 15 and (stc <= 1).sum() >= 15, (st, stc)
     both = ok & (stc <= 1)
@@ -209,9 +234,10 @@ def test_c4_full_batch_properties_and_determinism():
     from ttmpc import collision
     obs, x0, xg, zg = _c4_cases(256, seed=1)
     s = _solver(200, obs)
-    X, U, Z, st, it, kk = s.solve(x0, xg, z_guess=zg)
+    X, U, Z, st, it, kk, I = s.solve(x0, xg, z_guess=zg, iterate=True)
     X2, U2, Z2, st2, it2, kk2 = s.solve(x0, xg, z_guess=zg)
     assert np.array_equal(Z, Z2) and np.array_equal(st, st2)   # bitwise-deterministic
+    _ipopt_check_at_gpu_points(_oracle(200, obs), x0, I, st, kk, x_goal=xg)
     ok = st <= 1
     gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
@@ -237,8 +263,9 @@ def test_default_plan_matches_oracle():
     g = np.load(GOLDEN / "oracle_default_plan.npz")
     ob = np.load(GOLDEN / "reference_numpy.npz")["obstacles"].reshape(-1, 4)
     N, M = 200, ob.shape[0]
-    X, U, Z, st, it, kk = _solver(N, ob).solve(g["x_init"], g["x_goal"], z_guess=g["z_guess"])
+    X, U, Z, st, it, kk, I = _solver(N, ob).solve(g["x_init"], g["x_goal"], z_guess=g["z_guess"], iterate=True)
     assert st[0] == int(g["status"][0]) == 0, (st, it, kk)
+    _ipopt_check_at_gpu_points(_oracle(N, ob), g["x_init"], I, st, kk, x_goal=g["x_goal"])
     Xc, Uc, _, _ = co.obca_split(g["z"], N, M)
     assert np.abs(X - Xc).max() <= 1e-6 and np.abs(U - Uc).max() <= 1e-6
     d = X[0] - g["x_goal"][0]
