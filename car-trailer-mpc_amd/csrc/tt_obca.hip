@@ -628,7 +628,7 @@ __device__ __forceinline__ int blk_factor(Blk& k, const double* sig_w, double dw
     // Haynsworth: the block has IPOPT's inertia (8, 4, 0) iff negT == negA; negT > negA leaves it with too few negative
     // eigenvalues (its rows need delta_c), negT < negA with too many (negative curvature: delta_x)
     // (pd mode: A was positive definite, so a negative T pivot, -2, means too few negative eigenvalues)
-    if (negT < 0) return negT == -1 ? F_ZERO : F_MANY;
+    if (negT < 0) return negT == -1 ? F_ZERO : F_FEW;
     if (negT != negA) return negT > negA ? F_FEW : F_MANY;
     double Wm[4][4];  // LT^-1 G
 #pragma unroll

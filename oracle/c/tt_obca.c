@@ -803,7 +803,7 @@ static int block_factor(ws_t* W, int bi, double dw, double dc, double* Q) {
         /* pd mode: A is positive definite here (negA = 0), so a negative pivot of T leaves the block with too FEW
          * negative eigenvalues by Haynsworth (IPOPT: singular -> delta_c), not too many */
         const int f = chol(LT, 4);
-        if (f != 0) return f;
+        if (f != 0) return f == F_MANY ? F_FEW : f;
         for (int r = 0; r < 4; ++r) ST[r] = 1.0;
     }
     /* Q += W_xx - Z'Z + G' T^-1 G   (T^-1 G via two triangular solves per column) */
