@@ -727,6 +727,20 @@ def main_obca(args):
     if blocked is not None:
         solver_rec["infeasible_by_construction"] = int(blocked.sum())
         solver_rec["converged_of_feasible"] = f"{int(np.sum((status <= 1) & ~blocked))}/{int(np.sum(~blocked))}"
+    census = REPO / "tests" / "golden" / "c4_census.json"
+    if args.config == "c4" and (B, N, M, rank_seed(rank)) == (256, 200, 6, 7) and census.exists():
+        # instance-by-instance agreement with the oracle census of this exact batch (tests/golden/make_c4_census.py): which
+        # failures the restated IPOPT shares (its behaviour) and which are the kernel's alone (drift)
+        cen = json.loads(census.read_text()).get("bench")
+        if cen and cen.get("B") == B:
+            stc = np.asarray(cen["status"])
+            solver_rec["oracle_census"] = {
+                "oracle_status_counts": {str(k): int(v) for k, v in zip(*np.unique(stc, return_counts=True))},
+                "equal_status": int((status == stc).sum()),
+                "shared_failures": np.flatnonzero((status > 1) & (stc > 1)).tolist(),
+                "kernel_only_failures": np.flatnonzero((status > 1) & (stc <= 1)).tolist(),
+                "oracle_only_failures": np.flatnonzero((status <= 1) & (stc > 1)).tolist(),
+                "source": "tests/golden/c4_census.json (oracle/c/tt_obca.c on the same seeded batch)"}
     traffic, traffic_src = obca_traffic(args.config, float(iters.sum()))
     out = {
         "metric": f"OBCA {'plan' if args.config != 'cobs' else 'MPC+OBCA'} solves/sec (N={N}, M={M} obstacles, "
@@ -793,8 +807,8 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 
 # rocprofv3 PMC passes (tools/hbm_passes.sh) that the default C2 / C3 lines quote as roofline.traffic: the kernel
 # the bench runs; re-profile after a tracking-kernel change
-TRACK_PMC = {"c2": "profiles/r04/final/pmc_c2", "c3": "profiles/r04/final/pmc_c3"}
-TRACK_PMC_SOURCE = "profiles/r04/final/SOURCE.txt"
+TRACK_PMC = {"c2": "profiles/r05/session_b/pmc_c2", "c3": "profiles/r05/session_b/pmc_c3"}
+TRACK_PMC_SOURCE = "profiles/r05/SOURCE.txt"
 
 
 # committed PMC passes of obca_kernel (tools/obca_pmc.sh, one short probe per config on the shipped kernel): HBM bytes per

@@ -49,7 +49,8 @@ def main():
     z, st, it, kk = co.obca_solve_batch(P, x0, xg, z_guess=zg, nthreads=1)
     X, Uo, _, _ = co.obca_split(z, N, M)
     c = plan_cost(X[0], Uo[0], xg[0])
-    prov = ("C oracle (oracle/c/tt_obca.c, restated IPOPT incl. its perturbation handler) optimum of the reference's "
+    prov = ("C oracle (oracle/c/tt_obca.c, restated IPOPT incl. its perturbation handler and, since round 5, its full "
+            "convergence test) optimum of the reference's "
             "default OBCA problem; not produced by the reference (CasADi/IPOPT absent). OBCA optimality parity with "
             "IPOPT itself is unpinned beyond dynamics, bounds and collision (DESIGN.md section 5).")
     np.savez_compressed(HERE / "oracle_default_plan.npz", x_init=x0, x_goal=xg, z_guess=zg, z=z, status=st,
