@@ -558,7 +558,7 @@ static int chol(double* a, int n) {
  * positive definite matrix (IPOPT's inertia test needs the signs, not definiteness).  Returns the number of negative pivots, -1 on a (numerically) zero pivot. */
 /* TTO_CENSUS diagnostic counters (per solve): factorisations, block inertia failures by kind, zero pivots,
  * refinements that stop above IPOPT's residual_ratio_singular 1e-5 */
-static _Thread_local long g_cen[8];
+static _Thread_local long g_cen[10]; /* [8] refinement corrections, [9] refined step solves */
 static int schol(double* a, int n, double* S) {
     int neg = 0;
     for (int j = 0; j < n; ++j) {
@@ -2206,6 +2206,7 @@ static int refined_solve(ws_t* W, double mu, double* cres, double* dres, double*
     }
     solve_rhs(W, mu, cres, dres, fres);
     if ((W->P->opts & TTO_OPT_NO_REFINE) || W->lsq) return 0;
+    ++g_cen[9];
     const int r3 = (W->P->opts & TTO_OPT_R3_PERTURB) != 0;
     double bnorm = 0.0;
     double res = newton_resid(W, mu, cres, dres, fres, &bnorm);
@@ -2214,6 +2215,7 @@ static int refined_solve(ws_t* W, double mu, double* cres, double* dres, double*
     int quit = 0;
     for (int it = 0; !quit && (it < 1 || ratio > 1e-10); ++it) {
         if (r3 && it >= 10) break;
+        ++g_cen[8];
         /* save the solution, solve for the correction with the residuals as constants, add */
         double* o = W->sol;
         memcpy(o, W->dx, N1 * 48); o += N1 * 6; memcpy(o, W->ycp, N1 * 48); o += N1 * 6;
@@ -2904,8 +2906,8 @@ static int solve_one(ws_t* W, const double* xinit, const double* xgoal, const do
     if (W->R == M_RESTO) W->R = M_ORIG;
     if (dbg) fprintf(stderr, "status %d iters %d resto %d soft %d\n", status, iter, n_resto, n_soft);
     if (getenv("TTO_CENSUS"))
-        fprintf(stderr, "CENSUS status %d iters %d fact %ld blocks_ok %ld few %ld many %ld zero %ld ref>1e-10 %ld ref>1e-5 %ld pretend %ld\n",
-                status, iter, g_cen[0], g_cen[4], g_cen[1], g_cen[2], g_cen[3], g_cen[5], g_cen[6], g_cen[7]);
+        fprintf(stderr, "CENSUS status %d iters %d fact %ld blocks_ok %ld few %ld many %ld zero %ld ref>1e-10 %ld ref>1e-5 %ld pretend %ld corr %ld solves %ld\n",
+                status, iter, g_cen[0], g_cen[4], g_cen[1], g_cen[2], g_cen[3], g_cen[5], g_cen[6], g_cen[7], g_cen[8], g_cen[9]);
     pack(W, zout);
     if (it_out) pack_iterate(W, it_out);
     if (iters_out) *iters_out = iter;

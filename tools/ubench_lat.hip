@@ -11,7 +11,7 @@
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int R = 256;
 enum { T_MFMA_C, T_MFMA_AB, T_MFMA_IND4, T_FMA, T_FMA_IND4, T_RCP, T_READLANE, T_PERM, T_DS, T_MFMA_READLANE,
-       T_DPP, NT };
+       T_DPP, T_SINCOS, T_BPERM, T_LOG, T_DIV, NT };
 static const char* names[NT] = {
     "mfma_f64_16x16x4 dependent via srcC (accumulate chain)",
     "mfma_f64_16x16x4 result -> next srcA/srcB (operand chain)",
@@ -24,6 +24,10 @@ static const char* names[NT] = {
     "ds_write_b64 -> ds_read_b64 -> v_add_f64 (per link)",
     "mfma -> accvgpr/readlane -> v_fma as next srcA (per link)",
     "DPP row op (b64 as 2x32) -> v_add_f64 (per link)",
+    "sincos(double) -> v_fma_f64 (per link)",
+    "ds_bpermute_b32 x2 (b64, lane+3) -> v_add_f64 (per link)",
+    "log(double) -> v_add_f64 (per link)",
+    "IEEE 1.0 / x (double) (per link)",
 };
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -102,6 +106,24 @@ __global__ __launch_bounds__(64) void lat(int test, double seed, double* out, un
                 const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), 0x141, 0xF, 0xF, false);
                 x = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo) + y;
             }
+            break;
+        case T_SINCOS:
+            for (int r = 0; r < R; ++r) { double sn, cs; sincos(x, &sn, &cs); x = fma(cs, 1e-3, sn) + y; }
+            break;
+        case T_BPERM:
+            for (int r = 0; r < R; ++r) {
+                const long long b = __double_as_longlong(x);
+                const int src = ((lane + 3) & 63) << 2;
+                const int lo = __builtin_amdgcn_ds_bpermute(src, (int)(b & 0xffffffffll));
+                const int hi = __builtin_amdgcn_ds_bpermute(src, (int)(b >> 32));
+                x = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo) + y;
+            }
+            break;
+        case T_LOG:
+            for (int r = 0; r < R; ++r) x = log(x) + 1.5;
+            break;
+        case T_DIV:
+            for (int r = 0; r < R; ++r) x = 1.0 / x + y;
             break;
     }
     __builtin_amdgcn_s_waitcnt(0);
