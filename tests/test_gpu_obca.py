@@ -229,8 +229,35 @@ def test_c4_replan_subset_vs_oracle():
         assert collision.sat_gap(X[b], P6, obs).min() > 0.0
 
 
+def c4_census_compare(st, X, cen, Xc):
+    """Per-instance comparison of a GPU C4 batch with the oracle census of the same batch (tests/golden/c4_census.json,
+    tests/golden/make_c4_census.py).  Returns the table: status agreement, shared / kernel-only / oracle-only failures,
+    both-converged pairs at the same end point, and which disagreements fall on rounding-sensitive instances (the oracle's
+    own status or end point changes when its guess is perturbed by one ulp)."""
+    stc = np.asarray(cen["status"])
+    sens = np.asarray(cen["rounding_sensitive"], dtype=bool)
+    ok, okc = st <= 1, stc <= 1
+    both = ok & okc
+    d = np.abs(X - Xc).max(axis=(1, 2))
+    far = both & (d > 1e-6)
+    return {"equal_status": int((st == stc).sum()), "instances": int(st.size),
+            "shared_failures": np.flatnonzero(~ok & ~okc).tolist(),
+            "kernel_only_failures": np.flatnonzero(~ok & okc).tolist(),
+            "oracle_only_failures": np.flatnonzero(ok & ~okc).tolist(),
+            "both_converged": int(both.sum()), "both_converged_same_point": int((both & ~far).sum()),
+            "both_converged_other_point": np.flatnonzero(far).tolist(),
+            "status_mismatch_not_sensitive": np.flatnonzero((st != stc) & ~sens).tolist(),
+            "other_point_not_sensitive": np.flatnonzero(far & ~sens).tolist(),
+            "rounding_sensitive": int(sens.sum())}
+
+
 def test_c4_full_batch_properties_and_determinism():
-    """BASELINE config C4 at full size: B=256 test_cases.json scenarios, N=200, M=6, max_iter 5000."""
+    """BASELINE config C4 at full size: B=256 test_cases.json scenarios, N=200, M=6, max_iter 5000, compared instance by
+    instance with the oracle's census of the same batch.  Where the GPU's status differs from the
+    oracle's, or both converge to different points, the instance must be rounding-sensitive in the oracle itself: its
+    outcome changed when the oracle's guess was perturbed by one ulp (tests/golden/make_c4_census.py), i.e. it is decided
+    by last-bit differences, which is what separates the kernel's arithmetic from the oracle's."""
+    import json
     from ttmpc import collision
     obs, x0, xg, zg = _c4_cases(256, seed=1)
     s = _solver(200, obs)
@@ -245,7 +272,15 @@ def test_c4_full_batch_properties_and_determinism():
     # infeasible by construction: they never converge, and they end as IPOPT's restoration failure (status 3)
     # instead of running to max_iter
     assert np.all(st[blocked] == 3), np.bincount(st[blocked])
-    assert ok[~blocked].mean() >= 0.85, np.bincount(st[~blocked])
+    cen = json.loads((GOLDEN / "c4_census.json").read_text())["test"]
+    Xc = np.load(GOLDEN / "c4_census_test_x.npz")["X"]
+    assert np.array_equal(np.asarray(cen["blocked"], dtype=bool), blocked)
+    tab = c4_census_compare(st, X, cen, Xc)
+    print("C4 census comparison:", json.dumps(tab))
+    # every disagreement with the oracle -- a different status, or a different optimum -- is on an instance whose
+    # outcome the oracle itself changes under a one-ulp perturbation of its guess
+    assert not tab["status_mismatch_not_sensitive"], tab
+    assert not tab["other_point_not_sensitive"], tab
     dyn = X[:, 1:] - (X[:, :-1] + 0.1 * _f(X[:, :-1], U))
     assert np.abs(dyn[ok]).max() <= 1e-8
     assert np.abs(X[ok, 0] - x0[ok]).max() <= 1e-8

@@ -1,13 +1,16 @@
-"""Oracle refinement corrections per iteration on the round-4 GPU tail instances of the bench's C4 batch (seed 7):
-max_iter 4000 and 5000 runs, TTO_CENSUS counters differenced."""
-import os, sys, json, subprocess
-os.environ["TTO_ORACLE_LIB"] = "/root/scratch/libttoracle_diag.so"
+"""Oracle refinement corrections per iteration on given instances of the bench's C4 batch (seed 7), one core each:
+    python tools/obca_corrections_census.py 13,28,37 4000 > corr4000.log   (and again with 5000)
+The TTO_CENSUS line of each solve (stderr) carries the refined step solves and corrections; differencing the max_iter 4000
+and 5000 runs gives iterations 4,000-5,000 (profiles/r05/corrections/)."""
+import os, sys, json
+from pathlib import Path
 os.environ["TTO_CENSUS"] = "1"
-sys.path[:0] = ["/root/repo", "/root/repo/car-trailer-mpc_amd"]
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO), str(REPO / "car-trailer-mpc_amd")]
 import numpy as np
 from oracle import c_oracle as co
 from ttmpc import scenarios as sc
-G = "/root/repo/tests/golden/"
+G = str(REPO / "tests" / "golden") + "/"
 obs = sc.obstacles_array(sc.load_obstacles(G + "obstacles.json"))[:6]
 cases = json.loads(open(G + "test_cases.json").read())["cases"]
 x0, xg, zg = sc.obca_case_batch(cases, 256, 200, 6, seed=7, obstacles=obs, params=sc.OBCA_PARAMS)
