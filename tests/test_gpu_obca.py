@@ -269,12 +269,15 @@ def test_c4_full_batch_properties_and_determinism():
     gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
     blocked = (gs < 0.0) | (gg < 0.0)
-    # infeasible by construction: they never converge, and they end as IPOPT's restoration failure (status 3)
-    # instead of running to max_iter
-    assert np.all(st[blocked] == 3), np.bincount(st[blocked])
     cen = json.loads((GOLDEN / "c4_census.json").read_text())["test"]
     Xc = np.load(GOLDEN / "c4_census_test_x.npz")["X"]
     assert np.array_equal(np.asarray(cen["blocked"], dtype=bool), blocked)
+    sens = np.asarray(cen["rounding_sensitive"], dtype=bool)
+    # infeasible by construction: they never converge, and they end as IPOPT's restoration failure (status 3) instead of
+    # running to max_iter -- except where the oracle itself flips between the two under a one-ulp perturbation (blocked
+    # instance 61: max_iter unperturbed, status 3 in both perturbed runs; tests/golden/c4_census.json)
+    assert np.all(st[blocked] > 1), np.bincount(st[blocked])
+    assert np.all((st[blocked] == 3) | sens[blocked]), np.flatnonzero(blocked & (st != 3))
     tab = c4_census_compare(st, X, cen, Xc)
     print("C4 census comparison:", json.dumps(tab))
     # every disagreement with the oracle -- a different status, or a different optimum -- is on an instance whose
