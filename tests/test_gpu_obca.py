@@ -95,19 +95,29 @@ def test_mpc_obca_windows_match_oracle():
                                                                                        iterate=True)
     zc, stc, itc, kkc = co.obca_solve_batch(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0, xref=xr, uref=ur, nthreads=16)
     _ipopt_check_at_gpu_points(_oracle(50, obs, co.OBCA_TRACK, p, bnd), x0, I, st, kk, xref=xr, uref=ur)
-    assert np.array_equal(st, stc), (st, stc)           # identical statuses on all 16 windows
+    sens = _sensitive("windows")
+    # identical statuses on every window whose oracle outcome is not rounding-sensitive (measured: all 16)
+    assert np.array_equal(st[~sens], stc[~sens]), (st, stc, np.flatnonzero(sens))
     both = (st <= 1) & (stc <= 1)
     assert both.sum() >= 9, (st, stc)
     Xc = co.obca_split(zc, 50, 11)[0]
     # the same optimum: to 1e-8 wherever both runs stop at the tol-1e-8 optimum (to round-off where they take the
     # same path); a run that stops at an acceptable point (acceptable_tol 1e-6 on the scaled KKT error, 15 times)
     # is compared within that tolerance's reach
-    opt = both & (st == 0) & (stc == 0)
+    opt = both & (st == 0) & (stc == 0) & ~sens
     assert np.max(np.abs(X[opt] - Xc[opt])) <= 1e-8, np.abs(X - Xc).max(axis=(1, 2))
-    assert np.max(np.abs(X[both] - Xc[both])) <= 1e-6, np.abs(X - Xc).max(axis=(1, 2))
+    assert np.max(np.abs(X[both & ~sens] - Xc[both & ~sens])) <= 1e-6, np.abs(X - Xc).max(axis=(1, 2))
     gap = collision.sat_gap(x0[:, :4], p, obs).min(axis=(-1, -2))
     assert np.all(st[gap < 0.0] > 1) and np.all(stc[gap < 0.0] > 1)
     assert np.all(st[:4] == 0)                          # the open-road windows
+
+
+def _sensitive(name):
+    """Instances of a small parity batch whose oracle outcome (status, or converged end point) changes under a one-ulp
+    perturbation of the oracle's input: tests/golden/obca_sensitivity.json (make_obca_sensitivity.py).  The GPU must match
+    the oracle on every other instance; on these the kernel's last-bit differences may legitimately decide otherwise."""
+    import json
+    return np.asarray(json.loads((GOLDEN / "obca_sensitivity.json").read_text())[name]["rounding_sensitive"], dtype=bool)
 
 
 def _c4_cases(B, seed=0):
@@ -133,7 +143,9 @@ def test_c4_test_cases_vs_oracle():
     # every GPU-optimal end point -- in particular where the two runs end at different points or only the GPU
     # converges -- passes IPOPT's full convergence test as the oracle evaluates it at the GPU's primal-dual point
     _ipopt_check_at_gpu_points(_oracle(200, obs), x0, I, st, kk, x_goal=xg)
-    assert (st == stc).sum() >= 12, (st, stc)
+    sens = _sensitive("c4_cases")
+    # identical statuses wherever the oracle's own outcome is not rounding-sensitive (sensitive: cases 2, 9, 11)
+    assert np.array_equal(st[~sens], stc[~sens]), (st, stc, np.flatnonzero(sens))
     gs = collision.sat_gap(x0[:, :4], P6, obs).min(axis=(-1, -2))
     gg = collision.sat_gap(xg[:, :4], P6, obs).min(axis=(-1, -2))
     blocked = (gs < 0.0) | (gg < 0.0)
@@ -144,12 +156,12 @@ def test_c4_test_cases_vs_oracle():
     assert both.sum() >= 6, (st, stc)
     Xc, Uc, _, _ = co.obca_split(zc, 200, 6)
     same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6       # same local optimum (OBCA is nonconvex)
-    assert same[both].sum() >= both.sum() - 1, np.abs(X - Xc).max(axis=(1, 2))
-    # At most one pair ends at a different point.  The two runs compute the same iterates while they stay in lockstep
-    # (test_obca_lockstep_with_oracle); these runs last 1,000-5,000 iterations, and once rounding has separated them
-    # (after ~50-400 iterations on this workload) an optimal pair may end in a different basin of the
-    # nonconvex NLP.  Both ends are then "optimal" by IPOPT's scaled test (E_0 <= 1e-8 with the multiplier scaling
-    # s_d), which the oracle and the kernel each evaluate on their own iterate.
+    # Every both-converged pair ends at the same point unless the instance is rounding-sensitive.  The two runs compute
+    # the same iterates while they stay in lockstep (test_obca_lockstep_with_oracle); these runs last 1,000-5,000
+    # iterations, and on a sensitive instance (case 9: the oracle itself ends elsewhere under a one-ulp perturbation)
+    # rounding decides the basin of the nonconvex NLP.  Both ends are then KKT points: IPOPT's full convergence test
+    # holds at the GPU's own primal-dual point (_ipopt_check_at_gpu_points above).
+    assert same[both & ~sens].all(), np.abs(X - Xc).max(axis=(1, 2))
     ok = st <= 1
     assert np.abs(X[ok, -1] - xg[ok]).max() <= 1e-2 + 1e-7
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
@@ -221,7 +233,9 @@ def test_c4_replan_subset_vs_oracle():
     assert both.sum() >= 14, (st, stc)
     Xc = co.obca_split(zc, 200, 6)[0]
     same = np.abs(X - Xc).max(axis=(1, 2)) <= 1e-6
-    assert same[both].all(), np.abs(X - Xc).max(axis=(1, 2))[both]   # the same local optimum wherever both stop
+    sens = _sensitive("replans")
+    # the same local optimum wherever both stop, except on rounding-sensitive re-plans
+    assert same[both & ~sens].all(), np.abs(X - Xc).max(axis=(1, 2))[both]
     nlp = ObcaNLP(200, 6, P6, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB, sc.OBCA_UUB, obs)
     for b in np.flatnonzero(ok):
         gv, lbg, ubg = nlp.g(Z[b], x0[b], xg[b])
