@@ -30,8 +30,9 @@ struct TrackArgs {
 
 // phases timed by the TT_STAMPS diagnostic build
 // PH_NRIC / PH_NTRIAL: counts (Riccati attempts, line-search trials), not cycles
-enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC, PH_UPDATE, PH_NRIC, PH_NTRIAL, PH_TOTAL,
-       kNumPhases };
+// PH_X0..PH_X7: sub-phase slots for finer TT_STAMPS instrumentation inside a phase (SUBSTAMP in tt_track.hip)
+enum { PH_LOAD = 0, PH_LIN, PH_MU_BAR, PH_RIC, PH_FWD, PH_STEP, PH_MERIT, PH_SOC, PH_UPDATE, PH_NRIC, PH_NTRIAL,
+       PH_X0, PH_X1, PH_X2, PH_X3, PH_X4, PH_X5, PH_X6, PH_X7, PH_TOTAL, kNumPhases };
 
 // LDS: fixed head + rows per stage (doubles); see tt_track.hip for the map.
 // 116 used + 1 zero pad + 1 unused.  The even stride (= 2 mod 4, 944 B) keeps every stage record 16-B aligned and makes

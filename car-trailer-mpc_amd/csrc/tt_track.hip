@@ -226,9 +226,11 @@ struct Stamps {
 };
 #define STAMP(ph) stamps.mark(ph)
 #define COUNT(ph) (++stamps.acc[ph])
+#define SUBSTAMP(c, n) ((c).st->mark(PH_X0 + (n)))
 #else
 #define STAMP(ph) ((void)0)
 #define COUNT(ph) ((void)0)
+#define SUBSTAMP(c, n) ((void)0)
 #endif
 
 // Armijo test with IPOPT's round-off allowance (Compare_le: lhs - rhs <= 10 eps |reference|)
@@ -255,6 +257,10 @@ struct Ctx {
     __device__ __forceinline__ double& h(int i) const { return sm[i]; }
     // bit 16 of a specialised bound pattern: Q and R are diagonal (the reference's Q = I, R = 10 I)
     static constexpr bool kDiag = BM >= 0 && ((BM >> 16) & 1);
+    // bit 17: the two-waves-per-SIMD build.  The one-wave builds issue every LDS read of a stage-parallel pass before its
+    // stores (kLF, "loads first": with one wave per SIMD nothing hides a read queued behind a store); the two-wave build
+    // keeps the per-variable order, whose shorter live ranges suit its 256-register budget.  Same arithmetic either way.
+    static constexpr bool kLF = !(BM >= 0 && ((BM >> 17) & 1));
     __device__ __forceinline__ bool hl(int v) const {
         if constexpr (BM >= 0) return (BM >> v) & 1;
         else return sm[hLB + v] > -INFINITY;
@@ -294,6 +300,9 @@ struct Ctx {
     mutable double ts0, tc0, ts1, tc1, ts2, tc2;
     mutable double t_alpha;
     mutable int t_dz, t_ok;
+#ifdef TT_STAMPS
+    struct Stamps* st;  // diagnostic build: sub-phase clocks (SUBSTAMP)
+#endif
 };
 
 // sin / cos of theta, psi, phi of a stage.  Lane pairs: the two lanes evaluate theta (part 0) and phi
@@ -388,6 +397,270 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
     double dinf = 0.0, pinf = 0.0, zmx = -INFINITY, zmn = INFINITY, sy = 0.0, sz = 0.0, cost = 0.0, th = 0.0,
            logs = 0.0;
     bool fin = true, bad = false;
+    if constexpr (Ctx<BM>::kLF) {
+    if (c.pair) {
+        // lane pairs: both lanes linearise the dynamics (the curvature and dt*J feed both lanes' gradient
+        // rows), each writes and accounts for its own rows (2q + part) and its own variables (2t + part)
+        const int p = c.part();
+        for (int k = c.k0(); k <= N; k += c.kst()) {
+            const bool st = k < N;
+            double x[6], u[2] = {0.0, 0.0}, yk[6], y1[6] = {0, 0, 0, 0, 0, 0}, aj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            // Every LDS read of the stage is issued before the pass's first store: a read queued behind a store waits
+            // for it, and the per-variable load -> compute -> store order made the variable loop a chain of twelve LDS
+            // round trips (SUBSTAMP census, profiles/r05/track_ab/).  The arithmetic is unchanged (bitwise).
+            double zl[4] = {0, 0, 0, 0}, zu[4] = {0, 0, 0, 0}, lbv[4] = {0, 0, 0, 0}, ubv[4] = {0, 0, 0, 0};
+            double qw[3], xi0[3] = {0, 0, 0}, xn[3] = {0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { x[i] = c.r(rX + i, k); yk[i] = c.r(rY + i, k); }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int vb = 2 * t, v = vb + p;
+                if (vb >= 6 && k == N) break;
+                if (c.hl(vb)) { zl[t] = c.r(rZL + v, k); lbv[t] = c.lb(v); }
+                if (c.hu(vb)) { zu[t] = c.r(rZU + v, k); ubv[t] = c.ub(v); }
+            }
+#pragma unroll
+            for (int t = 0; t < 3; ++t) qw[t] = c.h(hQW + (2 * t + p) * 7);
+            const double rw = c.h(hRW + p * 3);
+            if (k == 0)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) xi0[q] = c.h(hXI + 2 * q + p);
+            if (st) {
+                u[0] = c.r(rX + 6, k);
+                u[1] = c.r(rX + 7, k);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) y1[i] = c.r(rY + i, k + 1);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) xn[q] = c.r(rX + 2 * q + p, k + 1);
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) sy += fabs(psel(p, yk[2 * q], yk[2 * q + 1]));
+            double cc0[3] = {0, 0, 0}, cc1[3] = {0, 0, 0}, wc[7];
+            if (k == 0) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const double cc = psel(p, x[2 * q], x[2 * q + 1]) - xi0[q];
+                    cc0[q] = cc;
+                    pinf = fmax(pinf, fabs(cc));
+                    th += fabs(cc);
+                }
+            }
+            if (st) {
+                double fo[6];
+                model_lin(c, x, u, y1, fo, aj, wc);
+                SUBSTAMP(c, 5);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const double cc = xn[q] - (psel(p, x[2 * q], x[2 * q + 1]) + c.dt * psel(p, fo[2 * q], fo[2 * q + 1]));
+                    cc1[q] = cc;
+                    pinf = fmax(pinf, fabs(cc));
+                    th += fabs(cc);
+                }
+            }
+            LogSum ls;
+            double gfv[4] = {0, 0, 0, 0}, sgv[4] = {0, 0, 0, 0}, dbv[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int vb = 2 * t, v = vb + p;
+                if (vb >= 6 && k == N) break;
+                double gf, g, xv;
+                if (vb < 6) {
+                    const double dxr = psel(p, x[vb], x[vb + 1]) - c.xr(v, k);
+                    gf = qw[t] * dxr;
+                    cost += dxr * gf;
+                    gf *= 2.0;
+                    g = gf + psel(p, yk[vb], yk[vb + 1]);
+                    if (k < N) g -= psel(p, y1[vb], y1[vb + 1]) + (p ? colJ(aj, vb + 1, y1, 1) : colJ(aj, vb, y1, 1));
+                    xv = psel(p, x[vb], x[vb + 1]);
+                } else {
+                    const double du = psel(p, u[0], u[1]) - c.ur(p, k);
+                    gf = rw * du;
+                    cost += du * gf;
+                    gf *= 2.0;
+                    g = gf - c.dt * psel(p, y1[5], y1[4]);
+                    xv = psel(p, u[0], u[1]);
+                }
+                gfv[t] = gf;
+                double sg = 0.0, db = 0.0;
+                if (c.hl(vb)) {
+                    const double sl = xv - lbv[t], rs = frcp(sl);
+                    g -= zl[t];
+                    zmx = fmax(zmx, zl[t] * sl);
+                    zmn = fmin(zmn, zl[t] * sl);
+                    sz += zl[t];
+                    sg += zl[t] * rs;
+                    db -= rs;
+                    if (sl <= 0.0) bad = true; else ls.add(sl);
+                }
+                if (c.hu(vb)) {
+                    const double su = ubv[t] - xv, rs = frcp(su);
+                    g += zu[t];
+                    zmx = fmax(zmx, zu[t] * su);
+                    zmn = fmin(zmn, zu[t] * su);
+                    sz += zu[t];
+                    sg += zu[t] * rs;
+                    db += rs;
+                    if (su <= 0.0) bad = true; else ls.add(su);
+                }
+                sgv[t] = sg;
+                dbv[t] = db;
+                if (!isfinite(g)) fin = false;
+                dinf = fmax(dinf, fabs(g));
+            }
+            // ---- the stage's stores, after every read ----
+            if (k == 0)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) c.r(rCC + 2 * q + p, 0) = cc0[q];
+            if (st) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    if (q == 4 && p) break;
+                    c.r(rAJ + 2 * q + p, k) = psel(p, aj[2 * q], aj[2 * q + 1]);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q == 3 && p) break;
+                    c.r(rWC + 2 * q + p, k) = psel(p, wc[2 * q], wc[2 * q + 1]);
+                }
+#pragma unroll
+                for (int q = 0; q < 3; ++q) c.r(rCC + 2 * q + p, k + 1) = cc1[q];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int v = 2 * t + p;
+                if (2 * t >= 6 && k == N) break;
+                c.r(rGF + v, k) = gfv[t];
+                c.r(rSG + v, k) = sgv[t];
+                c.r(rDB + v, k) = dbv[t];
+            }
+            SUBSTAMP(c, 6);
+            logs += ls.value();
+        }
+    } else
+    for (int k = c.lane; k <= N; k += W) {
+        // as in the lane-pair path: every LDS read of the stage, then the arithmetic, then the stores
+        const bool st = k < N;
+        double x[6], u[2] = {0.0, 0.0}, yk[6], y1[6] = {0, 0, 0, 0, 0, 0}, aj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        double xn[6] = {0, 0, 0, 0, 0, 0}, cc0[6] = {0, 0, 0, 0, 0, 0}, cc1[6] = {0, 0, 0, 0, 0, 0}, wc[7];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { x[i] = c.r(rX + i, k); yk[i] = c.r(rY + i, k); sy += fabs(yk[i]); }
+        if (st) {
+            u[0] = c.r(rX + 6, k);
+            u[1] = c.r(rX + 7, k);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { y1[i] = c.r(rY + i, k + 1); xn[i] = c.r(rX + i, k + 1); }
+        }
+        if (k == 0) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double cc = x[i] - c.h(hXI + i);
+                cc0[i] = cc;
+                pinf = fmax(pinf, fabs(cc));
+                th += fabs(cc);
+            }
+        }
+        if (st) {
+            double fo[6];
+            model_lin(c, x, u, y1, fo, aj, wc);
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const double cc = xn[i] - (x[i] + c.dt * fo[i]);
+                cc1[i] = cc;
+                pinf = fmax(pinf, fabs(cc));
+                th += fabs(cc);
+            }
+        }
+        // tracking cost and its gradient (no 1/2: F = dx' Qw dx + du' Rw du, grad = 2 Qw dx)
+        double dxr[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) dxr[i] = x[i] - c.xr(i, k);
+        double du0 = 0.0, du1 = 0.0;
+        if (st) { du0 = u[0] - c.ur(0, k); du1 = u[1] - c.ur(1, k); }
+        LogSum ls;
+        double gfv[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sgv[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dbv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            if (v >= 6 && k == N) break;
+            double gf;
+            if (v < 6) {
+                if constexpr (Ctx<BM>::kDiag) {
+                    gf = c.h(hQW + v * 7) * dxr[v];
+                } else {
+                    gf = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) gf += c.h(hQW + v * 6 + j) * dxr[j];
+                }
+                cost += dxr[v] * gf;
+                gf *= 2.0;
+            } else {
+                const int rr = v - 6;
+                if constexpr (Ctx<BM>::kDiag)
+                    gf = c.h(hRW + rr * 3) * (rr == 0 ? du0 : du1);
+                else
+                    gf = c.h(hRW + rr * 2) * du0 + c.h(hRW + rr * 2 + 1) * du1;
+                cost += (rr == 0 ? du0 : du1) * gf;
+                gf *= 2.0;
+            }
+            gfv[v] = gf;
+            // d/dz of the Lagrangian: grad F + y_k - A'y_{k+1} - zL + zU
+            double g = gf;
+            if (v < 6) {
+                g += yk[v];
+                if (k < N) g -= y1[v] + colJ(aj, v, y1, 1);
+            } else {
+                g -= c.dt * y1[v == 6 ? 5 : 4];
+            }
+            const double xv = v < 6 ? x[v] : u[v - 6];
+            double sg = 0.0, db = 0.0;
+            if (c.hl(v)) {
+                const double zl = c.r(rZL + v, k), s = xv - c.lb(v), rs = frcp(s);
+                g -= zl;
+                zmx = fmax(zmx, zl * s);
+                zmn = fmin(zmn, zl * s);
+                sz += zl;
+                sg += zl * rs;
+                db -= rs;
+                if (s <= 0.0) bad = true; else ls.add(s);
+            }
+            if (c.hu(v)) {
+                const double zu = c.r(rZU + v, k), s = c.ub(v) - xv, rs = frcp(s);
+                g += zu;
+                zmx = fmax(zmx, zu * s);
+                zmn = fmin(zmn, zu * s);
+                sz += zu;
+                sg += zu * rs;
+                db += rs;
+                if (s <= 0.0) bad = true; else ls.add(s);
+            }
+            sgv[v] = sg;
+            dbv[v] = db;
+            if (!isfinite(g)) fin = false;
+            dinf = fmax(dinf, fabs(g));
+        }
+        logs += ls.value();
+        // ---- the stage's stores, after every read ----
+        if (k == 0)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) c.r(rCC + i, 0) = cc0[i];
+        if (st) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) c.r(rAJ + i, k) = aj[i];
+#pragma unroll
+            for (int i = 0; i < 7; ++i) c.r(rWC + i, k) = wc[i];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) c.r(rCC + i, k + 1) = cc1[i];
+        }
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            if (v >= 6 && k == N) break;
+            c.r(rGF + v, k) = gfv[v];
+            c.r(rSG + v, k) = sgv[v];
+            c.r(rDB + v, k) = dbv[v];
+        }
+    }
+    } else {
+    // the two-wave build: the other wave on the SIMD hides the LDS round trips, and the load-first order's
+    // longer live ranges cost it more than they save (C5, profiles/r05/track_ab/)
     if (c.pair) {
         // lane pairs: both lanes linearise the dynamics (the curvature and dt*J feed both lanes' gradient
         // rows), each writes and accounts for its own rows (2q + part) and its own variables (2t + part)
@@ -585,6 +858,7 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
             dinf = fmax(dinf, fabs(g));
         }
         logs += ls.value();
+    }
     }
     Lin e;
     e.dinf = (fin && !bad) ? dinf : INFINITY;
@@ -940,7 +1214,8 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
     double ap = 1.0, az = 1.0, Dg = 0.0, rel = 0.0;
     const int p = c.part();
     for (int k = c.k0(); k <= N; k += c.kst()) {
-        double dx[6];
+        // the stage's y+ stores go after every LDS read of the stage (a read queued behind a store waits for it)
+        double dx[6], yp[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) dx[i] = c.r(dzr + i, k);
 #pragma unroll
@@ -950,7 +1225,8 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
             double s = c.r(rPV + i, k);
 #pragma unroll
             for (int j = 0; j < 6; ++j) s += c.r(rPS + (c.pair ? (p ? sym_idx(2 * q + 1, j) : sym_idx(2 * q, j)) : sym_idx(q, j)), k) * dx[j];
-            c.r(rYP + i, k) = -s;
+            if constexpr (Ctx<BM>::kLF) yp[q] = -s;
+            else c.r(rYP + i, k) = -s;
         }
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
@@ -971,6 +1247,12 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
                 ftb(zu, (c.mu + zu * d) * rs - zu, c.tau, az);
             }
         }
+        if constexpr (Ctx<BM>::kLF)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                if (c.pair && q >= 3) break;
+                c.r(rYP + (c.pair ? 2 * q + p : q), k) = yp[q];
+            }
     }
     StepInfo r;
     if (primal_pieces) {
@@ -1035,6 +1317,7 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
         }
         if (k < N) {
             const double e0 = u[0] - c.ur(0, k), e1 = u[1] - c.ur(1, k);
+            SUBSTAMP(c, 0);
             if (c.pair)
                 cost += p ? e1 * (c.h(hRW + 3) * e1) : e0 * (c.h(hRW) * e0);
             else if constexpr (Ctx<BM>::kDiag)
@@ -1053,6 +1336,18 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
             if (c.hu(vb)) { const double s = c.ub(v) - xv; if (s <= 0.0) bad = true; else ls.add(s); }
         }
         const int nrow = c.pair ? 3 : 6;
+        SUBSTAMP(c, 1);
+        // the next stage's trial state is read before any residual store of this pass (a read queued behind a store
+        // waits for it); the residual rows are stored at the end
+        constexpr bool LF = Ctx<BM>::kLF;
+        double xnv[6] = {0, 0, 0, 0, 0, 0}, cc0[6] = {0, 0, 0, 0, 0, 0}, cc1[6] = {0, 0, 0, 0, 0, 0};
+        if (LF && k < N)
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                if (q >= nrow) break;
+                const int i = c.pair ? 2 * q + p : q;
+                xnv[q] = c.r(rX + i, k + 1) + alpha * c.r(dzr + i, k + 1);
+            }
         if (k == 0) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) {
@@ -1060,7 +1355,8 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
                 const int i = c.pair ? 2 * q + p : q;
                 const double cc = psel(p, x[c.pair ? 2 * q : q], x[c.pair ? 2 * q + 1 : q]) - c.h(hXI + i);
                 th += fabs(cc);
-                if (storeC) c.r(rCT + i, 0) = cc;
+                cc0[q] = cc;
+                if (!LF && storeC) c.r(rCT + i, 0) = cc;
             }
         }
         if (k < N) {
@@ -1072,22 +1368,76 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
                 const int i = c.pair ? 2 * q + p : q;
                 const double xi = psel(p, x[c.pair ? 2 * q : q], x[c.pair ? 2 * q + 1 : q]);
                 const double fi = psel(p, fo[c.pair ? 2 * q : q], fo[c.pair ? 2 * q + 1 : q]);
-                const double xn = c.r(rX + i, k + 1) + alpha * c.r(dzr + i, k + 1);
+                const double xn = LF ? xnv[q] : c.r(rX + i, k + 1) + alpha * c.r(dzr + i, k + 1);
                 const double cc = xn - (xi + c.dt * fi);
                 th += fabs(cc);
-                if (storeC) c.r(rCT + i, k + 1) = cc;
+                cc1[q] = cc;
+                if (!LF && storeC) c.r(rCT + i, k + 1) = cc;
             }
         }
+        if (LF && storeC) {
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                if (q >= nrow) break;
+                const int i = c.pair ? 2 * q + p : q;
+                if (k == 0) c.r(rCT + i, 0) = cc0[q];
+                if (k < N) c.r(rCT + i, k + 1) = cc1[q];
+            }
+        }
+        SUBSTAMP(c, 2);
         val += cost - c.mu * ls.value();
         thl += th;
     }
+    SUBSTAMP(c, 3);
     Trial t;
     t.phi = bad ? INFINITY : val;  // any lane outside the relaxed box -> +inf
     t.th = thl;
     wred2(c.lane, t.phi, t.th, OpSum());
+    SUBSTAMP(c, 4);
     __syncthreads();
     return t;
 }
+
+// The switching condition alpha (-D)^s_phi > theta0^s_theta of the filter line search, and theta0^s_theta / (-D)^s_phi in
+// alpha_min, need two FP64 pow calls: ~1.8 k cycles per iteration on the critical path when they were evaluated up front
+// (SUBSTAMP census, profiles/r05/track_ab/).  They are now evaluated only where a decision needs them: the condition is
+// first bracketed by the binary exponents of alpha, -D and theta0, and when the two sides are more than a factor 4
+// apart (all of them in the normal range) the comparison of the pow values -- accurate to an ulp -- cannot come out
+// otherwise; the pows are computed in the remaining cases, and for alpha_min only when the line search backtracks.
+// Every decision is the one the exact pows give (the oracle evaluates them always).
+struct SwitchPow {
+    double mD, th0, pD = 0.0, pT = 0.0;
+    bool have = false;
+    __device__ __forceinline__ void pows() {
+        if (!have) {
+            // the empty volatile asm keeps the pows where a decision needs them: without it the compiler speculates
+            // them (they are pure and loop-invariant) to the front of the line search, back on the critical path
+            double a = mD, b = th0;
+            asm volatile("" : "+v"(a), "+v"(b));
+            pD = pow(a, kSPh);
+            pT = pow(b, kSTh);
+            have = true;
+        }
+    }
+    // alpha (-D)^s_phi > theta0^s_theta, for -D > 0
+    __device__ __forceinline__ bool cond(double alpha) {
+        if (th0 > 0.0 && alpha > 0.0) {
+            int e1, e2, e3;
+            (void)frexp(mD, &e1);
+            (void)frexp(th0, &e2);
+            (void)frexp(alpha, &e3);
+            // log2 of alpha (-D)^s_phi lies in [lo, hi), log2 of theta0^s_theta in [tlo, thi)
+            const double plo = kSPh * (e1 - 1), phi = kSPh * e1, lo = (e3 - 1) + plo, hi = e3 + phi;
+            const double tlo = kSTh * (e2 - 1), thi = kSTh * e2;
+            const bool normal = plo > -1000.0 && phi < 1000.0 && lo > -1000.0 && hi < 1000.0 && tlo > -1000.0 &&
+                                thi < 1000.0;
+            if (normal && lo > thi + 2.0) return true;
+            if (normal && hi < tlo - 2.0) return false;
+        }
+        pows();
+        return alpha * pD > pT;
+    }
+};
 
 // filter acceptance of a trial (theta, phi): not dominated by the filter (entries in the LDS head; lane
 // f tests entry f, one ballot) and either f-type Armijo (theta0 <= theta_min and the switching
@@ -1095,13 +1445,13 @@ __device__ __forceinline__ Trial phase_trial(const Ctx<BM>& c, double alpha, int
 // Wave-uniform result.
 template <int BM>
 __device__ __forceinline__ bool filter_ok(const Ctx<BM>& c, int nf, const Trial& t, double th0, double phi0, double D,
-                                          double alpha, double th_max, double th_min, double pD, double pT,
+                                          double alpha, double th_max, double th_min, SwitchPow& sp,
                                           bool& ftype) {
     if (!isfinite(t.phi) || t.th > th_max) return false;
     const int f = c.lane & (kTrackFilter - 1);
     if (__ballot(c.lane < nf && t.th >= c.sm[hFTH + f] && t.phi >= c.sm[hFPH + f]) != 0ull) return false;
-    // switching condition alpha (-D)^s_phi > theta0^s_theta (pD, pT precomputed once per iteration)
-    if (th0 <= th_min && D < 0.0 && alpha * pD > pT) {
+    // switching condition alpha (-D)^s_phi > theta0^s_theta
+    if (th0 <= th_min && D < 0.0 && sp.cond(alpha)) {
         ftype = true;
         return armijo(t.phi, phi0, alpha, D);
     }
@@ -1112,6 +1462,52 @@ __device__ __forceinline__ bool filter_ok(const Ctx<BM>& c, int nf, const Trial&
 // ============ accept the step (stage-parallel) ============
 template <int BM>
 __device__ __forceinline__ void phase_update(const Ctx<BM>& c, int dzr, double alpha, double az) {
+    if constexpr (Ctx<BM>::kLF) {
+    const int N = c.N, p = c.part();
+    for (int k = c.k0(); k <= N; k += c.kst()) {
+        // every LDS read of the stage before its stores (a read queued behind a store waits for it)
+        double xnv[8], zlv[8], zuv[8], ynv[6];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;
+            if (vb >= 6 && k == N) break;
+            const double d = c.r(dzr + v, k), xo = c.r(rX + v, k), xn = xo + alpha * d;
+            if (c.hl(vb)) {
+                const double zl = c.r(rZL + v, k), rs = frcp(xo - c.lb(v));
+                const double znew = zl + az * ((c.mu - zl * d) * rs - zl), rn = c.mu * frcp(xn - c.lb(v));
+                zlv[t] = fmax(fmin(znew, 1e10 * rn), 1e-10 * rn);  // kappa_sigma = 1e10
+            }
+            if (c.hu(vb)) {
+                const double zu = c.r(rZU + v, k), rs = frcp(c.ub(v) - xo);
+                const double znew = zu + az * ((c.mu + zu * d) * rs - zu), rn = c.mu * frcp(c.ub(v) - xn);
+                zuv[t] = fmax(fmin(znew, 1e10 * rn), 1e-10 * rn);
+            }
+            xnv[t] = xn;
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            if (c.pair && q >= 3) break;
+            const int i = c.pair ? 2 * q + p : q;
+            const double y = c.r(rY + i, k);
+            ynv[q] = y + alpha * (c.r(rYP + i, k) - y);
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            if (c.pair && t >= 4) break;
+            const int vb = c.pair ? 2 * t : t, v = vb + p;
+            if (vb >= 6 && k == N) break;
+            if (c.hl(vb)) c.r(rZL + v, k) = zlv[t];
+            if (c.hu(vb)) c.r(rZU + v, k) = zuv[t];
+            c.r(rX + v, k) = xnv[t];
+        }
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            if (c.pair && q >= 3) break;
+            c.r(rY + (c.pair ? 2 * q + p : q), k) = ynv[q];
+        }
+    }
+    } else {
     const int N = c.N, p = c.part();
     for (int k = c.k0(); k <= N; k += c.kst()) {
 #pragma unroll
@@ -1138,6 +1534,7 @@ __device__ __forceinline__ void phase_update(const Ctx<BM>& c, int dzr, double a
             const int i = c.pair ? 2 * q + p : q;
             c.r(rY + i, k) += alpha * (c.r(rYP + i, k) - c.r(rY + i, k));
         }
+    }
     }
     __syncthreads();
 }
@@ -1349,6 +1746,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
 #ifdef TT_STAMPS
     Stamps stamps;
     stamps.begin();
+    c.st = &stamps;
 #endif
     const bool fused = BM >= 0 && c.regref && !a.zg;
     if (fused) phase_load_init_reg(c, a, b);
@@ -1433,18 +1831,12 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             // correction; theta / phi_mu of the current point come from the linearisation pass
             const double th0 = e.th, phi0 = e.cost - c.mu * e.logs, D = si.Dg;
             if (iter == 0) { th_max = 1e4 * fmax(1.0, th0); th_min = 1e-4 * fmax(1.0, th0); }
-            // (-D)^s_phi and theta0^s_theta only matter when theta0 <= theta_min (switching condition, amin)
-            double pD = 0.0, pT = 0.0;
-            if (th0 <= th_min && D < 0.0) {
-                pD = pow(-D, kSPh);
-                pT = pow(th0, kSTh);
-            }
-            double amin = kGTh;
-            if (D < 0.0) {
-                amin = fmin(kGTh, kGPh * th0 / (-D));
-                if (th0 <= th_min) amin = fmin(amin, pT / pD);
-            }
-            amin *= 0.05;
+            // (-D)^s_phi and theta0^s_theta only matter when theta0 <= theta_min (switching condition, alpha_min):
+            // evaluated lazily (SwitchPow)
+            SwitchPow sp;
+            sp.mD = -D;
+            sp.th0 = th0;
+            SUBSTAMP(c, 7);
             double alpha = si.ap, az = si.az;
             int accepted = si.rel < 1e-15 ? 1 : 0;
             c.t_dz = -1;  // no trial point of this iteration yet (a tiny step is taken without one)
@@ -1454,7 +1846,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
                 const Trial t = phase_trial(c, alpha, rDX, ls == 0);
                 STAMP(PH_MERIT);
                 COUNT(PH_NTRIAL);
-                if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, pD, pT, ftype)) { accepted = 1; break; }
+                if (filter_ok(c, nf, t, th0, phi0, D, alpha, th_max, th_min, sp, ftype)) { accepted = 1; break; }
                 if (ls == 0 && isfinite(t.phi) && t.th >= th0) {
                     phase_soc_rhs(c, alpha);
                     phase_soc_backward(c, dw);
@@ -1462,7 +1854,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
                     const double as = phase_soc_alpha(c);
                     const Trial ts = phase_trial(c, as, rDXS, false);
                     STAMP(PH_SOC);
-                    if (filter_ok(c, nf, ts, th0, phi0, D, alpha, th_max, th_min, pD, pT, ftype)) {
+                    if (filter_ok(c, nf, ts, th0, phi0, D, alpha, th_max, th_min, sp, ftype)) {
                         accepted = 2;
                         soc = true;
                         alpha = as;
@@ -1470,6 +1862,17 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
                         break;
                     }
                 }
+                // alpha_min (IPOPT: alpha_min_frac 0.05 of the smallest of gamma_theta, gamma_phi theta0 / (-D) and
+                // delta theta0^s_theta / (-D)^s_phi), needed only now that the line search backtracks
+                double amin = kGTh;
+                if (D < 0.0) {
+                    amin = fmin(kGTh, kGPh * th0 / (-D));
+                    if (th0 <= th_min) {
+                        sp.pows();
+                        amin = fmin(amin, sp.pT / sp.pD);
+                    }
+                }
+                amin *= 0.05;
                 if (alpha * 0.5 < amin) break;
                 alpha *= 0.5;
             }
@@ -1538,6 +1941,7 @@ hipError_t launch(const TrackArgs& a, hipStream_t stream) {
 constexpr int kMaskMPC = 0xFCFC;
 constexpr int kMaskOBCA = 0xF8F8;
 constexpr int kDiagBit = 1 << 16;  // Q, R diagonal: the cost and its gradient skip the off-diagonal terms
+constexpr int kOccBit = 1 << 17;   // the two-waves-per-SIMD build (Ctx::kLF)
 
 // Q and R diagonal after symmetrisation (the kernel's weights are 0.5 (Q + Q'), 0.5 (R + R'))
 bool diagonal_weights(const TrackArgs& a) {
@@ -1559,8 +1963,10 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // Above B = 2048 (two rounds of one wave per SIMD) the two-waves-per-SIMD build wins: 12.6 vs 10.3 M solves/s at
     // B = 4096, 12.0 vs 9.8 at 3072, equal at 2048, 3 % slower at 1024 (profiles/r04/occ_by_batch/); round 3 switched
     // at 4096, so the 4096-instance chunks of the sharded C5 path ran one wave per SIMD.
-    if (m == kMaskMPC && d && a.N == 20 && a.B > 2048) return launch<kMaskMPC | kDiagBit, 2, 20>(a, stream);
+    if (m == kMaskMPC && d && a.N == 20 && a.B > 2048) return launch<kMaskMPC | kDiagBit | kOccBit, 2, 20>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
+    // (the generic two-wave build keeps the load-first order: its one-stage-per-lane passes would otherwise contract
+    // differently from the one-wave build's and results would depend on B, test_occupancy_build_boundary_n31_n32)
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);

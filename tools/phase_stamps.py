@@ -17,7 +17,7 @@ from ttmpc.scenarios import synthetic_batch  # noqa: E402
 from oracle import ttmpc_oracle as to  # noqa: E402
 
 PH = ["load", "linearize", "mu+barrier", "riccati", "forward", "step", "merit", "soc", "update", "#riccati",
-      "#trials", "total"]
+      "#trials", "sub0", "sub1", "sub2", "sub3", "sub4", "sub5", "sub6", "sub7", "total"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 psi = 0.9 if N >= 40 else 0.3
