@@ -36,6 +36,8 @@ struct Handle {
     char *d_sin = nullptr, *d_sout = nullptr, *h_sin = nullptr, *h_sout = nullptr;
     std::string err;
     unsigned long long* obca_stamps = nullptr;  // diagnostics: per-phase clocks (ttx_obca_set_stamps)
+    unsigned long long* d_board = nullptr;      // OBCA helper-workgroup board, (ocap + 1) lines
+    int nhelp = -1;                             // OBCA helper workgroups per launch (-1: one per CU; ttx_obca_set_helpers)
 };
 
 thread_local std::string g_err;
@@ -115,6 +117,8 @@ void free_ows(Handle* h) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
+    if (h->d_board) (void)hipFree(h->d_board);
+    h->d_board = nullptr;
     h->ocap = 0;
 }
 
@@ -127,6 +131,7 @@ int ensure_ows(Handle* h, int B) {
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_oxg, b * 6 * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_ozg, b * n * 8);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_ozo, b * n * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_board, (b + 1) * ttmpc::kObcaBoardStride * 8);
     (void)N; (void)M;
     if (e != hipSuccess) {
         free_ows(h);
@@ -452,6 +457,16 @@ int tt_obca_solve_batch_iterate_device(void* handle, int B, const double* d_x0, 
     a.ws = h->d_ows;
     a.stamps = h->obca_stamps;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (h->nhelp < 0) {  // one helper workgroup per CU: they run while CUs are idle (the batch's tail)
+        int cus = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+        if (e != hipSuccess) return hip_fail(h, e, "hipDeviceGetAttribute");
+        h->nhelp = cus;
+    }
+    a.board = h->d_board;
+    a.nhelp = h->nhelp;
+    e = hipMemsetAsync(h->d_board, 0, ((size_t)B + 1) * ttmpc::kObcaBoardStride * 8, s);
+    if (e != hipSuccess) return hip_fail(h, e, "hipMemsetAsync (OBCA board)");
     e = ttmpc::launch_obca(a, s);
     if (e != hipSuccess) return hip_fail(h, e, "OBCA kernel launch");
     return 0;
@@ -534,6 +549,15 @@ int ttx_obca_set_stamps(void* handle, unsigned long long* d_stamps) {
     Handle* h = static_cast<Handle*>(handle);
     if (h) h->obca_stamps = d_stamps;
     return ttmpc::kObcaPhases;
+}
+
+/* diagnostics only: helper workgroups of the handle's OBCA launches (0: none, every instance runs its own block
+ * passes; -1: one per CU, the default).  The results are bitwise the same either way (tests/test_gpu_obca.py). */
+int ttx_obca_set_helpers(void* handle, int n) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h) return -EINVAL;
+    h->nhelp = n < 0 ? -1 : n;
+    return 0;
 }
 
 int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess, double* x_out,

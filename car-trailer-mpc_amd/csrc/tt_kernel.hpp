@@ -86,7 +86,12 @@ struct ObcaArgs {
     double* itout;                  // [B][obca_iterate_len] final primal-dual iterate (diagnostic export) or nullptr
     double* ws;                     // per-instance workspace, obca_ws_doubles(N, M) each
     unsigned long long* stamps;     // [B][kObcaPhases] cycle sums (diagnostics), or nullptr
+    // helper workgroups (tt_obca.hip, "helper workgroups"): nhelp extra workgroups after the B instances run the block
+    // passes of the instances still solving; board: (B + 1) x kObcaBoardStride words, zeroed before every launch
+    unsigned long long* board;
+    int nhelp;
 };
+constexpr int kObcaBoardStride = 16;  // 128-B line per instance (+ one header line)
 // phase clocks, then event counters (diagnostics, tools/obca_stamps.py / obca_tail.py): factorisations (inertia
 // attempts incl. the SOC and pretend-singular refactorisations), restoration-phase iterations, soft-restoration steps,
 // refinement corrections, second-order corrections, pretend-singular re-solves, line-search trial points
@@ -96,7 +101,7 @@ enum { OPH_LIN = 0, OPH_COMPL, OPH_FACTOR, OPH_RIC, OPH_FWD, OPH_REC, OPH_TRIAL,
 
 // workspace layout (doubles): stage fields [f][k] then block fields [f][j][k], k in 0..N
 constexpr int kObcaStageFields = 353;
-constexpr int kObcaBlockFields = 212;
+constexpr int kObcaBlockFields = 229;
 __host__ __device__ inline size_t obca_ws_doubles(int N, int M) {
     return (size_t)(kObcaStageFields + kObcaBlockFields * 2 * M) * (size_t)(N + 1);
 }

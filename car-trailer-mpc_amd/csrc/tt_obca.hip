@@ -81,10 +81,12 @@ enum : int {
     B_OS = 184, B_OP = 188, B_ON = 192,
     // the right-hand side of a correction solve (phase_nres prep -> NR_CORR): fw 8 | zf_lam 4 | t 4.  The elimination
     // itself is recomputed by every pass that needs it (block_refactor), not stored.
-    B_FR = 196, B_END = 212
+    B_FR = 196,
+    // phase_nres: a block's contribution record (nres_block -> the stage part)
+    B_CB = 212, B_END = 229
 };
 enum : int { FR_FW = 0, FR_ZFL = 8, FR_T = 12, FR_END = 16 };
-static_assert(B_FR + FR_END == B_END, "factor record");
+static_assert(B_FR + FR_END == B_CB, "factor record");
 static_assert(B_END == kObcaBlockFields, "block field count");
 
 // packed symmetric 6x6 (upper) index
@@ -147,6 +149,11 @@ struct Shared {
     int flag;    // the Riccati sweep's factorisation code (F_OK / F_MANY / F_ZERO)
     unsigned long long stamp[kObcaPhases];
     unsigned long long t0;
+    // helper workgroups (run_pass / helper_main): passes published, the claimed chunk / instance, exit and failure flags,
+    // and a helper's copy of the pass parameters
+    unsigned hep;
+    int hcur, hb, hexit, hfail, hp_pk;
+    double hp_mu, hp_dw, hp_tau;
 };
 typedef __attribute__((address_space(3))) Shared LShared;  // the kernel's Shared block, LDS-addressed
 
@@ -911,6 +918,116 @@ __device__ __forceinline__ void block_refactor(const Ctx& c, const LShared& sh, 
     block_setup<RHS>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
 }
 
+// ---------------- helper workgroups: the block passes of the instances still solving ----------------
+// The launch has nhelp workgroups after the B instances' (blockIdx >= B).  They start once instance workgroups have
+// finished and CUs are free -- in the C4 tail a handful of instances run thousands of iterations on an otherwise idle
+// GPU -- and run chunks (T consecutive blocks of the flat block index) of those instances' factor and residual passes.
+// A chunk's arithmetic does not depend on which workgroup runs it, so the results are bitwise those of the instance
+// running every chunk itself (the local path, taken while no helper has started: the whole busy phase of a large batch).
+// Board (HBM, zeroed before every launch), one 128-B line per instance:
+//   [0] claim = epoch << 40 | chunks << 32 | next chunk (odd epoch: open), [1] done = epoch << 32 | chunks done by
+//   helpers, [2..6] mu dw tau zeta dc (bits), [7] pass | buf << 4 | prep << 8 | mode << 12 | R << 16 | lsq << 20;
+// header line (index B): [0] instances finished, [1] helpers started, [2] instances started.
+// Hand-off (agent scope; MI355X_MICROARCH.md, inter-workgroup visibility): the instance's waves drain their stores, one
+// lane releases (L2 write-back) and stores the claim word; a helper's claim is followed by one acquire before any load
+// of the instance's data; a helper's chunk ends with drained stores, a release and the done add; the instance acquires
+// once the done count is complete.  Every spin is bounded.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+enum { PASS_FACTOR = 1, PASS_NRES = 2 };
+struct ChunkPass {
+    double mu, dw, tau;
+    int pass, buf, prep, mode;
+};
+__device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1);
+
+__device__ __forceinline__ gu64* board_line(LArgs& a, int b) { return (gu64*)(a.board + (size_t)b * kObcaBoardStride); }
+__device__ __forceinline__ unsigned long long ld_rlx(gu64* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(gu64* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long add_rlx(gu64* p, unsigned long long v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
+__device__ __forceinline__ double bitsd(unsigned long long v) { return __longlong_as_double((long long)v); }
+constexpr unsigned long long kSpinTicks = 500000000ull;  // 5 s of the 100 MHz s_memrealtime clock
+
+// one block pass of this instance (every thread of its workgroup), ending with a workgroup barrier
+__device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
+    LArgs& a = *c.a;
+    const int nch = (c.nbk * c.NP + T - 1) / T;
+    if (threadIdx.x == 0) sh.hcur = (a.board && a.nhelp > 0 && ld_rlx(board_line(a, a.B) + 1) > 0) ? 1 : 0;
+    __syncthreads();
+    const bool shared = sh.hcur != 0;
+    __syncthreads();
+    if (!shared) {
+        do_chunks(c, sh, p, 0, nch);
+        __syncthreads();
+        return;
+    }
+    gu64* ln = board_line(a, c.b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's workspace stores complete
+    __syncthreads();
+    unsigned long long ep = 0;
+    if (threadIdx.x == 0) {
+        ep = 2ull * sh.hep + 1ull;
+        sh.hep += 1;
+        ln[2] = dbits(p.mu); ln[3] = dbits(p.dw); ln[4] = dbits(p.tau); ln[5] = dbits(sh.zeta); ln[6] = dbits(sh.dc);
+        ln[7] = (unsigned long long)(p.pass | p.buf << 4 | p.prep << 8 | p.mode << 12 | sh.R << 16 | sh.lsq << 20);
+        st_rlx(ln + 1, ep << 32);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_rlx(ln, ep << 40 | (unsigned long long)nch << 32);
+    }
+    int own = 0;
+    for (;;) {
+        if (threadIdx.x == 0) sh.hcur = (int)(unsigned)(add_rlx(ln, 1) & 0xffffffffull);
+        __syncthreads();
+        const int ci = sh.hcur;
+        __syncthreads();
+        if (ci >= nch) break;
+        do_chunks(c, sh, p, ci, ci + 1);
+        ++own;
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long want = ep << 32 | (unsigned long long)(nch - own), t0 = __builtin_amdgcn_s_memrealtime();
+        while (ld_rlx(ln + 1) != want) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { sh.hfail = 1; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        st_rlx(ln, (ep + 1ull) << 40);  // closed
+        if (own < nch) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+}
+
+// ---- the factor pass's block part: linearise + factor + right-hand side of block (j, k) of the flat block index ----
+// Only the block's contributions to its stage leave it (the recovery passes recompute the elimination, block_refactor):
+// the Schur complement C4, the gradient q4 and the factorisation outcome, in its record B_CB; phase_factor's stage part
+// adds a stage's records in block order (the arithmetic of the block loop inside the stage loop).
+enum : int { CF_C4 = 0, CF_Q4 = 10, CF_FAIL = 14, CF_END = 15 };
+static_assert(CF_END <= B_END - B_CB, "factor contribution record");
+__device__ __forceinline__ void factor_block(const Ctx& c, const LShared& sh, const WsView& vw, int j, int k, double mu,
+                                             double dw) {
+    double x[6];
+    load_x(c, k, x);
+    const Trig tr = stage_trig(x);
+    Blk bk;
+    bk.m = c.slab + threadIdx.x;
+    double fw[8], zf[8], t4[4];
+    double cf[CF_END] = {};
+    BlkIn cur;
+    load_blk_in(c, sh.R != 0, j, k, cur);
+    cf[CF_FAIL] = (double)block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, cf + CF_C4, cf + CF_Q4);
+#pragma unroll
+    for (int i = 0; i < CF_END; ++i) vw.B(B_CB + i, j, k) = cf[i];
+}
+
 // ======== phase: stage Hessians + gradients (all threads) -> factorisation outcome (uniform) ========
 // Also the effective dynamics-row residuals S_CE (= S_CR + delta_c y outside the restoration phase) and the soft-row
 // scales S_SD = sqrt(E) (E = 1/D_p + 1/D_n in the restoration phase, + delta_c).
@@ -922,23 +1039,22 @@ __device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, d
     const double dc = sh.dc;
     const bool soft = rs || dc > 0.0;
     double fail[3] = {0.0, 0.0, 0.0};  // F_ZERO, F_MANY, F_FEW seen
+    // the block part over the flat block index (factor_block), by this workgroup and any helpers
+    run_pass(c, sh, ChunkPass{mu, dw, 0.0, PASS_FACTOR, 0, 0, 0});
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6];
         load_x(c, k, x);
-        // the OBCA blocks first: only x, C4, q4 stay live across the block loop (register pressure)
+        // the blocks' stage contributions, in block order
         double C4[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, q4[4] = {0, 0, 0, 0};
-        const Trig tr = stage_trig(x);
-        // only the stage contributions leave this pass: the recovery passes recompute the elimination
-        // (block_refactor), so a failed inertia attempt costs the block reads and no stores
-        // (each block's inputs are loaded at its start: loading block j+1's during block j measured 3.8 % slower
-        // once the pass spills, profiles/r04/factor_nopf/)
         for (int j = 0; j < c.nbk; ++j) {
-            Blk bk;
-            bk.m = c.slab + threadIdx.x;
-            double fw[8], zf[8], t4[4];
-            BlkIn cur;
-            load_blk_in(c, rs, j, k, cur);
-            const int f = block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, C4, q4);
+            double cf[CF_END];
+#pragma unroll
+            for (int i = 0; i < CF_END; ++i) cf[i] = vw.B(B_CB + i, j, k);
+#pragma unroll
+            for (int i = 0; i < 10; ++i) C4[i] += cf[CF_C4 + i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q4[i] += cf[CF_Q4 + i];
+            const int f = (int)cf[CF_FAIL];
             if (f == F_ZERO) fail[0] = 1.0;
             if (f == F_MANY) fail[1] = 1.0;
             if (f == F_FEW) fail[2] = 1.0;
@@ -947,6 +1063,7 @@ __device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, d
         const double sc = (k == N && plan) ? a.tfac : 1.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i)
+#pragma unroll
             for (int j2 = i; j2 < 6; ++j2)
                 Qs[sy6(i, j2)] = lsq ? (i == j2 ? 1.0 : 0.0) : rs ? 0.0 : sc * (a.Q[i * 6 + j2] + a.Q[j2 * 6 + i]);
         if (k < N && !lsq) {
@@ -977,6 +1094,7 @@ __device__ __noinline__ int phase_factor(const Ctx& c, LShared& sh, double mu, d
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
+#pragma unroll
             for (int q = 0; q <= p; ++q) Qs[sy6(q, p)] += C4[lo4(p, q)];
             qv[p] += q4[p];
         }
@@ -2933,6 +3051,300 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src src, bool soft)
 // the blocks instead of two); NR_CORR a correction's dx is in buffer 2, the stage parts are already added into buf
 // (phase_stage_add), and the blocks' correction is recovered here (with the constants prep left) and added.
 enum { NR_STEP = 0, NR_MAIN = 1, NR_CORR = 2 };
+// ---- the residual pass's block part: block (j, k) of the flat block index f = j (N + 1) + k ----
+// Everything one OBCA block contributes to phase_nres, from the workspace alone (the stage's x, its step dx and the
+// block's own fields): the block's step / correction (NR_MAIN, NR_CORR) and the next correction's right-hand side (prep)
+// go to the block's fields; its contributions to the stage rows and to the pass's reductions go to its record B_CB --
+// the x rows' adds (W_xx dx, W_x lam dw_lam + Jx' y+), the gradient adds of the correction's right-hand side, its part of
+// grad phi' d as one term, and its maxima / minima.  The stage part (phase_nres) adds a stage's records in block order:
+// the arithmetic of the pass with the block loop inside the stage loop.  No block reads another block's output, so any
+// thread of any workgroup can run any block.
+enum : int { CB_DM = 0, CB_RMAX = 1, CB_BMAX = 2, CB_SN = 3, CB_REL = 4, CB_AP = 5, CB_AZ = 6, CB_RX = 7, CB_Q4 = 13,
+             CB_END = 17 };
+static_assert(B_CB + CB_END == B_END, "contribution record");
+__device__ __forceinline__ void nres_block(const Ctx& c, const LShared& sh, const WsView& vw, int j, int k, double mu,
+                                           double dw, double tau, int buf, bool prep, int mode) {
+    LArgs& a = *c.a;
+    const bool rs = sh.R != 0;
+    const double zeta = sh.zeta, dc = sh.dc;
+    double x[6], dx[6];
+    load_x(c, k, x);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dx[i] = vw.S(S_DX + 6 * buf + i, k);
+    const Trig tr = stage_trig(x);
+    double rmax = 0.0, bmax = 0.0, snorm = 0.0, ap = 1.0, az = 1.0, rel = 0.0, Dmb = 0.0;
+    double cb[CB_END] = {};
+    auto R = [&](double v) { rmax = fmax(rmax, fabs(v)); return v; };
+    auto Bc = [&](double v) { bmax = fmax(bmax, fabs(v)); return v; };
+    auto dual = [&](double z, double dz) { if (dz < 0.0) az = fmin(az, -tau * z * inv(dz)); };
+    BlkIn in;
+    load_blk_in(c, rs, j, k, in);
+    const double *w = in.w, *zw = in.zw, *sv = in.s, *vl = in.vl, *vu = in.vu, *dres = in.dr;
+    double dwv[8], ds[4], ydp[4];
+    Blk bk;
+    bk.m = c.slab + threadIdx.x;
+    // the elimination (block_refactor, which linearises too) where the pass recovers a step or prepares a
+    // correction's right-hand side; the linearisation alone otherwise
+    if (mode == NR_MAIN || mode == NR_CORR || prep) {
+        double fw[8], zf[8], t4[4];
+        if (mode == NR_MAIN) {
+            block_refactor<true>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
+        } else {
+            block_refactor<false>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
+            if (mode == NR_CORR) {  // the correction's right-hand side, as the previous prep pass left it
+#pragma unroll
+                for (int e = 0; e < 8; ++e) fw[e] = vw.B(B_FR + FR_FW + e, j, k);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { zf[4 + e] = vw.B(B_FR + FR_ZFL + e, j, k); t4[e] = vw.B(B_FR + FR_T + e, j, k); }
+            }
+        }
+        if (mode != NR_STEP) {
+            // ---- the block's part of the step (NR_MAIN) or of the correction (NR_CORR) ----
+            double ypr[4], dwr[8], dxr[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)vw.S(S_DX + 12 + i, k);
+            blk_recover(bk, fw, zf, t4, dxr, ypr, dwr);
+            const bool add = mode == NR_CORR;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                dwv[e] = add ? (double)vw.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
+                vw.B(B_DW + 8 * buf + e, j, k) = dwv[e];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double gs = add ? (double)vw.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
+                const double dsr = (ypr[r] - gs) / bk.D[r];
+                ydp[r] = add ? (double)vw.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
+                ds[r] = add ? (double)vw.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
+                vw.B(B_YP + 4 * buf + r, j, k) = ydp[r];
+                vw.B(B_DS + 4 * buf + r, j, k) = ds[r];
+                if (rs) {
+                    const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
+                    const double gp = add ? (double)vw.B(B_OP + r, j, k) : RHO - mu / p;
+                    const double gn = add ? (double)vw.B(B_ON + r, j, k) : RHO - mu / n;
+                    const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
+                    vw.B(B_DP + 4 * buf + r, j, k) = add ? (double)vw.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
+                    vw.B(B_DN + 4 * buf + r, j, k) = add ? (double)vw.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
+                }
+            }
+        }
+    } else {
+        blk_lin(a, x, tr, j, w, in.y, bk);
+    }
+    if (mode == NR_STEP) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dwv[e] = vw.B(B_DW + 8 * buf + e, j, k);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { ds[r] = vw.B(B_DS + 4 * buf + r, j, k); ydp[r] = vw.B(B_YP + 4 * buf + r, j, k); }
+    }
+    // x rows: W_xx dx + W_x lam dw_lam + Jx' y+
+    cb[CB_RX] = bk.hxx22 * dx[2] + bk.hxx23 * dx[3];
+    cb[CB_RX + 1] = bk.hxx23 * dx[2] + bk.hxx33 * dx[3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double t = 0.0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += bk.H(q, e) * dwv[4 + e];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) t += jx(bk, r, q) * ydp[r];
+        cb[CB_RX + 2 + q] = t;
+    }
+    // w rows
+    double rw[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const double sl = w[e] + RELAX, isl = inv(sl), d = dwv[e];
+        double hw = 0.0, gw = -mu * isl;
+        if (rs) {
+            hw = zeta * in.drw[e];
+            gw += hw * (w[e] - in.wr[e]);
+        }
+        double t = Bc(gw) + (zw[e] * isl + dw + hw) * d;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * ydp[r];
+        if (e >= 4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t += bk.H(q, e - 4) * dx[q];
+#pragma unroll
+            for (int b2 = 0; b2 < 4; ++b2) t += hll(bk, max(e - 4, b2), min(e - 4, b2)) * dwv[4 + b2];
+        }
+        rw[e] = R(t);
+        Dmb += gw * d;
+        rel = fmax(rel, fabs(d) * inv(1.0 + fabs(w[e])));
+        snorm = fmax(snorm, fabs(d));
+        ftb_lo(w[e], -RELAX, d, tau, ap);
+        dual(zw[e], mu * isl - zw[e] - zw[e] * isl * d);
+    }
+    // slack, row and elastic-pair rows
+    double rsl[4], rdv[4], rpv[4] = {0, 0, 0, 0}, rnv[4] = {0, 0, 0, 0}, Dpv[4] = {1, 1, 1, 1}, Dnv[4] = {1, 1, 1, 1};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double s = sv[r], d = ds[r];
+        const double iu = inv(c.rU(r) - s), il = c.hrl(r) ? inv(s - c.rL(r)) : 0.0;
+        const double gs = c.hrl(r) ? mu * iu - mu * il : mu * iu;
+        const double sgr = c.hrl(r) ? vu[r] * iu + vl[r] * il : vu[r] * iu;
+        rsl[r] = R(Bc(gs) + (sgr + dw) * d - ydp[r]);
+        double t = Bc(dc > 0.0 ? fma(dc, in.y[r], dres[r]) : dres[r]) - d;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += jx(bk, r, q) * dx[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += jwm(bk, r, e) * dwv[e] + jwl(bk, r, e) * dwv[4 + e];
+        if (rs) {
+            const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
+            const double dp = vw.B(B_DP + 4 * buf + r, j, k), dn = vw.B(B_DN + 4 * buf + r, j, k);
+            t += -dp + dn;
+            const double ip = inv(p), in_ = inv(n);
+            Dpv[r] = zp * ip + dw;
+            Dnv[r] = zn * in_ + dw;
+            const double gp = RHO - mu * ip, gn = RHO - mu * in_;
+            rpv[r] = R(Bc(gp) + Dpv[r] * dp - ydp[r]);
+            rnv[r] = R(Bc(gn) + Dnv[r] * dn + ydp[r]);
+            ftb_lo(p, 0.0, dp, tau, ap);
+            ftb_lo(n, 0.0, dn, tau, ap);
+            dual(zp, mu * ip - zp - zp * ip * dp);
+            dual(zn, mu * in_ - zn - zn * in_ * dn);
+            Dmb += gp * dp + gn * dn;
+            rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
+        }
+        if (dc > 0.0) t -= dc * ydp[r];
+        rdv[r] = R(t);
+        Dmb += gs * d;
+        rel = fmax(rel, fabs(d) * inv(1.0 + fabs(s)));
+        ftb_hi(s, c.rU(r), d, tau, ap);
+        dual(vu[r], mu * iu - vu[r] + vu[r] * iu * d);
+        if (c.hrl(r)) {
+            ftb_lo(s, c.rL(r), d, tau, ap);
+            dual(vl[r], mu * il - vl[r] - vl[r] * il * d);
+        }
+    }
+    if (prep) {  // bk holds the elimination (block_refactor above)
+        double rdc[4], zf[8], t4[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / bk.D[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
+        blk_rhs(bk, rw, rdc, zf, t4, cb + CB_Q4);
+        auto stf = [&](int f, double v) { vw.B(B_FR + f, j, k) = v; };
+#pragma unroll
+        for (int e = 0; e < 8; ++e) stf(FR_FW + e, rw[e]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { stf(FR_ZFL + e, zf[4 + e]); stf(FR_T + e, t4[e]); }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            vw.B(B_OS + r, j, k) = rsl[r];
+            if (rs) { vw.B(B_OP + r, j, k) = rpv[r]; vw.B(B_ON + r, j, k) = rnv[r]; }
+        }
+    }
+    cb[CB_DM] = Dmb; cb[CB_RMAX] = rmax; cb[CB_BMAX] = bmax; cb[CB_SN] = snorm; cb[CB_REL] = rel; cb[CB_AP] = ap;
+    cb[CB_AZ] = az;
+#pragma unroll
+    for (int i = 0; i < CB_END; ++i) vw.B(B_CB + i, j, k) = cb[i];
+}
+
+// chunks [c0, c1) of a block pass: thread t runs block f = ci T + t of the flat block index (one function per pass, so
+// that neither block part's registers constrain the other's)
+__device__ __noinline__ void nres_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+    const WsView vw = ws_view(c);
+    const int nblk = c.nbk * c.NP, np = c.NP;
+    for (int ci = c0; ci < c1; ++ci) {
+        const int f = ci * T + (int)threadIdx.x;
+        if (f >= nblk) break;
+        const int j = f / np;
+        nres_block(c, sh, vw, j, f - j * np, p.mu, p.dw, p.tau, p.buf, p.prep != 0, p.mode);
+    }
+}
+__device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+    const WsView vw = ws_view(c);
+    const int nblk = c.nbk * c.NP, np = c.NP;
+    for (int ci = c0; ci < c1; ++ci) {
+        const int f = ci * T + (int)threadIdx.x;
+        if (f >= nblk) break;
+        const int j = f / np;
+        factor_block(c, sh, vw, j, f - j * np, p.mu, p.dw);
+    }
+}
+__device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+    if (p.pass == PASS_NRES) nres_chunks(c, sh, p, c0, c1);
+    else factor_chunks(c, sh, p, c0, c1);
+}
+
+// a helper workgroup: serve open chunks of any instance until every instance has finished
+__device__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
+    const int B = a.B, lane = (int)threadIdx.x;
+    gu64* hdr = board_line(a, B);
+    if (lane == 0) {
+        // a helper that finds an instance not yet started leaves at once: a workgroup that waits for the batch to finish
+        // must never hold a CU an instance still needs (dispatch order is not promised)
+        sh.hexit = ld_rlx(hdr + 2) < (unsigned long long)B ? 1 : 0;
+        if (!sh.hexit) add_rlx(hdr + 1, 1);
+    }
+    __syncthreads();
+    if (sh.hexit) return;
+    int pos = (((int)blockIdx.x - B) * 7) % B;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (lane < 64) {  // wave 0 looks at 64 instances per round
+            int ex = 0;
+            if (lane == 0)
+                ex = ld_rlx(hdr) >= (unsigned long long)B || __builtin_amdgcn_s_memrealtime() - t0 > 12ull * kSpinTicks;
+            ex = __builtin_amdgcn_readfirstlane(ex);
+            int gb = -1, gc = -1;
+            if (!ex) {
+                const int b = (pos + lane) % B;
+                const unsigned long long w = lane < B ? ld_rlx(board_line(a, b)) : 0ull;
+                const bool open = ((w >> 40) & 1ull) && (unsigned)w < (unsigned)((w >> 32) & 0xffull);
+                const unsigned long long m = __ballot(open);
+                if (m) {
+                    const int l = __ffsll((long long)m) - 1;
+                    int cb = -1, cc = -1;
+                    if (lane == l) {
+                        const unsigned long long o = add_rlx(board_line(a, b), 1);
+                        if (((o >> 40) & 1ull) && (unsigned)o < (unsigned)((o >> 32) & 0xffull)) { cb = b; cc = (int)(unsigned)o; }
+                    }
+                    gb = __builtin_amdgcn_readlane(cb, l);
+                    gc = __builtin_amdgcn_readlane(cc, l);
+                    pos = (pos + l) % B;  // the next round starts at the instance just served
+                } else {
+                    pos = (pos + 64) % B;
+                }
+            }
+            if (lane == 0) { sh.hexit = ex; sh.hb = gb; sh.hcur = gc; }
+        }
+        __syncthreads();
+        const int b = sh.hb, ci = sh.hcur, ex = sh.hexit;
+        __syncthreads();
+        if (ex) break;
+        if (b < 0) {
+            __builtin_amdgcn_s_sleep(32);
+            continue;
+        }
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            gu64* ln = board_line(a, b);
+            const unsigned long long pk = ld_rlx(ln + 7);
+            sh.hp_mu = bitsd(ld_rlx(ln + 2)); sh.hp_dw = bitsd(ld_rlx(ln + 3)); sh.hp_tau = bitsd(ld_rlx(ln + 4));
+            sh.zeta = bitsd(ld_rlx(ln + 5)); sh.dc = bitsd(ld_rlx(ln + 6));
+            sh.hp_pk = (int)pk;
+            sh.R = (int)(pk >> 16) & 15;
+            sh.lsq = (int)(pk >> 20) & 15;
+            cw.ws = (gdouble*)(a.ws + (size_t)b * obca_ws_doubles(a.N, a.M));
+            cw.b = b;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        ChunkPass p;
+        p.mu = sh.hp_mu; p.dw = sh.hp_dw; p.tau = sh.hp_tau;
+        const int pk = sh.hp_pk;
+        p.pass = pk & 15; p.buf = (pk >> 4) & 15; p.prep = (pk >> 8) & 15; p.mode = (pk >> 12) & 15;
+        do_chunks(cw, sh, p, ci, ci + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            add_rlx(board_line(a, b) + 1, 1);
+        }
+    }
+}
+
 __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, double dw, double tau, int buf, bool prep,
                                         int mode, double (&out)[7]) {
     const WsView vw = ws_view(c);
@@ -2944,6 +3356,9 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
     auto R = [&](double v) { rmax = fmax(rmax, fabs(v)); return v; };
     auto Bc = [&](double v) { bmax = fmax(bmax, fabs(v)); return v; };
     auto dual = [&](double z, double dz) { if (dz < 0.0) az = fmin(az, -tau * z * inv(dz)); };
+    // the block part over the flat block index (all threads busy: 2M (N + 1) blocks in ceil(2M (N + 1) / T) rounds), by
+    // this workgroup and any helpers
+    run_pass(c, sh, ChunkPass{mu, dw, tau, PASS_NRES, buf, prep ? 1 : 0, mode});
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         const bool st = k < N;
         double x[6], dx[6], yp[6], ypn[6] = {0, 0, 0, 0, 0, 0}, dj[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, wd[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -2999,166 +3414,26 @@ __device__ __noinline__ void phase_nres(const Ctx& c, LShared& sh, double mu, do
         rx[3] -= dj[6] * ypn[3];
         rx[4] -= dj[4] * ypn[2] + dj[7] * ypn[3];
         rx[5] -= dj[1] * ypn[0] + dj[3] * ypn[1] + dj[5] * ypn[2] + dj[8] * ypn[3];
-        // ---- OBCA blocks ----
+        // ---- OBCA blocks: their records (nres_block), in block order ----
         double q4[4] = {0, 0, 0, 0};
-        const Trig tr = stage_trig(x);
         for (int j = 0; j < c.nbk; ++j) {
-            BlkIn in;
-            load_blk_in(c, rs, j, k, in);
-            const double *w = in.w, *zw = in.zw, *sv = in.s, *vl = in.vl, *vu = in.vu, *dres = in.dr;
-            double dwv[8], ds[4], ydp[4];
-            Blk bk;
-            bk.m = c.slab + threadIdx.x;
-            // the elimination (block_refactor, which linearises too) where the pass recovers a step or prepares a
-            // correction's right-hand side; the linearisation alone otherwise
-            if (mode == NR_MAIN || mode == NR_CORR || prep) {
-                double fw[8], zf[8], t4[4];
-                if (mode == NR_MAIN) {
-                    block_refactor<true>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
-                } else {
-                    block_refactor<false>(c, sh, in, j, x, tr, mu, dw, bk, fw, zf, t4);
-                    if (mode == NR_CORR) {  // the correction's right-hand side, as the previous prep pass left it
+            double cb[CB_END];
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) fw[e] = vw.B(B_FR + FR_FW + e, j, k);
+            for (int i = 0; i < CB_END; ++i) cb[i] = vw.B(B_CB + i, j, k);
+            rx[2] += cb[CB_RX];
+            rx[3] += cb[CB_RX + 1];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) { zf[4 + e] = vw.B(B_FR + FR_ZFL + e, j, k); t4[e] = vw.B(B_FR + FR_T + e, j, k); }
-                    }
-                }
-                if (mode != NR_STEP) {
-                    // ---- the block's part of the step (NR_MAIN) or of the correction (NR_CORR) ----
-                    double ypr[4], dwr[8], dxr[6];
+            for (int q = 0; q < 4; ++q) rx[q] += cb[CB_RX + 2 + q];
+            if (prep)
 #pragma unroll
-                    for (int i = 0; i < 6; ++i) dxr[i] = mode == NR_MAIN ? dx[i] : (double)vw.S(S_DX + 12 + i, k);
-                    blk_recover(bk, fw, zf, t4, dxr, ypr, dwr);
-                    const bool add = mode == NR_CORR;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        dwv[e] = add ? (double)vw.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
-                        vw.B(B_DW + 8 * buf + e, j, k) = dwv[e];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const double gs = add ? (double)vw.B(B_OS + r, j, k) : grad_row(c, r, sv[r], mu);
-                        const double dsr = (ypr[r] - gs) / bk.D[r];
-                        ydp[r] = add ? (double)vw.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
-                        ds[r] = add ? (double)vw.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
-                        vw.B(B_YP + 4 * buf + r, j, k) = ydp[r];
-                        vw.B(B_DS + 4 * buf + r, j, k) = ds[r];
-                        if (rs) {
-                            const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
-                            const double gp = add ? (double)vw.B(B_OP + r, j, k) : RHO - mu / p;
-                            const double gn = add ? (double)vw.B(B_ON + r, j, k) : RHO - mu / n;
-                            const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
-                            vw.B(B_DP + 4 * buf + r, j, k) = add ? (double)vw.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
-                            vw.B(B_DN + 4 * buf + r, j, k) = add ? (double)vw.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
-                        }
-                    }
-                }
-            } else {
-                blk_lin(a, x, tr, j, w, in.y, bk);
-            }
-            if (mode == NR_STEP) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) dwv[e] = vw.B(B_DW + 8 * buf + e, j, k);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) { ds[r] = vw.B(B_DS + 4 * buf + r, j, k); ydp[r] = vw.B(B_YP + 4 * buf + r, j, k); }
-            }
-            // x rows: W_xx dx + W_x lam dw_lam + Jx' y+
-            rx[2] += bk.hxx22 * dx[2] + bk.hxx23 * dx[3];
-            rx[3] += bk.hxx23 * dx[2] + bk.hxx33 * dx[3];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                double t = 0.0;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) t += bk.H(q, e) * dwv[4 + e];
-#pragma unroll
-                for (int r = 0; r < 3; ++r) t += jx(bk, r, q) * ydp[r];
-                rx[q] += t;
-            }
-            // w rows
-            double rw[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const double sl = w[e] + RELAX, isl = inv(sl), d = dwv[e];
-                double hw = 0.0, gw = -mu * isl;
-                if (rs) {
-                    hw = zeta * in.drw[e];
-                    gw += hw * (w[e] - in.wr[e]);
-                }
-                double t = Bc(gw) + (zw[e] * isl + dw + hw) * d;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) t += (e < 4 ? jwm(bk, r, e) : jwl(bk, r, e - 4)) * ydp[r];
-                if (e >= 4) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) t += bk.H(q, e - 4) * dx[q];
-#pragma unroll
-                    for (int b2 = 0; b2 < 4; ++b2) t += hll(bk, max(e - 4, b2), min(e - 4, b2)) * dwv[4 + b2];
-                }
-                rw[e] = R(t);
-                Dm += gw * d;
-                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(w[e])));
-                snorm = fmax(snorm, fabs(d));
-                ftb_lo(w[e], -RELAX, d, tau, ap);
-                dual(zw[e], mu * isl - zw[e] - zw[e] * isl * d);
-            }
-            // slack, row and elastic-pair rows
-            double rsl[4], rdv[4], rpv[4] = {0, 0, 0, 0}, rnv[4] = {0, 0, 0, 0}, Dpv[4] = {1, 1, 1, 1}, Dnv[4] = {1, 1, 1, 1};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double s = sv[r], d = ds[r];
-                const double iu = inv(c.rU(r) - s), il = c.hrl(r) ? inv(s - c.rL(r)) : 0.0;
-                const double gs = c.hrl(r) ? mu * iu - mu * il : mu * iu;
-                const double sgr = c.hrl(r) ? vu[r] * iu + vl[r] * il : vu[r] * iu;
-                rsl[r] = R(Bc(gs) + (sgr + dw) * d - ydp[r]);
-                double t = Bc(dc > 0.0 ? fma(dc, in.y[r], dres[r]) : dres[r]) - d;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) t += jx(bk, r, q) * dx[q];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) t += jwm(bk, r, e) * dwv[e] + jwl(bk, r, e) * dwv[4 + e];
-                if (rs) {
-                    const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
-                    const double dp = vw.B(B_DP + 4 * buf + r, j, k), dn = vw.B(B_DN + 4 * buf + r, j, k);
-                    t += -dp + dn;
-                    const double ip = inv(p), in_ = inv(n);
-                    Dpv[r] = zp * ip + dw;
-                    Dnv[r] = zn * in_ + dw;
-                    const double gp = RHO - mu * ip, gn = RHO - mu * in_;
-                    rpv[r] = R(Bc(gp) + Dpv[r] * dp - ydp[r]);
-                    rnv[r] = R(Bc(gn) + Dnv[r] * dn + ydp[r]);
-                    ftb_lo(p, 0.0, dp, tau, ap);
-                    ftb_lo(n, 0.0, dn, tau, ap);
-                    dual(zp, mu * ip - zp - zp * ip * dp);
-                    dual(zn, mu * in_ - zn - zn * in_ * dn);
-                    Dm += gp * dp + gn * dn;
-                    rel = fmax(rel, fmax(fabs(dp) * inv(1.0 + fabs(p)), fabs(dn) * inv(1.0 + fabs(n))));
-                }
-                if (dc > 0.0) t -= dc * ydp[r];
-                rdv[r] = R(t);
-                Dm += gs * d;
-                rel = fmax(rel, fabs(d) * inv(1.0 + fabs(s)));
-                ftb_hi(s, c.rU(r), d, tau, ap);
-                dual(vu[r], mu * iu - vu[r] + vu[r] * iu * d);
-                if (c.hrl(r)) {
-                    ftb_lo(s, c.rL(r), d, tau, ap);
-                    dual(vl[r], mu * il - vl[r] - vl[r] * il * d);
-                }
-            }
-            if (prep) {  // bk holds the elimination (block_refactor above)
-                double rdc[4], zf[8], t4[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / bk.D[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
-                blk_rhs(bk, rw, rdc, zf, t4, q4);
-                auto stf = [&](int f, double v) { vw.B(B_FR + f, j, k) = v; };
-#pragma unroll
-                for (int e = 0; e < 8; ++e) stf(FR_FW + e, rw[e]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) { stf(FR_ZFL + e, zf[4 + e]); stf(FR_T + e, t4[e]); }
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    vw.B(B_OS + r, j, k) = rsl[r];
-                    if (rs) { vw.B(B_OP + r, j, k) = rpv[r]; vw.B(B_ON + r, j, k) = rnv[r]; }
-                }
-            }
+                for (int q = 0; q < 4; ++q) q4[q] += cb[CB_Q4 + q];
+            rmax = fmax(rmax, cb[CB_RMAX]);
+            bmax = fmax(bmax, cb[CB_BMAX]);
+            snorm = fmax(snorm, cb[CB_SN]);
+            rel = fmax(rel, cb[CB_REL]);
+            ap = fmin(ap, cb[CB_AP]);
+            az = fmin(az, cb[CB_AZ]);
+            Dm += cb[CB_DM];
         }
         // ---- u rows (after the blocks: their operands are re-read rather than kept live across the block loop) ----
         double yq[6], yn4 = 0.0, yn5 = 0.0;
@@ -3910,6 +4185,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     if (threadIdx.x == 0) cs_storage = c;
     __syncthreads();
     const Ctx& cs = cs_storage;
+    if (blockIdx.x >= (unsigned)a.B) {  // a helper workgroup (see run_pass)
+        helper_main(a, cs_storage, sh);
+        return;
+    }
     const int st = 8 + 16 * a.M;
     const size_t nz = obca_n(N, a.M);
     const double* zg = a.zg ? a.zg + (size_t)c.b * nz : nullptr;
@@ -3922,6 +4201,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         sh.lsq = 0;
         sh.zeta = 0.0;
         sh.nfl[0] = sh.nfl[1] = 0;
+        sh.hep = 0;
+        sh.hfail = 0;
+        if (a.board) add_rlx(board_line(a, a.B) + 2, 1);
     }
     const unsigned long long tstart = clock64();
     // ---------------- initial point (bound push, slacks = pushed d(x0), multipliers 1 / 0) ----------------
@@ -4043,7 +4325,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 phase_lin(cs, sh, red);
                 stamp(sh, ston, OPH_LIN);
                 double dinf = red[0], pinf = red[1], c0 = red[2];
-                if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; done = true; break; }
+                if (!isfinite(dinf) || !isfinite(pinf) || sh.hfail) { status = 4; done = true; break; }
                 const double nbd = n_bounds + (R ? 2.0 * n_rows : 0.0);
                 double sd = fmax(smax, red[3] / (n_rows + nbd)) / smax, sc = fmax(smax, red[4] / nbd) / smax;
                 E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
@@ -4377,6 +4659,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
             }
         }
     }
+    if (tid == 0 && a.board) {  // the helpers stop once every instance has counted itself finished
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        add_rlx(board_line(a, a.B), 1);
+    }
     if (tid == 0) {
         a.status[c.b] = status;
         if (a.iters) a.iters[c.b] = iter;
@@ -4399,7 +4685,7 @@ hipError_t launch_obca(const ObcaArgs& a, hipStream_t stream) {
         hipError_t e = hipFuncSetAttribute((const void*)obca_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(obca_kernel, dim3(a.B), dim3(T), bytes, stream, a);
+    hipLaunchKernelGGL(obca_kernel, dim3(a.B + (a.board ? a.nhelp : 0)), dim3(T), bytes, stream, a);
     return hipGetLastError();
 }
 

@@ -119,6 +119,7 @@ def lib():
            "tt_plant_update_noise_device": [i, C.POINTER(TTPlant), vp, vp, ll, vp, i, vp, vp, vp],
            "tt_policy_plant_noise_device": [i, C.POINTER(TTPlant), i, vp, vp, ll, vp, vp, vp, vp, vp, vp, vp, vp],
            "tt_fuzzy_weights_device": [i, i, vp, vp, vp, vp]}
+    sim["ttx_obca_set_helpers"] = [C.c_void_p, i]  # diagnostics (not in include/ttmpc.h)
     for name, args in sim.items():
         if os.environ.get("TTMPC_LIB") and not hasattr(L, name):
             continue  # A/B diagnostics against an older build
@@ -306,6 +307,12 @@ class ObcaSolver:
         if rc != 0:
             self._err(rc, "tt_obca_solve_batch")
         return X, U, Z, st, it, kk
+
+    def set_helpers(self, n):
+        """Diagnostics: helper workgroups of this handle's launches (0 none, -1 one per CU: the default).  The block
+        passes of the instances still solving run on the idle CUs; the results are bitwise the same either way."""
+        if hasattr(self._L, "ttx_obca_set_helpers"):
+            self._L.ttx_obca_set_helpers(self._h, int(n))
 
     def solve_device(self, B, x0, x_goal, xref, uref, z_guess, x_out, u_out, z_out, status, iters=0, kkt=0, stream=0):
         """Device pointers (ints), enqueued on ``stream``."""

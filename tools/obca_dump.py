@@ -2,7 +2,9 @@
 
     TTMPC_LIB=<build> python tools/obca_dump.py OUT.npz [B] [max_iter]
     python tools/obca_dump.py --compare A.npz B.npz
-Solves the seed-0 cobs windows (B) and c4 plans (B/4) of the bench workloads and saves X, U, status, iters."""
+Solves the seed-0 cobs windows (B) and c4 plans (B/4) of the bench workloads and saves X, U, status, iters.
+OBCA_HELPERS=n sets the helper workgroups (0: none)."""
+import os
 import sys
 from pathlib import Path
 
@@ -22,6 +24,8 @@ def dump(out, B, max_iter):
         variant = ttmpc.TT_VARIANT_TRACK_OBCA if cfg == "cobs" else ttmpc.TT_VARIANT_OBCA_PLAN
         s = ttmpc.ObcaSolver(P["N"], P["params"], sc.OBCA_Q, sc.OBCA_R, *P["bnd"], P["obs"], variant=variant,
                              max_iter=max_iter)
+        if os.environ.get("OBCA_HELPERS"):  # helper workgroups: -1 one per CU (default), 0 none
+            s.set_helpers(int(os.environ["OBCA_HELPERS"]))
         if cfg == "cobs":
             X, U, Z, st, it, kk = s.solve(data["x0"], xref=data["xref"], uref=data["uref"])
         else:

@@ -4,6 +4,7 @@
 Phase clocks are thread 0's shader cycles between phase boundaries (clock64), summed per instance."""
 import ctypes as C
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -40,6 +41,8 @@ else:
     s = ttmpc.ObcaSolver(200, sc.OBCA_PARAMS, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB,
                          sc.OBCA_UUB, obs_all[:6], max_iter=mi)
     run = lambda: s.solve(x0, xg, z_guess=zg)  # noqa: E731
+if os.environ.get("OBCA_HELPERS"):  # helper workgroups: -1 one per CU (default), 0 none
+    s.set_helpers(int(os.environ["OBCA_HELPERS"]))
 run()  # warm-up
 L.ttx_obca_set_stamps(s._h, d.data_ptr())
 X, U, Z, st, it, kk = run()
