@@ -958,7 +958,17 @@ constexpr unsigned long long kSpinTicks = 500000000ull;  // 5 s of the 100 MHz s
 __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
     LArgs& a = *c.a;
     const int nch = (c.nbk * c.NP + T - 1) / T;
-    if (threadIdx.x == 0) sh.hcur = (a.board && a.nhelp > 0 && ld_rlx(board_line(a, a.B) + 1) > 0) ? 1 : 0;
+    if (threadIdx.x == 0) {
+        // shared mode once there is a helper for every instance still solving (before that the hand-off costs the
+        // instances more than the few helpers return: profiles/r05/helpers/stamps_h.txt)
+        int on = 0;
+        if (a.board && a.nhelp > 0) {
+            gu64* hdr = board_line(a, a.B);
+            const unsigned long long fin = ld_rlx(hdr), hlp = ld_rlx(hdr + 1), started = ld_rlx(hdr + 2);
+            on = hlp > 0 && hlp + fin >= started;
+        }
+        sh.hcur = on;
+    }
     __syncthreads();
     const bool shared = sh.hcur != 0;
     __syncthreads();

@@ -167,6 +167,29 @@ def test_c4_test_cases_vs_oracle():
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
 
 
+def test_helper_workgroups_are_bitwise_neutral():
+    """The block passes (factor_block / nres_block chunks of the flat block index) run on helper workgroups once CUs are
+    idle -- here from the start, the batches being smaller than the CU count.  A chunk's arithmetic does not depend on
+    which workgroup runs it, so the outputs with helpers (the default) equal those without (every instance running its
+    own chunks) bit for bit: the 14 C4 test cases and the 16 MPC+OBCA windows, stopped at max_iter 400."""
+    import ttmpc
+    from ttmpc import scenarios as sc
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    obs, x0, xg, zg = _c4_cases(14)
+    x0w, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 16, 50, seed=0)
+    runs = []
+    for nh in (-1, 0):
+        s = _solver(200, obs, max_iter=400)
+        s.set_helpers(nh)
+        sw = _solver(50, g["obstacles"], ttmpc.TT_VARIANT_TRACK_OBCA, dict(P6, dt=0.05), (sc.XLB, sc.XUB, sc.ULB, sc.UUB),
+                     max_iter=400)
+        sw.set_helpers(nh)
+        runs.append((s.solve(x0, xg, z_guess=zg), sw.solve(x0w, xref=xr, uref=ur)))
+    for a, b in zip(runs[0], runs[1]):
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+
+
 def test_obca_lockstep_with_oracle():
     """Step-level parity: every instance of the three parity workloads (16 MPC+OBCA windows, the 14 C4 test cases, 16
     re-plans), GPU and oracle both stopped at max_iter K.  Both run the same restated IPOPT on the same inputs, so
