@@ -26,6 +26,10 @@
 //     T = E + Y'Y (never C'DC: D reaches 1e10 on the +-1e-5 range rows and that product cancels).
 //   * serial phases (Riccati backward sweep over the 6x6 stage blocks, forward sweep): wave 0, lane
 //     (i,j) owns entry (i,j) of the 6x6 products; P and PA tiles in LDS.
+//   * the factor and residual passes' block parts run over the flat block index f = j (N + 1) + k in chunks of T blocks
+//     (factor_block / nres_block, each writing a contribution record its stage adds in block order), and helper
+//     workgroups -- one per CU, launched after the B instances' -- run chunks of the instances still solving once
+//     CUs are idle (run_pass / helper_main): the C4 tail's handful of max_iter instances spread over the idle GPU.
 // Workspace: per instance in HBM, stage fields [f][k] and block fields [f][j][k] so that the lanes of a
 // stage-parallel phase (consecutive k) read consecutive addresses.
 #include <math.h>
