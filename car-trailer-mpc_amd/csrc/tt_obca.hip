@@ -208,6 +208,30 @@ __device__ __forceinline__ double inv(double x) {
 }
 
 
+// a if p else b by bit masks, both operands computed in every lane (the empty asm): no divergent branch, whatever the
+// backend would make of a select on a lane-dependent condition
+__device__ __forceinline__ double bsel(bool p, double a, double b) {
+    asm("" : "+v"(a), "+v"(b));
+    const unsigned long long m = 0ull - (unsigned long long)p;
+    return __longlong_as_double((long long)(((unsigned long long)__double_as_longlong(a) & m) |
+                                            ((unsigned long long)__double_as_longlong(b) & ~m)));
+}
+// v_q of six values computed in every lane, as v_cndmask selects: the empty asm makes each operand a value computed before
+// the select, so the backend cannot sink the arithmetic into lane-divergent branches (a serial sweep paid an exec-masked
+// branch per operand and stage for that)
+__device__ __forceinline__ double sel6(int q, double v0, double v1, double v2, double v3, double v4, double v5) {
+    asm("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5));
+    // bit masks instead of a select chain (which the backend turns into a cascade of divergent branches on q)
+    unsigned long long r = (unsigned long long)__double_as_longlong(v0);
+    const double v[5] = {v1, v2, v3, v4, v5};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const unsigned long long m = 0ull - (unsigned long long)(q == i + 1);
+        r = ((unsigned long long)__double_as_longlong(v[i]) & m) | (r & ~m);
+    }
+    return __longlong_as_double((long long)r);
+}
+
 // row_newbcast:l (gfx90a+ DPP on a 64-bit move): every lane of a 16-lane row receives lane l of that row
 template <int L_>
 __device__ __forceinline__ double rowbc(double v) {
@@ -1600,10 +1624,12 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src s
 #pragma unroll
         for (int p = 0; p < 6; ++p) {
             const double piv = readlane_d(mv, 7 * p);
-            if (!fail && !(piv >= 2.2250738585072014e-308)) fcode = pivot_fail(piv, readlane_d(m0, 7 * p));
+            // (wave-uniform scalars: selected, not branched on)
+            const int fc = pivot_fail(piv, readlane_d(m0, 7 * p));
+            fcode = (!fail && !(piv >= 2.2250738585072014e-308)) ? fc : fcode;
             const double aip = __shfl(mv, 6 * i + p), apj = __shfl(mv, 6 * p + j);
             const double ip = 1.0 / piv;
-            const double nv = (i == p && j == p) ? ip : (i == p) ? apj * ip : (j == p) ? -aip * ip : mv - aip * apj * ip;
+            const double nv = bsel(i == p && j == p, ip, bsel(i == p, apj * ip, bsel(j == p, -aip * ip, mv - aip * apj * ip)));
             fail = fail || !(piv >= 2.2250738585072014e-308);
             mv = act ? nv : 0.0;
         }
@@ -1612,7 +1638,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src s
         // expression; the HBM stores keep theirs)
         const double mji = __shfl(mv, 6 * j + i);
         // Y = S M^-1 S from the upper entry (symmetric by construction)
-        const double y = i <= j ? cur.si * mv * cur.sj : cur.sj * mji * cur.si;
+        const double y = bsel(i <= j, cur.si * mv * cur.sj, cur.sj * mji * cur.si);
         Yt[tij] = y;
         if (act && i <= j) vw.S(S_Y + sij, k) = y;
         lds_order();
@@ -1681,7 +1707,7 @@ __device__ __noinline__ void riccati_soft(const Ctx& c, LShared& sh, const Src s
             dcol(o.dj, mr, c0, c1, c2, c3);
             double ppr = ppl[0];
 #pragma unroll
-            for (int q = 1; q < 6; ++q) ppr = r == q ? ppl[q] : ppr;
+            for (int q = 1; q < 6; ++q) ppr = bsel(r == q, ppl[q], ppr);
             const double H0 = dt * Tt[8 * 5 + r], H1 = dt * Tt[8 * 4 + r];
             pnew = o.qv + fma(c0, ppl[0], fma(c1, ppl[1], fma(c2, ppl[2], fma(c3, ppl[3], ppr)))) + fma(H0, kf0, H1 * kf1);
             const double K0 = -fma(Gi00, H0, Gi01 * H1), K1 = -fma(Gi01, H0, Gi11 * H1);
@@ -1831,7 +1857,7 @@ __device__ __noinline__ void forward_soft(const Ctx& c, const Src src, int buf) 
         const double n3 = (d[3] - eq) + fma(aj[6], d[3], fma(aj[7], d[4], aj[8] * d[5]));
         const double n4 = (d[4] - eq) + dt * du1;
         const double n5 = (d[5] - eq) + dt * du0;
-        dq = q == 0 ? n0 : q == 1 ? n1 : q == 2 ? n2 : q == 3 ? n3 : q == 4 ? n4 : n5;
+        dq = sel6(q, n0, n1, n2, n3, n4, n5);
         return true;
     };
     Ops oa, ob;
@@ -3003,8 +3029,9 @@ __device__ __forceinline__ void vec_ops(const Src& src, int k, int q, bool soft,
 }
 // lanes 0..5 hold p[q] (q = lane); the serial chain per stage is sv -> (soft: 6 broadcasts, 6 FMAs) -> 6 broadcasts of
 // p' -> np, with only the lane's own row of PY, K, QV and W read from LDS, one stage ahead (ping-pong operand sets)
-template <class Src>
-__device__ __noinline__ void riccati_vec(const Ctx& c, const Src src, bool soft) {
+template <class Src, bool SOFT>
+__device__ __noinline__ void riccati_vec_t(const Ctx& c, const Src src) {
+    constexpr bool soft = SOFT;  // one instantiation per row type: no exec-masked branches on the flag in the chain
     const WsView vw = ws_view(c);
     const int lane = threadIdx.x, N = c.N;
     const double dt = c.dt;
@@ -3035,7 +3062,7 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src src, bool soft)
         const double* dj = o.dj;
         const double t2 = fma(dj[0], pp0, dj[2] * pp1), t4 = fma(dj[4], pp2, dj[7] * pp3);
         const double t5 = fma(dj[1], pp0, fma(dj[3], pp1, fma(dj[5], pp2, dj[8] * pp3)));
-        np = q == 2 ? np + t2 : q == 3 ? fma(dj[6], pp3, np) : q == 4 ? np + t4 : q == 5 ? np + t5 : np;
+        np = sel6(q, np, np, np + t2, fma(dj[6], pp3, np), np + t4, np + t5);
         if (lane < 6) vw.S(S_PV + q, km) = np;
         if (lane == 0) { vw.S(S_KF, km) = kf0; vw.S(S_KF + 1, km) = kf1; }
         pq = np;
@@ -3050,6 +3077,10 @@ __device__ __noinline__ void riccati_vec(const Ctx& c, const Src src, bool soft)
         stage(k - 1, ob);
     }
     if (k >= 1) stage(k, oa);
+}
+template <class Src>
+__device__ __forceinline__ void riccati_vec(const Ctx& c, const Src src, bool soft) {
+    soft ? riccati_vec_t<Src, true>(c, src) : riccati_vec_t<Src, false>(c, src);
 }
 
 // ---- residuals of the un-condensed Newton rows at the step in buffer buf (+ the correction's right-hand side) ----
