@@ -2204,6 +2204,233 @@ __device__ __forceinline__ void phase_trial(const Ctx& c, LShared& sh, double mu
 }
 
 
+// ======== phase: NA line-search trial points in one pass (the backtracking trials after the first) ========
+// The filter line search tries alpha, alpha/2, ... one after the other (8.8 trial points per iteration in the C4 tail,
+// profiles/r05/session_o/tail.txt), and each trial is a full pass over the trajectory whose time is its memory latency,
+// not its arithmetic.  This pass loads the iterate and the step once and evaluates NA step lengths: for each the same
+// expressions as phase_trial_t in the same order, so out[a] is bitwise phase_trial_t's result for alphas[a].  No
+// trial residual rows are stored: only the first trial of an iteration feeds a second-order correction.
+template <bool RS_, int NA>
+__device__ __noinline__ void phase_trial_multi_t(const Ctx& c, LShared& sh, double mu, const double (&al)[NA], int buf,
+                                                 double (&out)[NA][3]) {
+    LArgs& a = *c.a;
+    const int N = c.N;
+    const bool plan = c.plan();
+    constexpr bool rs = RS_;
+    double th[NA], F[NA], logs[NA], bad[NA];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) { th[q] = 0.0; F[q] = 0.0; logs[q] = 0.0; bad[q] = 0.0; }
+    for (int k = (int)threadIdx.x; k <= N; k += T) {
+        double X[6], DX[6], U[2] = {0.0, 0.0}, DU[2] = {0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { X[i] = c.S(S_X + i, k); DX[i] = c.S(S_DX + 6 * buf + i, k); }
+        if (k < N)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { U[i] = c.S(S_U + i, k); DU[i] = c.S(S_DU + 2 * buf + i, k); }
+        double x[NA][6], u[NA][2];
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) x[q][i] = X[i] + al[q] * DX[i];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) u[q][i] = k < N ? U[i] + al[q] * DU[i] : 0.0;
+        }
+        double scost[NA];
+#pragma unroll
+        for (int q = 0; q < NA; ++q) scost[q] = rs ? 0.0 : stage_cost(c, k, x[q], u[q]);
+        LogSum ls[NA];
+        bool ok[NA];
+        double Fr[NA], prox[NA];
+#pragma unroll
+        for (int q = 0; q < NA; ++q) { ok[q] = true; Fr[q] = 0.0; prox[q] = 0.0; }
+        double xr[6], drx[6];
+        if (rs)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) { xr[i] = c.S(S_XR + i, k); drx[i] = c.S(S_DRX + i, k); }
+#pragma unroll
+        for (int q = 0; q < NA; ++q)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                if (c.hlx(i)) { const double sl = x[q][i] - c.xl[i]; ok[q] &= sl > 0.0; ls[q].add(sl); }
+                if (c.hux(i)) { const double sl = c.xu[i] - x[q][i]; ok[q] &= sl > 0.0; ls[q].add(sl); }
+                if (rs) { const double e = x[q][i] - xr[i]; prox[q] += drx[i] * e * e; }
+            }
+        if (k < N) {
+            double ur[2], dru[2];
+            if (rs)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) { ur[i] = c.S(S_UR + i, k); dru[i] = c.S(S_DRU + i, k); }
+#pragma unroll
+            for (int q = 0; q < NA; ++q)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (c.hlu(i)) { const double sl = u[q][i] - c.ul[i]; ok[q] &= sl > 0.0; ls[q].add(sl); }
+                    if (c.huu(i)) { const double sl = c.uu[i] - u[q][i]; ok[q] &= sl > 0.0; ls[q].add(sl); }
+                    if (rs) { const double e = u[q][i] - ur[i]; prox[q] += dru[i] * e * e; }
+                }
+        }
+        double ck[NA][6];
+#pragma unroll
+        for (int q = 0; q < NA; ++q)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) ck[q][i] = k == 0 ? x[q][i] - a.x0[6 * (size_t)c.b + i] : 0.0;
+        if (k < N) {
+            double XN[6], DXN[6], PN[6], DPN[6], NN[6], DNN[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                XN[i] = c.S(S_X + i, k + 1); DXN[i] = c.S(S_DX + 6 * buf + i, k + 1);
+                if (rs) {
+                    PN[i] = c.S(S_PR + i, k + 1); DPN[i] = c.S(S_DP + 6 * buf + i, k + 1);
+                    NN[i] = c.S(S_NR + i, k + 1); DNN[i] = c.S(S_DN + 6 * buf + i, k + 1);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NA; ++q) {
+                double fo[6];
+                model_f(a, x[q], u[q], fo);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const double xn = XN[i] + al[q] * DXN[i];
+                    double cv = xn - (x[q][i] + a.dt * fo[i]);
+                    if (rs) {
+                        const double p = PN[i] + al[q] * DPN[i];
+                        const double n = NN[i] + al[q] * DNN[i];
+                        cv -= p - n;
+                    }
+                    th[q] += fabs(cv);
+                }
+            }
+        }
+        if (rs) {
+            double P0[6], DP0[6], N0[6], DN0[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                P0[i] = c.S(S_PR + i, k); DP0[i] = c.S(S_DP + 6 * buf + i, k);
+                N0[i] = c.S(S_NR + i, k); DN0[i] = c.S(S_DN + 6 * buf + i, k);
+            }
+#pragma unroll
+            for (int q = 0; q < NA; ++q)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const double p = P0[i] + al[q] * DP0[i];
+                    const double n = N0[i] + al[q] * DN0[i];
+                    ok[q] &= p > 0.0 && n > 0.0;
+                    ls[q].add(p);
+                    ls[q].add(n);
+                    Fr[q] += p + n;
+                    if (k == 0) ck[q][i] -= p - n;
+                }
+        }
+        if (k == 0)
+#pragma unroll
+            for (int q = 0; q < NA; ++q)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) th[q] += fabs(ck[q][i]);
+        Trig tr[NA];
+#pragma unroll
+        for (int q = 0; q < NA; ++q) tr[q] = stage_trig(x[q]);
+        for (int j = 0; j < c.nbk; ++j) {
+            double W[8], DW[8], wr[8], drw[8], S[4], DS[4], PV[4], DPV[4], NV[4], DNV[4];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                W[e] = c.B(B_W + e, j, k); DW[e] = c.B(B_DW + 8 * buf + e, j, k);
+                if (rs) { wr[e] = c.B(B_WR + e, j, k); drw[e] = c.B(B_DRW + e, j, k); }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                S[r] = c.B(B_S + r, j, k); DS[r] = c.B(B_DS + 4 * buf + r, j, k);
+                if (rs) {
+                    PV[r] = c.B(B_PR + r, j, k); DPV[r] = c.B(B_DP + 4 * buf + r, j, k);
+                    NV[r] = c.B(B_NR + r, j, k); DNV[r] = c.B(B_DN + 4 * buf + r, j, k);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NA; ++q) {
+                double w[8], d[4];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) w[e] = W[e] + al[q] * DW[e];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const double sl = w[e] + RELAX;
+                    ok[q] &= sl > 0.0;
+                    ls[q].add(sl);
+                    if (rs) { const double ew = w[e] - wr[e]; prox[q] += drw[e] * ew * ew; }
+                }
+                blk_vals(a, x[q], tr[q], j, w, d);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double s = S[r] + al[q] * DS[r];
+                    double res = d[r] - s;
+                    if (rs) {
+                        const double p = PV[r] + al[q] * DPV[r];
+                        const double n = NV[r] + al[q] * DNV[r];
+                        ok[q] &= p > 0.0 && n > 0.0;
+                        ls[q].add(p);
+                        ls[q].add(n);
+                        Fr[q] += p + n;
+                        res -= p - n;
+                    }
+                    th[q] += fabs(res);
+                    const double su = c.rU(r) - s;
+                    ok[q] &= su > 0.0;
+                    ls[q].add(su);
+                    if (c.hrl(r)) { const double sl = s - c.rL(r); ok[q] &= sl > 0.0; ls[q].add(sl); }
+                }
+            }
+        }
+        if (k == N && plan)
+#pragma unroll
+            for (int q = 0; q < NA; ++q)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const double s = sh.sf[i] + al[q] * sh.dsf[buf][i];
+                    double res = (x[q][i] - c.tgt_x[i]) - s;
+                    if (rs) {
+                        const double p = sh.pf[i] + al[q] * sh.dpf[buf][i], n = sh.nf[i] + al[q] * sh.dnf[buf][i];
+                        ok[q] &= p > 0.0 && n > 0.0;
+                        ls[q].add(p);
+                        ls[q].add(n);
+                        Fr[q] += p + n;
+                        res -= p - n;
+                    }
+                    th[q] += fabs(res);
+                    const double sl = s - c.fL, su = c.fU - s;
+                    ok[q] &= sl > 0.0 && su > 0.0;
+                    ls[q].add(sl);
+                    ls[q].add(su);
+                }
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            F[q] += rs ? RHO * Fr[q] + 0.5 * sh.zeta * prox[q] : scost[q];
+            if (!ok[q]) bad[q] = 1.0;
+            else logs[q] += ls[q].value();
+        }
+    }
+    double v[4 * NA];
+    int ops[4 * NA];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+        v[4 * q] = th[q]; v[4 * q + 1] = F[q]; v[4 * q + 2] = logs[q]; v[4 * q + 3] = bad[q];
+        ops[4 * q] = R_SUM; ops[4 * q + 1] = R_SUM; ops[4 * q + 2] = R_SUM; ops[4 * q + 3] = R_MAX;
+    }
+    wg_reduce(sh, v, ops);
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+        out[q][0] = v[4 * q + 3] > 0.0 ? INFINITY : v[4 * q];
+        out[q][1] = v[4 * q + 3] > 0.0 ? INFINITY : v[4 * q + 1] - mu * v[4 * q + 2];
+        out[q][2] = v[4 * q + 3];
+    }
+}
+#ifndef OBCA_TRIAL_BATCH
+#define OBCA_TRIAL_BATCH 4
+#endif
+constexpr int kTrialBatch = OBCA_TRIAL_BATCH;  // trials per batched pass (A/B builds: -DOBCA_TRIAL_BATCH=n)
+__device__ __forceinline__ void phase_trial_multi(const Ctx& c, LShared& sh, double mu, const double (&al)[kTrialBatch],
+                                                  int buf, double (&out)[kTrialBatch][3]) {
+    sh.R ? phase_trial_multi_t<true, kTrialBatch>(c, sh, mu, al, buf, out)
+         : phase_trial_multi_t<false, kTrialBatch>(c, sh, mu, al, buf, out);
+}
+
 // ======== phase: second-order-correction residual r <- a_soc r + r(trial) ========
 // (both residual phases load every value before the stores that would precede it in program order -- their
 // waits would include those stores, one in-order vmcnt queue -- so a block's results are stored after the
@@ -2956,7 +3183,9 @@ struct VecG {
     __device__ double K(int i, int k) const { return c.S(S_K + i, k); }
     __device__ double AJ(int i, int k) const { return c.S(S_AJ + i, k); }
 };
-__device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft) {
+template <bool SOFT>
+__device__ __noinline__ void stage_vec_inputs_t(const Ctx& c, double* A) {
+    constexpr bool soft = SOFT;
     for (int k = (int)threadIdx.x; k <= c.N; k += T) {
         lds_double* r = (lds_double*)A + (size_t)k * LV;
         double P[21], e[6];
@@ -2967,15 +3196,14 @@ __device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft
         double q[6], rv[2] = {0.0, 0.0}, gi[3] = {0.0, 0.0, 0.0}, kk[12], aj[9];
 #pragma unroll
         for (int i = 0; i < 6; ++i) q[i] = c.S(S_QV + i, k);
-        const bool st = k < c.N;
+        // (stage N's K, AJ, RV, GI rows are never read by the sweep -- it reads them at k - 1 -- so every stage loads them:
+        // no exec-masked branch per field)
 #pragma unroll
-        for (int i = 0; i < 12; ++i) kk[i] = st ? (double)c.S(S_K + i, k) : 0.0;
+        for (int i = 0; i < 12; ++i) kk[i] = c.S(S_K + i, k);
 #pragma unroll
-        for (int i = 0; i < 9; ++i) aj[i] = st ? (double)c.S(S_AJ + i, k) : 0.0;
-        if (st) {
-            rv[0] = c.S(S_RV, k); rv[1] = c.S(S_RV + 1, k);
-            gi[0] = c.S(S_GI, k); gi[1] = c.S(S_GI + 1, k); gi[2] = c.S(S_GI + 2, k);
-        }
+        for (int i = 0; i < 9; ++i) aj[i] = c.S(S_AJ + i, k);
+        rv[0] = c.S(S_RV, k); rv[1] = c.S(S_RV + 1, k);
+        gi[0] = c.S(S_GI, k); gi[1] = c.S(S_GI + 1, k); gi[2] = c.S(S_GI + 2, k);
         double Y[21];
 #pragma unroll
         for (int i = 0; i < 21; ++i) Y[i] = soft ? (double)c.S(S_Y + i, k) : 0.0;
@@ -3005,6 +3233,9 @@ __device__ __noinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft
 #pragma unroll
         for (int i = 0; i < 9; ++i) r[65 + i] = aj[i];
     }
+}
+__device__ __forceinline__ void stage_vec_inputs(const Ctx& c, double* A, bool soft) {
+    soft ? stage_vec_inputs_t<true>(c, A) : stage_vec_inputs_t<false>(c, A);
 }
 // operands of one stage of the vector sweep (lane q's row), loaded one stage ahead of its use
 struct VecOps {
@@ -4484,10 +4715,26 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                         }
                         amin *= g_al;
                         accepted = rel < 1e-15;
+                        // backtracking trials (ls >= 1) are evaluated kTrialBatch at a time (phase_trial_multi: the
+                        // loop's own alpha sequence, bitwise phase_trial's results) and consumed one by one below
+                        double pre[kTrialBatch][3];
+                        int npre = 0;
                         for (int ls = 0; !accepted; ++ls) {
                             double tr[3];
                             count(sh, ston, OCNT_TRIAL);
-                            phase_trial(cs, sh, mu, alpha, 0, tr);
+                            if (ls == 0) {
+                                phase_trial(cs, sh, mu, alpha, 0, tr);
+                            } else {
+                                if (npre == 0) {
+                                    double al[kTrialBatch], an = alpha;
+#pragma unroll
+                                    for (int q = 0; q < kTrialBatch; ++q) { al[q] = an; an *= 0.5; }
+                                    phase_trial_multi(cs, sh, mu, al, 0, pre);
+                                    npre = kTrialBatch;
+                                }
+                                const int q = kTrialBatch - npre--;
+                                tr[0] = pre[q][0]; tr[1] = pre[q][1]; tr[2] = pre[q][2];
+                            }
                             stamp(sh, ston, OPH_TRIAL);
                             const bool sw = Dm < 0.0 && alpha * pow(-Dm, s_ph) > delta * pow(th0, s_th);
                             bool okls = false;
