@@ -178,6 +178,7 @@ __device__ __forceinline__ void count(LShared& sh, bool on, int ev) {
 // workgroup reduction of NV values with per-value op; result uniform in every thread, fixed order
 template <int NV>
 __device__ __forceinline__ void wg_reduce(LShared& sh, double (&v)[NV], const int (&op)[NV]) {
+    static_assert(NV <= 16, "Shared::red holds 16 values per wave");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double r[NV];
 #pragma unroll
