@@ -84,13 +84,14 @@ def lib():
     L.tt_obca_solve_batch.restype = C.c_int
     L.tt_obca_solve_batch_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 12
     L.tt_obca_solve_batch_device.restype = C.c_int
-    L.tt_obca_solve_batch_iterate.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip,
-                                              _dp, _dp]
-    L.tt_obca_solve_batch_iterate.restype = C.c_int
-    L.tt_obca_solve_batch_iterate_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 13
-    L.tt_obca_solve_batch_iterate_device.restype = C.c_int
-    L.tt_obca_iterate_len.argtypes = [C.c_int, C.c_int]
-    L.tt_obca_iterate_len.restype = C.c_longlong
+    if not os.environ.get("TTMPC_LIB") or hasattr(L, "tt_obca_iterate_len"):  # (A/B against a pre-round-5 build)
+        L.tt_obca_solve_batch_iterate.argtypes = [C.c_void_p, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip,
+                                                  _dp, _dp]
+        L.tt_obca_solve_batch_iterate.restype = C.c_int
+        L.tt_obca_solve_batch_iterate_device.argtypes = [C.c_void_p, C.c_int] + [C.c_void_p] * 13
+        L.tt_obca_solve_batch_iterate_device.restype = C.c_int
+        L.tt_obca_iterate_len.argtypes = [C.c_int, C.c_int]
+        L.tt_obca_iterate_len.restype = C.c_longlong
     L.tt_obca_n.argtypes = [C.c_int, C.c_int]
     L.tt_obca_n.restype = C.c_longlong
     L.tt_obca_workspace_bytes.argtypes = [C.c_int, C.c_int]
