@@ -967,7 +967,7 @@ struct ChunkPass {
     double mu, dw, tau;
     int pass, buf, prep, mode;
 };
-__device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1);
+__device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1, bool helper);
 
 __device__ __forceinline__ gu64* board_line(LArgs& a, int b) { return (gu64*)(a.board + (size_t)b * kObcaBoardStride); }
 __device__ __forceinline__ unsigned long long ld_rlx(gu64* p) {
@@ -1002,7 +1002,7 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
     const bool shared = sh.hcur != 0;
     __syncthreads();
     if (!shared) {
-        do_chunks(c, sh, p, 0, nch);
+        do_chunks(c, sh, p, 0, nch, false);
         __syncthreads();
         return;
     }
@@ -1027,7 +1027,7 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
         const int ci = sh.hcur;
         __syncthreads();
         if (ci >= nch) break;
-        do_chunks(c, sh, p, ci, ci + 1);
+        do_chunks(c, sh, p, ci, ci + 1, false);
         ++own;
     }
     if (threadIdx.x == 0) {
@@ -1045,12 +1045,22 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
     __syncthreads();
 }
 
+// a block part's store: plain (the instance's own chunks), or write-through (sc1) when a helper workgroup runs the chunk,
+// so that its hand-off needs no L2 write-back (MI355X guide, R1: every payload byte stored sc1 and drained, then the done
+// count; the instance still acquires before reading)
+template <bool SC1>
+__device__ __forceinline__ void bst(gdouble& ref, double v) {
+    if constexpr (SC1) __hip_atomic_store((gu64*)&ref, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    else ref = v;
+}
 // ---- the factor pass's block part: linearise + factor + right-hand side of block (j, k) of the flat block index ----
 // Only the block's contributions to its stage leave it (the recovery passes recompute the elimination, block_refactor):
 // the Schur complement C4, the gradient q4 and the factorisation outcome, in its record B_CB; phase_factor's stage part
 // adds a stage's records in block order (the arithmetic of the block loop inside the stage loop).
 enum : int { CF_C4 = 0, CF_Q4 = 10, CF_FAIL = 14, CF_END = 15 };
 static_assert(CF_END <= B_END - B_CB, "factor contribution record");
+template <bool SC1>
 __device__ __forceinline__ void factor_block(const Ctx& c, const LShared& sh, const WsView& vw, int j, int k, double mu,
                                              double dw) {
     double x[6];
@@ -1064,7 +1074,7 @@ __device__ __forceinline__ void factor_block(const Ctx& c, const LShared& sh, co
     load_blk_in(c, sh.R != 0, j, k, cur);
     cf[CF_FAIL] = (double)block_setup(c, sh, cur, j, x, tr, mu, dw, bk, fw, zf, t4, cf + CF_C4, cf + CF_Q4);
 #pragma unroll
-    for (int i = 0; i < CF_END; ++i) vw.B(B_CB + i, j, k) = cf[i];
+    for (int i = 0; i < CF_END; ++i) bst<SC1>(vw.B(B_CB + i, j, k), cf[i]);
 }
 
 // ======== phase: stage Hessians + gradients (all threads) -> factorisation outcome (uniform) ========
@@ -3339,6 +3349,7 @@ enum { NR_STEP = 0, NR_MAIN = 1, NR_CORR = 2 };
 enum : int { CB_DM = 0, CB_RMAX = 1, CB_BMAX = 2, CB_SN = 3, CB_REL = 4, CB_AP = 5, CB_AZ = 6, CB_RX = 7, CB_Q4 = 13,
              CB_END = 17 };
 static_assert(B_CB + CB_END == B_END, "contribution record");
+template <bool SC1>
 __device__ __forceinline__ void nres_block(const Ctx& c, const LShared& sh, const WsView& vw, int j, int k, double mu,
                                            double dw, double tau, int buf, bool prep, int mode) {
     LArgs& a = *c.a;
@@ -3385,7 +3396,7 @@ __device__ __forceinline__ void nres_block(const Ctx& c, const LShared& sh, cons
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 dwv[e] = add ? (double)vw.B(B_DW + 8 * buf + e, j, k) + dwr[e] : dwr[e];
-                vw.B(B_DW + 8 * buf + e, j, k) = dwv[e];
+                bst<SC1>(vw.B(B_DW + 8 * buf + e, j, k), dwv[e]);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -3393,15 +3404,15 @@ __device__ __forceinline__ void nres_block(const Ctx& c, const LShared& sh, cons
                 const double dsr = (ypr[r] - gs) / bk.D[r];
                 ydp[r] = add ? (double)vw.B(B_YP + 4 * buf + r, j, k) + ypr[r] : ypr[r];
                 ds[r] = add ? (double)vw.B(B_DS + 4 * buf + r, j, k) + dsr : dsr;
-                vw.B(B_YP + 4 * buf + r, j, k) = ydp[r];
-                vw.B(B_DS + 4 * buf + r, j, k) = ds[r];
+                bst<SC1>(vw.B(B_YP + 4 * buf + r, j, k), ydp[r]);
+                bst<SC1>(vw.B(B_DS + 4 * buf + r, j, k), ds[r]);
                 if (rs) {
                     const double p = in.pr[r], n = in.nr[r], zp = in.zp[r], zn = in.zn[r];
                     const double gp = add ? (double)vw.B(B_OP + r, j, k) : RHO - mu / p;
                     const double gn = add ? (double)vw.B(B_ON + r, j, k) : RHO - mu / n;
                     const double dpr = (ypr[r] - gp) / (zp / p + dw), dnr = (-ypr[r] - gn) / (zn / n + dw);
-                    vw.B(B_DP + 4 * buf + r, j, k) = add ? (double)vw.B(B_DP + 4 * buf + r, j, k) + dpr : dpr;
-                    vw.B(B_DN + 4 * buf + r, j, k) = add ? (double)vw.B(B_DN + 4 * buf + r, j, k) + dnr : dnr;
+                    bst<SC1>(vw.B(B_DP + 4 * buf + r, j, k), add ? (double)vw.B(B_DP + 4 * buf + r, j, k) + dpr : dpr);
+                    bst<SC1>(vw.B(B_DN + 4 * buf + r, j, k), add ? (double)vw.B(B_DN + 4 * buf + r, j, k) + dnr : dnr);
                 }
             }
         }
@@ -3499,25 +3510,26 @@ __device__ __forceinline__ void nres_block(const Ctx& c, const LShared& sh, cons
 #pragma unroll
         for (int r = 0; r < 4; ++r) rdc[r] = rdv[r] + rsl[r] / bk.D[r] + (rs ? rpv[r] / Dpv[r] - rnv[r] / Dnv[r] : 0.0);
         blk_rhs(bk, rw, rdc, zf, t4, cb + CB_Q4);
-        auto stf = [&](int f, double v) { vw.B(B_FR + f, j, k) = v; };
+        auto stf = [&](int f, double v) { bst<SC1>(vw.B(B_FR + f, j, k), v); };
 #pragma unroll
         for (int e = 0; e < 8; ++e) stf(FR_FW + e, rw[e]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { stf(FR_ZFL + e, zf[4 + e]); stf(FR_T + e, t4[e]); }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            vw.B(B_OS + r, j, k) = rsl[r];
-            if (rs) { vw.B(B_OP + r, j, k) = rpv[r]; vw.B(B_ON + r, j, k) = rnv[r]; }
+            bst<SC1>(vw.B(B_OS + r, j, k), rsl[r]);
+            if (rs) { bst<SC1>(vw.B(B_OP + r, j, k), rpv[r]); bst<SC1>(vw.B(B_ON + r, j, k), rnv[r]); }
         }
     }
     cb[CB_DM] = Dmb; cb[CB_RMAX] = rmax; cb[CB_BMAX] = bmax; cb[CB_SN] = snorm; cb[CB_REL] = rel; cb[CB_AP] = ap;
     cb[CB_AZ] = az;
 #pragma unroll
-    for (int i = 0; i < CB_END; ++i) vw.B(B_CB + i, j, k) = cb[i];
+    for (int i = 0; i < CB_END; ++i) bst<SC1>(vw.B(B_CB + i, j, k), cb[i]);
 }
 
 // chunks [c0, c1) of a block pass: thread t runs block f = ci T + t of the flat block index (one function per pass, so
 // that neither block part's registers constrain the other's)
+template <bool SC1>
 __device__ __noinline__ void nres_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
     const WsView vw = ws_view(c);
     const int nblk = c.nbk * c.NP, np = c.NP;
@@ -3525,9 +3537,10 @@ __device__ __noinline__ void nres_chunks(const Ctx& c, const LShared& sh, ChunkP
         const int f = ci * T + (int)threadIdx.x;
         if (f >= nblk) break;
         const int j = f / np;
-        nres_block(c, sh, vw, j, f - j * np, p.mu, p.dw, p.tau, p.buf, p.prep != 0, p.mode);
+        nres_block<SC1>(c, sh, vw, j, f - j * np, p.mu, p.dw, p.tau, p.buf, p.prep != 0, p.mode);
     }
 }
+template <bool SC1>
 __device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
     const WsView vw = ws_view(c);
     const int nblk = c.nbk * c.NP, np = c.NP;
@@ -3535,12 +3548,12 @@ __device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, Chun
         const int f = ci * T + (int)threadIdx.x;
         if (f >= nblk) break;
         const int j = f / np;
-        factor_block(c, sh, vw, j, f - j * np, p.mu, p.dw);
+        factor_block<SC1>(c, sh, vw, j, f - j * np, p.mu, p.dw);
     }
 }
-__device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
-    if (p.pass == PASS_NRES) nres_chunks(c, sh, p, c0, c1);
-    else factor_chunks(c, sh, p, c0, c1);
+__device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1, bool helper) {
+    if (p.pass == PASS_NRES) helper ? nres_chunks<true>(c, sh, p, c0, c1) : nres_chunks<false>(c, sh, p, c0, c1);
+    else helper ? factor_chunks<true>(c, sh, p, c0, c1) : factor_chunks<false>(c, sh, p, c0, c1);
 }
 
 // a helper workgroup: serve open chunks of any instance until every instance has finished
@@ -3611,14 +3624,10 @@ __device__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
         p.mu = sh.hp_mu; p.dw = sh.hp_dw; p.tau = sh.hp_tau;
         const int pk = sh.hp_pk;
         p.pass = pk & 15; p.buf = (pk >> 4) & 15; p.prep = (pk >> 8) & 15; p.mode = (pk >> 12) & 15;
-        do_chunks(cw, sh, p, ci, ci + 1);
+        do_chunks(cw, sh, p, ci, ci + 1, true);  // write-through stores: no release (L2 write-back) needed
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            add_rlx(board_line(a, b) + 1, 1);
-        }
+        if (lane == 0) add_rlx(board_line(a, b) + 1, 1);
     }
 }
 
