@@ -962,7 +962,7 @@ __device__ __forceinline__ void block_refactor(const Ctx& c, const LShared& sh, 
 // of the instance's data; a helper's chunk ends with drained stores, a release and the done add; the instance acquires
 // once the done count is complete.  Every spin is bounded.
 typedef __attribute__((address_space(1))) unsigned long long gu64;
-enum { PASS_FACTOR = 1, PASS_NRES = 2 };
+enum { PASS_FACTOR = 1, PASS_NRES = 2, PASS_UPDATE = 4 };
 struct ChunkPass {
     double mu, dw, tau;
     int pass, buf, prep, mode;
@@ -2522,6 +2522,67 @@ __device__ __forceinline__ void load_upd_in(const Ctx& c, bool rs, int buf, int 
     }
 }
 
+// ---- the update pass's block part: block (j, k) of the flat block index (no reduction: any workgroup can run it) ----
+template <bool RS_, bool SC1>
+__device__ __forceinline__ void update_block(const Ctx& c, const WsView& vw, int j, int k, double mu, double alpha,
+                                             double az, int buf) {
+    constexpr bool rs = RS_;
+    UpdIn cur;
+    load_upd_in(c, rs, buf, j, k, cur);
+    double wn[8], zwn[8], sn[4], vun[4], vln[4], ydn[4], prn[4], nrn[4], zpn[4], znn[4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const double w = cur.w[e], dv = cur.dw[e], z = cur.zw[e];
+        const double sl = w + RELAX;
+        wn[e] = w + alpha * dv;
+        double zn2 = z + az * (mu * inv(sl) - z - z * inv(sl) * dv);
+        clamp_mult(zn2, wn[e] + RELAX, mu);
+        zwn[e] = zn2;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double sv = cur.s[r], dv = cur.ds[r];
+        sn[r] = sv + alpha * dv;
+        const double vu = cur.vu[r], slu = c.rU(r) - sv;
+        double vu2 = vu + az * (mu * inv(slu) - vu + vu * inv(slu) * dv);
+        clamp_mult(vu2, c.rU(r) - sn[r], mu);
+        vun[r] = vu2;
+        if (c.hrl(r)) {
+            const double vl = cur.vl[r], sll = sv - c.rL(r);
+            double vl2 = vl + az * (mu * inv(sll) - vl - vl * inv(sll) * dv);
+            clamp_mult(vl2, sn[r] - c.rL(r), mu);
+            vln[r] = vl2;
+        }
+        ydn[r] = cur.yd[r] + alpha * (cur.yp[r] - cur.yd[r]);
+        if (rs) {
+            const double p = cur.pr[r], n = cur.nr[r], zpv = cur.zp[r], znv = cur.zn[r];
+            prn[r] = p + alpha * cur.dp[r];
+            nrn[r] = n + alpha * cur.dn[r];
+            double a1 = zpv + az * (mu * inv(p) - zpv - zpv * inv(p) * cur.dp[r]);
+            double a2 = znv + az * (mu * inv(n) - znv - znv * inv(n) * cur.dn[r]);
+            clamp_mult(a1, prn[r], mu);
+            clamp_mult(a2, nrn[r], mu);
+            zpn[r] = a1;
+            znn[r] = a2;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { bst<SC1>(vw.B(B_W + e, j, k), wn[e]); bst<SC1>(vw.B(B_ZW + e, j, k), zwn[e]); }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        bst<SC1>(vw.B(B_VU + r, j, k), vun[r]);
+        if (c.hrl(r)) bst<SC1>(vw.B(B_VL + r, j, k), vln[r]);
+        bst<SC1>(vw.B(B_S + r, j, k), sn[r]);
+        bst<SC1>(vw.B(B_YD + r, j, k), ydn[r]);
+        if (rs) {
+            bst<SC1>(vw.B(B_PR + r, j, k), prn[r]);
+            bst<SC1>(vw.B(B_NR + r, j, k), nrn[r]);
+            bst<SC1>(vw.B(B_ZP + r, j, k), zpn[r]);
+            bst<SC1>(vw.B(B_ZN + r, j, k), znn[r]);
+        }
+    }
+}
+
 // ======== phase: accept the step (primal alpha, duals az, kappa_sigma safeguard) ========
 // All loads of a stage are issued before its stores, and block j+1's loads before block j's stores: the
 // workspace fields may alias as far as the compiler knows, so interleaved load / store pairs would each wait
@@ -2530,6 +2591,9 @@ template <bool RS_>
 __device__ __noinline__ void phase_update_t(const Ctx& c, LShared& sh, double mu, double alpha, double az, int buf) {
     const int N = c.N;
     constexpr bool rs = RS_;
+    // the blocks over the flat block index (update_block), by this workgroup and any helpers (alpha and az travel as
+    // the pass's second and third parameters); the stage fields below
+    run_pass(c, sh, ChunkPass{mu, alpha, az, PASS_UPDATE, buf, 0, 0});
     for (int k = (int)threadIdx.x; k <= N; k += T) {
         double x[6], d[6], zl[6], zu[6], y[6], yp[6], pr[6], nr[6], zp[6], zn[6], dp[6], dn[6];
 #pragma unroll
@@ -2551,8 +2615,6 @@ __device__ __noinline__ void phase_update_t(const Ctx& c, LShared& sh, double mu
                 if (c.hlu(i)) zlu[i] = c.S(S_ZLU + i, k);
                 if (c.huu(i)) zuu[i] = c.S(S_ZUU + i, k);
             }
-        UpdIn cur;
-        if (c.nbk > 0) load_upd_in(c, rs, buf, 0, k, cur);
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const double xv = x[i], dv = d[i];
@@ -2602,61 +2664,6 @@ __device__ __noinline__ void phase_update_t(const Ctx& c, LShared& sh, double mu
                 }
                 c.S(S_U + i, k) = un;
             }
-        for (int j = 0; j < c.nbk; ++j) {
-            double wn[8], zwn[8], sn[4], vun[4], vln[4], ydn[4], prn[4], nrn[4], zpn[4], znn[4];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const double w = cur.w[e], dv = cur.dw[e], z = cur.zw[e];
-                const double sl = w + RELAX;
-                wn[e] = w + alpha * dv;
-                double zn2 = z + az * (mu * inv(sl) - z - z * inv(sl) * dv);
-                clamp_mult(zn2, wn[e] + RELAX, mu);
-                zwn[e] = zn2;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double sv = cur.s[r], dv = cur.ds[r];
-                sn[r] = sv + alpha * dv;
-                const double vu = cur.vu[r], slu = c.rU(r) - sv;
-                double vu2 = vu + az * (mu * inv(slu) - vu + vu * inv(slu) * dv);
-                clamp_mult(vu2, c.rU(r) - sn[r], mu);
-                vun[r] = vu2;
-                if (c.hrl(r)) {
-                    const double vl = cur.vl[r], sll = sv - c.rL(r);
-                    double vl2 = vl + az * (mu * inv(sll) - vl - vl * inv(sll) * dv);
-                    clamp_mult(vl2, sn[r] - c.rL(r), mu);
-                    vln[r] = vl2;
-                }
-                ydn[r] = cur.yd[r] + alpha * (cur.yp[r] - cur.yd[r]);
-                if (rs) {
-                    const double p = cur.pr[r], n = cur.nr[r], zpv = cur.zp[r], znv = cur.zn[r];
-                    prn[r] = p + alpha * cur.dp[r];
-                    nrn[r] = n + alpha * cur.dn[r];
-                    double a1 = zpv + az * (mu * inv(p) - zpv - zpv * inv(p) * cur.dp[r]);
-                    double a2 = znv + az * (mu * inv(n) - znv - znv * inv(n) * cur.dn[r]);
-                    clamp_mult(a1, prn[r], mu);
-                    clamp_mult(a2, nrn[r], mu);
-                    zpn[r] = a1;
-                    znn[r] = a2;
-                }
-            }
-            if (j + 1 < c.nbk) load_upd_in(c, rs, buf, j + 1, k, cur);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { c.B(B_W + e, j, k) = wn[e]; c.B(B_ZW + e, j, k) = zwn[e]; }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                c.B(B_VU + r, j, k) = vun[r];
-                if (c.hrl(r)) c.B(B_VL + r, j, k) = vln[r];
-                c.B(B_S + r, j, k) = sn[r];
-                c.B(B_YD + r, j, k) = ydn[r];
-                if (rs) {
-                    c.B(B_PR + r, j, k) = prn[r];
-                    c.B(B_NR + r, j, k) = nrn[r];
-                    c.B(B_ZP + r, j, k) = zpn[r];
-                    c.B(B_ZN + r, j, k) = znn[r];
-                }
-            }
-        }
         if (k == N && c.plan())
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
@@ -3551,9 +3558,22 @@ __device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, Chun
         factor_block<SC1>(c, sh, vw, j, f - j * np, p.mu, p.dw);
     }
 }
+template <bool RS_, bool SC1>
+__device__ __noinline__ void update_chunks(const Ctx& c, ChunkPass p, int c0, int c1) {
+    const WsView vw = ws_view(c);
+    const int nblk = c.nbk * c.NP, np = c.NP;
+    for (int ci = c0; ci < c1; ++ci) {
+        const int f = ci * T + (int)threadIdx.x;
+        if (f >= nblk) break;
+        const int j = f / np;
+        update_block<RS_, SC1>(c, vw, j, f - j * np, p.mu, p.dw, p.tau, p.buf);
+    }
+}
 __device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1, bool helper) {
     if (p.pass == PASS_NRES) helper ? nres_chunks<true>(c, sh, p, c0, c1) : nres_chunks<false>(c, sh, p, c0, c1);
-    else helper ? factor_chunks<true>(c, sh, p, c0, c1) : factor_chunks<false>(c, sh, p, c0, c1);
+    else if (p.pass == PASS_FACTOR) helper ? factor_chunks<true>(c, sh, p, c0, c1) : factor_chunks<false>(c, sh, p, c0, c1);
+    else if (sh.R) helper ? update_chunks<true, true>(c, p, c0, c1) : update_chunks<true, false>(c, p, c0, c1);
+    else helper ? update_chunks<false, true>(c, p, c0, c1) : update_chunks<false, false>(c, p, c0, c1);
 }
 
 // a helper workgroup: serve open chunks of any instance until every instance has finished
