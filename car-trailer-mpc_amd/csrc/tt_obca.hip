@@ -35,6 +35,7 @@
 #include <math.h>
 
 #include "tt_kernel.hpp"
+#include "tt_trig.hpp"
 
 // FMA contraction within a source expression only (the C rule), never across statements: the backend's
 // cross-statement fusion depends on how many uses a product has in the inlined context, so the same block
@@ -336,8 +337,7 @@ __device__ __forceinline__ void model_f(LArgs& a, const double* x, const double*
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
     const double t = tan(phi);
     double sth, cth, sps, cps;
-    sincos(th, &sth, &cth);
-    sincos(psi, &sps, &cps);
+    sincos2(th, sth, cth, psi, sps, cps);
     fo[0] = v * cth;
     fo[1] = v * sth;
     fo[2] = v * t / a.L1;
@@ -351,8 +351,7 @@ __device__ __forceinline__ void model_lin(LArgs& a, const double* x, const doubl
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
     const double L1 = a.L1, L2 = a.L2, M = a.Mh, dt = a.dt;
     double sn, cs, sp, cp;
-    sincos(th, &sn, &cs);
-    sincos(psi, &sp, &cp);
+    sincos2(th, sn, cs, psi, sp, cp);
     const double t = tan(phi), cphi = cos(phi), c2 = 1.0 / (cphi * cphi), k = 1.0 + M / L2 * cp;
     dj[0] = dt * (-v * sn);
     dj[1] = dt * cs;
@@ -383,8 +382,7 @@ struct Trig {
 };
 __device__ __forceinline__ Trig stage_trig(const double* xk) {
     Trig t;
-    sincos(xk[2], &t.st, &t.ct);
-    sincos(xk[2] + xk[3], &t.sa, &t.ca);
+    sincos2(xk[2], t.st, t.ct, xk[2] + xk[3], t.sa, t.ca);
     return t;
 }
 __device__ __forceinline__ void body_geom(LArgs& a, const double* xk, int body, const Trig& tr, Geom& g) {

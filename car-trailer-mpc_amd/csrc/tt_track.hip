@@ -44,6 +44,7 @@
 #include <math.h>
 
 #include "tt_kernel.hpp"
+#include "tt_trig.hpp"
 
 namespace ttmpc {
 namespace {
@@ -307,22 +308,20 @@ struct Ctx {
 
 // sin / cos of theta, psi, phi of a stage.  Lane pairs: the two lanes evaluate theta (part 0) and phi
 // (part 1) in the same instruction stream and swap the results with one DPP quad_perm [1,0,3,2], so the
-// stage pays two sincos of latency instead of three.
+// stage pays two sincos of latency instead of three; the sincos are the library's algorithm as straight-line code
+// (tt_trig.hpp), so that they interleave.
 template <int BM>
 __device__ __forceinline__ void stage_trig(const Ctx<BM>& c, const double* x, double& sth, double& cth, double& sps,
                                            double& cps, double& sph, double& cph) {
     if (c.pair) {
         const bool p = c.part() != 0;
         double s1, c1;
-        sincos(psel(p, x[2], x[4]), &s1, &c1);
-        sincos(x[3], &sps, &cps);
+        sincos2(psel(p, x[2], x[4]), s1, c1, x[3], sps, cps);
         const double os = dppd<0xB1>(s1), oc = dppd<0xB1>(c1);
         sth = p ? os : s1; cth = p ? oc : c1;
         sph = p ? s1 : os; cph = p ? c1 : oc;
     } else {
-        sincos(x[2], &sth, &cth);
-        sincos(x[3], &sps, &cps);
-        sincos(x[4], &sph, &cph);
+        sincos3(x[2], sth, cth, x[3], sps, cps, x[4], sph, cph);
     }
 }
 
