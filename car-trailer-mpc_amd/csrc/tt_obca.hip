@@ -335,9 +335,9 @@ __device__ __forceinline__ WsView ws_view(const Ctx& c) {
 // ---------------- model: truck_trailer_model.py:8-24 ----------------
 __device__ __forceinline__ void model_f(LArgs& a, const double* x, const double* u, double* fo) {
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
-    const double t = tan(phi);
-    double sth, cth, sps, cps;
-    sincos2(th, sth, cth, psi, sps, cps);
+    double sth, cth, sps, cps, t, cphi;
+    sincos2_tancos(th, sth, cth, psi, sps, cps, phi, t, cphi);
+    (void)cphi;
     fo[0] = v * cth;
     fo[1] = v * sth;
     fo[2] = v * t / a.L1;
@@ -350,9 +350,9 @@ __device__ __forceinline__ void model_f(LArgs& a, const double* x, const double*
 __device__ __forceinline__ void model_lin(LArgs& a, const double* x, const double* y, double* dj, double* wd) {
     const double th = x[2], psi = x[3], phi = x[4], v = x[5];
     const double L1 = a.L1, L2 = a.L2, M = a.Mh, dt = a.dt;
-    double sn, cs, sp, cp;
-    sincos2(th, sn, cs, psi, sp, cp);
-    const double t = tan(phi), cphi = cos(phi), c2 = 1.0 / (cphi * cphi), k = 1.0 + M / L2 * cp;
+    double sn, cs, sp, cp, t, cphi;
+    sincos2_tancos(th, sn, cs, psi, sp, cp, phi, t, cphi);
+    const double c2 = 1.0 / (cphi * cphi), k = 1.0 + M / L2 * cp;
     dj[0] = dt * (-v * sn);
     dj[1] = dt * cs;
     dj[2] = dt * (v * cs);

@@ -12,11 +12,10 @@ namespace ttmpc {
 
 __device__ __forceinline__ double tt_bits(unsigned long long b) { return __longlong_as_double((long long)b); }
 
-// sin and cos of x, |x| < 2^30 and finite
-__device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_out) {
+// argument reduction of ax = |x| < 2^30: ax = t pi/2 + (hi + lo), three-part pi/2 (Cody-Waite with exact products);
+// q = t mod 4 (ocml __ocmlpriv_trigredsmall_f64)
+__device__ __forceinline__ void trigred_small(double ax, double& hi, double& lo, int& q) {
 #pragma clang fp contract(off)
-    const double ax = fabs(x);
-    // argument reduction: ax = t pi/2 + (hi + lo), three-part pi/2 (Cody-Waite with exact products)
     const double t = __builtin_rint(ax * tt_bits(0x3FE45F306DC9C883ull));
     const double r1 = __builtin_fma(t, tt_bits(0xBFF921FB54442D18ull), ax);
     const double r2 = __builtin_fma(t, tt_bits(0xBC91A62633145C00ull), r1);
@@ -26,10 +25,13 @@ __device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_
     const double d2 = (r1 - d1) - p;
     const double d3 = ((d1 - r2) + d2) - pe;
     const double d4 = __builtin_fma(t, tt_bits(0xB97B839A252049C0ull), d3);
-    const double hi = r2 + d4;
-    const double lo = d4 - (hi - r2);
-    const int q = (int)t & 3;
-    // sin and cos of hi + lo on [-pi/4, pi/4]
+    hi = r2 + d4;
+    lo = d4 - (hi - r2);
+    q = (int)t & 3;
+}
+// sin and cos of hi + lo on [-pi/4, pi/4] (ocml __ocmlpriv_sincosred2_f64)
+__device__ __forceinline__ void sincosred2(double hi, double lo, double& sv, double& cv) {
+#pragma clang fp contract(off)
     const double x2 = hi * hi;
     const double h = x2 * 0.5;
     const double w = 1.0 - h;
@@ -40,7 +42,7 @@ __device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_
     pc = __builtin_fma(x2, pc, tt_bits(0x3EFA01A019F4EC90ull));
     pc = __builtin_fma(x2, pc, tt_bits(0xBF56C16C16C16967ull));
     pc = __builtin_fma(x2, pc, tt_bits(0x3FA5555555555555ull));
-    const double cv = w + __builtin_fma(x4, pc, __builtin_fma(hi, -lo, wc));
+    cv = w + __builtin_fma(x4, pc, __builtin_fma(hi, -lo, wc));
     double ps = __builtin_fma(x2, tt_bits(0x3DE5E0B2F9A43BB8ull), tt_bits(0xBE5AE600B42FDFA7ull));
     ps = __builtin_fma(x2, ps, tt_bits(0x3EC71DE3796CDE01ull));
     ps = __builtin_fma(x2, ps, tt_bits(0xBF2A01A019E83E5Cull));
@@ -48,13 +50,70 @@ __device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_
     const double x3 = hi * (-x2);
     const double sa = __builtin_fma(x3, ps, lo * 0.5);
     const double sb = __builtin_fma(x2, sa, -lo);
-    const double sv = hi - __builtin_fma(x3, tt_bits(0xBFC5555555555555ull), sb);
+    sv = hi - __builtin_fma(x3, tt_bits(0xBFC5555555555555ull), sb);
+}
+// tan of hi + lo on [-pi/4, pi/4], or -1/tan when odd (ocml __ocmlpriv_tanred2_f64)
+__device__ __forceinline__ double tanred2(double x, double y, bool odd) {
+#pragma clang fp contract(off)
+    const double x2 = x * x;
+    const double s = x2 + __builtin_fma(x, y * 2.0, __builtin_fma(x, x, -x2));
+    double p = __builtin_fma(s, tt_bits(0x3EF5E089C751C08Cull), tt_bits(0xBF078809A9A29F71ull));
+    p = __builtin_fma(s, p, tt_bits(0x3F17746F90A8AAE0ull));
+    p = __builtin_fma(s, p, tt_bits(0xBEFBB44DA6FBF144ull));
+    p = __builtin_fma(s, p, tt_bits(0x3F21E634A7943ACFull));
+    p = __builtin_fma(s, p, tt_bits(0x3F2D250FDEB68FEBull));
+    p = __builtin_fma(s, p, tt_bits(0x3F437FD9B58C4D95ull));
+    p = __builtin_fma(s, p, tt_bits(0x3F57D5AF15120E2Cull));
+    p = __builtin_fma(s, p, tt_bits(0x3F6D6D93E09491DFull));
+    p = __builtin_fma(s, p, tt_bits(0x3F8226E12033784Dull));
+    p = __builtin_fma(s, p, tt_bits(0x3F9664F49AC36AE2ull));
+    p = __builtin_fma(s, p, tt_bits(0x3FABA1BA1B451C21ull));
+    p = __builtin_fma(s, p, tt_bits(0x3FC11111111185B7ull));
+    p = __builtin_fma(s, p, tt_bits(0x3FD55555555554EEull));
+    const double sp = s * p;
+    const double a = x * sp;
+    const double ae = __builtin_fma(x, sp, -a);
+    const double b = x + a;
+    const double be = a - (b - x);
+    const double cc = (y + ae) + be;
+    const double th = b + cc;
+    const double tl = cc - (th - b);
+    const double r0 = __builtin_amdgcn_rcp(th);
+    const double r1 = __builtin_fma(__builtin_fma(-th, r0, 1.0), r0, r0);
+    const double r = __builtin_fma(__builtin_fma(-th, r1, 1.0), r1, r1);
+    const double m = th * r;
+    const double e = __builtin_fma(r, tl, __builtin_fma(r, th, -m));
+    const double u = m + e;
+    const double ue = e - (u - m);
+    const double v = 1.0 - u;
+    const double ve = (((1.0 - v) - u) - ue);
+    const double it = r + r * (v + ve);
+    return odd ? -it : th;
+}
+__device__ __forceinline__ unsigned long long tt_u(double v) { return (unsigned long long)__double_as_longlong(v); }
+constexpr unsigned long long kSign = 0x8000000000000000ull;
+
+// sin and cos of x, |x| < 2^30 and finite (ocml __ocml_sincos_f64)
+__device__ __forceinline__ void sincos_small(double x, double& s_out, double& c_out) {
+    double hi, lo, sv, cv;
+    int q;
+    trigred_small(fabs(x), hi, lo, q);
+    sincosred2(hi, lo, sv, cv);
     // quadrant: sin = +-(sin | cos), cos = +-(cos | -sin); the sine also takes the sign of x
     const bool even = (q & 1) == 0;
-    const unsigned long long neg = q > 1 ? 0x8000000000000000ull : 0ull;
-    const unsigned long long sx = (unsigned long long)__double_as_longlong(x) & 0x8000000000000000ull;
-    s_out = tt_bits((unsigned long long)__double_as_longlong(even ? sv : cv) ^ sx ^ neg);
-    c_out = tt_bits((unsigned long long)__double_as_longlong(even ? cv : -sv) ^ neg);
+    const unsigned long long neg = q > 1 ? kSign : 0ull;
+    s_out = tt_bits(tt_u(even ? sv : cv) ^ (tt_u(x) & kSign) ^ neg);
+    c_out = tt_bits(tt_u(even ? cv : -sv) ^ neg);
+}
+// tan and cos of x, |x| < 2^30 and finite, one reduction for both (ocml __ocml_tan_f64, __ocml_cos_f64)
+__device__ __forceinline__ void tancos_small(double x, double& t_out, double& c_out) {
+    double hi, lo, sv, cv;
+    int q;
+    trigred_small(fabs(x), hi, lo, q);
+    sincosred2(hi, lo, sv, cv);
+    const bool even = (q & 1) == 0;
+    c_out = tt_bits(tt_u(even ? cv : -sv) ^ (q > 1 ? kSign : 0ull));
+    t_out = tt_bits(tt_u(tanred2(hi, lo, !even)) ^ (tt_u(x) & kSign));
 }
 
 // true when the fast path is exact for every lane of the wave (wave-uniform)
@@ -69,6 +128,20 @@ __device__ __forceinline__ void sincos2(double a, double& sa, double& ca, double
     } else {
         sincos(a, &sa, &ca);
         sincos(b, &sb, &cb);
+    }
+}
+// sin / cos of a and b, tan and cos of c (the OBCA model's theta, psi, phi)
+__device__ __forceinline__ void sincos2_tancos(double a, double& sa, double& ca, double b, double& sb, double& cb, double c,
+                                               double& tc, double& cc) {
+    if (sincos_small_ok(sincos_arg_ok(a) && sincos_arg_ok(b) && sincos_arg_ok(c))) {
+        sincos_small(a, sa, ca);
+        sincos_small(b, sb, cb);
+        tancos_small(c, tc, cc);
+    } else {
+        sincos(a, &sa, &ca);
+        sincos(b, &sb, &cb);
+        tc = tan(c);
+        cc = cos(c);
     }
 }
 __device__ __forceinline__ void sincos3(double a, double& sa, double& ca, double b, double& sb, double& cb, double c,

@@ -1,4 +1,4 @@
-// Bitwise check of tt_trig.hpp's straight-line sincos against the device library's sincos on gfx950 (diagnostic, GPU
+// Bitwise check of tt_trig.hpp's straight-line sincos and tan / cos against the device library's on gfx950 (diagnostic, GPU
 // box): random arguments over several magnitude ranges, arguments next to multiples of pi/4, and special values.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I car-trailer-mpc_amd/csrc tools/trig_check.hip -o tools/trig_check
 #include <hip/hip_runtime.h>
@@ -32,11 +32,16 @@ __global__ void check(unsigned long long n, unsigned long long* bad, double* fir
     } else {                                                   // tiny and subnormal magnitudes
         x = ldexp(2.0 * u - 1.0, -(int)((r >> 40) % 1070));
     }
-    double s0, c0, s1, c1;
+    double s0, c0, s1, c1, t1, c2;
     sincos(x, &s0, &c0);
     ttmpc::sincos_small(x, s1, c1);
+    const double t0 = tan(x), c3 = cos(x);
+    ttmpc::tancos_small(x, t1, c2);
     if (__double_as_longlong(s0) != __double_as_longlong(s1) || __double_as_longlong(c0) != __double_as_longlong(c1)) {
         if (atomicAdd(bad, 1ull) == 0ull) { first[0] = x; first[1] = s0; first[2] = s1; first[3] = c0; first[4] = c1; }
+    }
+    if (__double_as_longlong(t0) != __double_as_longlong(t1) || __double_as_longlong(c3) != __double_as_longlong(c2)) {
+        if (atomicAdd(bad + 1, 1ull) == 0ull) { first[5] = x; first[6] = t0; first[7] = t1; first[8] = c3; first[9] = c2; }
     }
 }
 
@@ -44,17 +49,18 @@ int main(int argc, char** argv) {
     const unsigned long long n = argc > 1 ? strtoull(argv[1], nullptr, 10) : (1ull << 28);
     unsigned long long* bad;
     double* first;
-    if (hipMalloc(&bad, 8) != hipSuccess || hipMalloc(&first, 5 * 8) != hipSuccess) return 2;
-    hipMemset(bad, 0, 8);
-    hipMemset(first, 0, 40);
+    if (hipMalloc(&bad, 16) != hipSuccess || hipMalloc(&first, 10 * 8) != hipSuccess) return 2;
+    if (hipMemset(bad, 0, 16) != hipSuccess || hipMemset(first, 0, 80) != hipSuccess) return 2;
     const unsigned blocks = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(check, dim3(blocks), dim3(256), 0, 0, n, bad, first);
     if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 2; }
-    unsigned long long hb = 0;
-    double hf[5];
-    hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost);
-    hipMemcpy(hf, first, 40, hipMemcpyDeviceToHost);
-    printf("sincos_small vs library sincos: %llu arguments, %llu bitwise mismatches\n", n, hb);
-    if (hb) printf("first: x=%.17g sin %.17g vs %.17g, cos %.17g vs %.17g\n", hf[0], hf[1], hf[2], hf[3], hf[4]);
-    return hb ? 1 : 0;
+    unsigned long long hb[2] = {0, 0};
+    double hf[10];
+    if (hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost) != hipSuccess || hipMemcpy(hf, first, 80, hipMemcpyDeviceToHost) != hipSuccess)
+        return 2;
+    printf("sincos_small vs library sincos: %llu arguments, %llu bitwise mismatches\n", n, hb[0]);
+    printf("tancos_small vs library tan, cos: %llu arguments, %llu bitwise mismatches\n", n, hb[1]);
+    if (hb[0]) printf("first: x=%.17g sin %.17g vs %.17g, cos %.17g vs %.17g\n", hf[0], hf[1], hf[2], hf[3], hf[4]);
+    if (hb[1]) printf("first: x=%.17g tan %.17g vs %.17g, cos %.17g vs %.17g\n", hf[5], hf[6], hf[7], hf[8], hf[9]);
+    return hb[0] || hb[1] ? 1 : 0;
 }
