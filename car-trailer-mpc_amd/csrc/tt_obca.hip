@@ -3533,9 +3533,11 @@ __device__ __forceinline__ void nres_block(const Ctx& c, const LShared& sh, cons
 }
 
 // chunks [c0, c1) of a block pass: thread t runs block f = ci T + t of the flat block index (one function per pass, so
-// that neither block part's registers constrain the other's)
+// that neither block part's registers constrain the other's).  The helpers' write-through instances (SC1) are inlined
+// into the helper path of the kernel entry, which saves no registers: as calls, every chunk paid the callee-saved
+// register saves and restores of a ~270-register frame.
 template <bool SC1>
-__device__ __noinline__ void nres_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+__device__ __forceinline__ void nres_chunks_body(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
     const WsView vw = ws_view(c);
     const int nblk = c.nbk * c.NP, np = c.NP;
     for (int ci = c0; ci < c1; ++ci) {
@@ -3546,7 +3548,7 @@ __device__ __noinline__ void nres_chunks(const Ctx& c, const LShared& sh, ChunkP
     }
 }
 template <bool SC1>
-__device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+__device__ __forceinline__ void factor_chunks_body(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
     const WsView vw = ws_view(c);
     const int nblk = c.nbk * c.NP, np = c.NP;
     for (int ci = c0; ci < c1; ++ci) {
@@ -3557,7 +3559,7 @@ __device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, Chun
     }
 }
 template <bool RS_, bool SC1>
-__device__ __noinline__ void update_chunks(const Ctx& c, ChunkPass p, int c0, int c1) {
+__device__ __forceinline__ void update_chunks_body(const Ctx& c, ChunkPass p, int c0, int c1) {
     const WsView vw = ws_view(c);
     const int nblk = c.nbk * c.NP, np = c.NP;
     for (int ci = c0; ci < c1; ++ci) {
@@ -3567,15 +3569,34 @@ __device__ __noinline__ void update_chunks(const Ctx& c, ChunkPass p, int c0, in
         update_block<RS_, SC1>(c, vw, j, f - j * np, p.mu, p.dw, p.tau, p.buf);
     }
 }
+__device__ __noinline__ void nres_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+    nres_chunks_body<false>(c, sh, p, c0, c1);
+}
+__device__ __noinline__ void factor_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+    factor_chunks_body<false>(c, sh, p, c0, c1);
+}
+template <bool RS_>
+__device__ __noinline__ void update_chunks(const Ctx& c, ChunkPass p, int c0, int c1) {
+    update_chunks_body<RS_, false>(c, p, c0, c1);
+}
+// the instance's own chunks (plain stores, calls)
 __device__ void do_chunks(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1, bool helper) {
-    if (p.pass == PASS_NRES) helper ? nres_chunks<true>(c, sh, p, c0, c1) : nres_chunks<false>(c, sh, p, c0, c1);
-    else if (p.pass == PASS_FACTOR) helper ? factor_chunks<true>(c, sh, p, c0, c1) : factor_chunks<false>(c, sh, p, c0, c1);
-    else if (sh.R) helper ? update_chunks<true, true>(c, p, c0, c1) : update_chunks<true, false>(c, p, c0, c1);
-    else helper ? update_chunks<false, true>(c, p, c0, c1) : update_chunks<false, false>(c, p, c0, c1);
+    (void)helper;
+    if (p.pass == PASS_NRES) nres_chunks(c, sh, p, c0, c1);
+    else if (p.pass == PASS_FACTOR) factor_chunks(c, sh, p, c0, c1);
+    else if (sh.R) update_chunks<true>(c, p, c0, c1);
+    else update_chunks<false>(c, p, c0, c1);
+}
+// a helper's chunk (write-through stores, inlined)
+__device__ __forceinline__ void do_chunks_helper(const Ctx& c, const LShared& sh, ChunkPass p, int c0, int c1) {
+    if (p.pass == PASS_NRES) nres_chunks_body<true>(c, sh, p, c0, c1);
+    else if (p.pass == PASS_FACTOR) factor_chunks_body<true>(c, sh, p, c0, c1);
+    else if (sh.R) update_chunks_body<true, true>(c, p, c0, c1);
+    else update_chunks_body<false, true>(c, p, c0, c1);
 }
 
 // a helper workgroup: serve open chunks of any instance until every instance has finished
-__device__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
+__device__ __forceinline__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
     const int B = a.B, lane = (int)threadIdx.x;
     gu64* hdr = board_line(a, B);
     if (lane == 0) {
@@ -3642,7 +3663,7 @@ __device__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
         p.mu = sh.hp_mu; p.dw = sh.hp_dw; p.tau = sh.hp_tau;
         const int pk = sh.hp_pk;
         p.pass = pk & 15; p.buf = (pk >> 4) & 15; p.prep = (pk >> 8) & 15; p.mode = (pk >> 12) & 15;
-        do_chunks(cw, sh, p, ci, ci + 1, true);  // write-through stores: no release (L2 write-back) needed
+        do_chunks_helper(cw, sh, p, ci, ci + 1);  // write-through stores: no release (L2 write-back) needed
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (lane == 0) add_rlx(board_line(a, b) + 1, 1);
