@@ -814,7 +814,7 @@ TRACK_PMC_SOURCE = "profiles/r05/SOURCE.txt, profiles/r05/session_j/SOURCE.txt"
 # committed PMC passes of obca_kernel (tools/obca_pmc.sh, one short probe per config on the shipped kernel): HBM bytes per
 # instance-iteration, scaled by a launch's summed IPM iterations for roofline.traffic of the OBCA lines -- an estimate
 # (the probe's iteration mix is not the full launch's), flagged as such in the line (traffic_estimated)
-OBCA_PMC = {"c4": "profiles/r05/final/pmc_obca_c4", "c4all": "profiles/r05/final/pmc_obca_c4all", "cobs": "profiles/r05/final/pmc_obca_cobs"}
+OBCA_PMC = {"c4": "profiles/r05/final3/pmc_obca_c4", "c4all": "profiles/r05/final3/pmc_obca_c4all", "cobs": "profiles/r05/final3/pmc_obca_cobs"}
 
 
 def obca_traffic(cfg, iters_sum):
