@@ -807,8 +807,8 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 
 # rocprofv3 PMC passes (tools/hbm_passes.sh) that the default C2 / C3 lines quote as roofline.traffic: the kernel
 # the bench runs; re-profile after a tracking-kernel change
-TRACK_PMC = {"c2": "profiles/r05/session_j/pmc_c2", "c3": "profiles/r05/session_b/pmc_c3"}
-TRACK_PMC_SOURCE = "profiles/r05/SOURCE.txt, profiles/r05/session_j/SOURCE.txt"
+TRACK_PMC = {"c2": "profiles/r05/final3/pmc_track_c2", "c3": "profiles/r05/final3/pmc_track_c3"}
+TRACK_PMC_SOURCE = "profiles/r05/final3/SOURCE.txt"
 
 
 # committed PMC passes of obca_kernel (tools/obca_pmc.sh, one short probe per config on the shipped kernel): HBM bytes per
