@@ -38,6 +38,8 @@ struct Handle {
     unsigned long long* obca_stamps = nullptr;  // diagnostics: per-phase clocks (ttx_obca_set_stamps)
     unsigned long long* d_board = nullptr;      // OBCA helper-workgroup board, (ocap + 1) lines
     int nhelp = -1;                             // OBCA helper workgroups per launch (-1: one per CU; ttx_obca_set_helpers)
+    unsigned long long spin_ticks = 0;          // hand-off spin limit (0: 5 s) and forced-timeout instance (-1: none),
+    int fail_b = -1;                            //   ttx_obca_set_handoff_debug
 };
 
 thread_local std::string g_err;
@@ -465,6 +467,8 @@ int tt_obca_solve_batch_iterate_device(void* handle, int B, const double* d_x0, 
     }
     a.board = h->d_board;
     a.nhelp = h->nhelp;
+    a.spin_ticks = h->spin_ticks;
+    a.fail_b = h->fail_b;
     e = hipMemsetAsync(h->d_board, 0, ((size_t)B + 1) * ttmpc::kObcaBoardStride * 8, s);
     if (e != hipSuccess) return hip_fail(h, e, "hipMemsetAsync (OBCA board)");
     e = ttmpc::launch_obca(a, s);
@@ -559,6 +563,18 @@ int ttx_obca_set_helpers(void* handle, int n) {
     h->nhelp = n < 0 ? -1 : n;
     return 0;
 }
+
+/* diagnostics only: the helper hand-off's spin limit in microseconds (0: the default 5 s) and one instance whose
+ * hand-offs never complete (-1: none), so that it ends with TT_HANDOFF_TIMEOUT while its neighbours solve normally
+ * (tests/test_gpu_obca.py::test_helper_handoff_timeout_is_reported_and_isolated). */
+int ttx_obca_set_handoff_debug(void* handle, long long spin_us, int fail_b) {
+    Handle* h = static_cast<Handle*>(handle);
+    if (!h || spin_us < 0) return -EINVAL;
+    h->spin_ticks = (unsigned long long)spin_us * 100ull;  // s_memrealtime: 100 MHz
+    h->fail_b = fail_b < 0 ? -1 : fail_b;
+    return 0;
+}
+static_assert(TT_HANDOFF_TIMEOUT == 6, "tt_obca.hip kStatusHandoffTimeout");
 
 int tt_plan_batch(void* handle, int B, const double* x0, const double* xgoal, const double* z_guess, double* x_out,
                   double* u_out, int* status, int* iters) {

@@ -90,8 +90,17 @@ struct ObcaArgs {
     // passes of the instances still solving; board: (B + 1) x kObcaBoardStride words, zeroed before every launch
     unsigned long long* board;
     int nhelp;
+    // hand-off diagnostics (ttx_obca_set_handoff_debug): spin limit of an instance waiting for helper chunks in
+    // s_memrealtime ticks (0: kSpinTicks, 5 s), and one instance whose hand-offs never complete (-1: none), which
+    // forces the TT_HANDOFF_TIMEOUT path (tests/test_gpu_obca.py)
+    unsigned long long spin_ticks;
+    int fail_b;
 };
 constexpr int kObcaBoardStride = 16;  // 128-B line per instance (+ one header line)
+// claim word of an instance's board line: epoch << 40 | chunks << 20 | next chunk (20 + 20 bits: a pass of
+// N = 100000 at M = 16 has 12,501 chunks, and the claim counter overshoots by at most one per claiming workgroup)
+constexpr int kClaimChunkShift = 20;
+constexpr unsigned long long kClaimFieldMask = (1ull << kClaimChunkShift) - 1ull;
 // phase clocks, then event counters (diagnostics, tools/obca_stamps.py / obca_tail.py): factorisations (inertia
 // attempts incl. the SOC and pretend-singular refactorisations), restoration-phase iterations, soft-restoration steps,
 // refinement corrections, second-order corrections, pretend-singular re-solves, line-search trial points

@@ -952,13 +952,18 @@ __device__ __forceinline__ void block_refactor(const Ctx& c, const LShared& sh, 
 // A chunk's arithmetic does not depend on which workgroup runs it, so the results are bitwise those of the instance
 // running every chunk itself (the local path, taken while no helper has started: the whole busy phase of a large batch).
 // Board (HBM, zeroed before every launch), one 128-B line per instance:
-//   [0] claim = epoch << 40 | chunks << 32 | next chunk (odd epoch: open), [1] done = epoch << 32 | chunks done by
+//   [0] claim = epoch << 40 | chunks << 20 | next chunk (odd epoch: open; kClaimChunkShift), [1] done = epoch << 32 | chunks done by
 //   helpers, [2..6] mu dw tau zeta dc (bits), [7] pass | buf << 4 | prep << 8 | mode << 12 | R << 16 | lsq << 20;
 // header line (index B): [0] instances finished, [1] helpers started, [2] instances started.
 // Hand-off (agent scope; MI355X_MICROARCH.md, inter-workgroup visibility): the instance's waves drain their stores, one
 // lane releases (L2 write-back) and stores the claim word; a helper's claim is followed by one acquire before any load
 // of the instance's data; a helper's chunk ends with drained stores, a release and the done add; the instance acquires
-// once the done count is complete.  Every spin is bounded.
+// once the done count is complete.  Every spin is bounded: an instance that waits longer than the spin limit for its
+// helpers' chunks (kSpinTicks, 5 s) sets hfail, runs every later pass of the iteration itself and ends the solve with
+// status TT_HANDOFF_TIMEOUT (6); helpers leave after 12 spin limits (60 s) of wall clock whatever the board says.
+// Memory model: a helper's chunk stores are agent-scope write-through (sc1) stores drained by s_waitcnt vmcnt(0) in
+// every wave before the workgroup barrier, and lane 0 then publishes with a RELEASE done add; the instance's acquire
+// after the done count pairs with that release.
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 enum { PASS_FACTOR = 1, PASS_NRES = 2, PASS_UPDATE = 4 };
 struct ChunkPass {
@@ -980,6 +985,10 @@ __device__ __forceinline__ unsigned long long add_rlx(gu64* p, unsigned long lon
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 __device__ __forceinline__ double bitsd(unsigned long long v) { return __longlong_as_double((long long)v); }
 constexpr unsigned long long kSpinTicks = 500000000ull;  // 5 s of the 100 MHz s_memrealtime clock
+constexpr int kStatusHandoffTimeout = 6;  // TT_HANDOFF_TIMEOUT (include/ttmpc.h)
+#ifndef OBCA_HELPER_RELEASE
+#define OBCA_HELPER_RELEASE 1
+#endif
 
 // one block pass of this instance (every thread of its workgroup), ending with a workgroup barrier
 __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
@@ -987,9 +996,10 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
     const int nch = (c.nbk * c.NP + T - 1) / T;
     if (threadIdx.x == 0) {
         // shared mode once there is a helper for every instance still solving (before that the hand-off costs the
-        // instances more than the few helpers return: profiles/r05/helpers/stamps_h.txt)
+        // instances more than the few helpers return: profiles/r05/helpers/stamps_h.txt); never again after a hand-off
+        // timed out (the solve ends with TT_HANDOFF_TIMEOUT at the next convergence test)
         int on = 0;
-        if (a.board && a.nhelp > 0) {
+        if (a.board && a.nhelp > 0 && !sh.hfail) {
             gu64* hdr = board_line(a, a.B);
             const unsigned long long fin = ld_rlx(hdr), hlp = ld_rlx(hdr + 1), started = ld_rlx(hdr + 2);
             on = hlp > 0 && hlp + fin >= started;
@@ -1016,11 +1026,13 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
         st_rlx(ln + 1, ep << 32);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st_rlx(ln, ep << 40 | (unsigned long long)nch << 32);
+        st_rlx(ln, ep << 40 | (unsigned long long)nch << kClaimChunkShift);
     }
+    // the debug instance (ObcaArgs::fail_b) leaves every chunk to the helpers and waits for a count that never comes
+    const bool forced = c.b == a.fail_b;
     int own = 0;
     for (;;) {
-        if (threadIdx.x == 0) sh.hcur = (int)(unsigned)(add_rlx(ln, 1) & 0xffffffffull);
+        if (threadIdx.x == 0) sh.hcur = forced ? nch : (int)(add_rlx(ln, 1) & kClaimFieldMask);
         __syncthreads();
         const int ci = sh.hcur;
         __syncthreads();
@@ -1029,9 +1041,10 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
         ++own;
     }
     if (threadIdx.x == 0) {
-        const unsigned long long want = ep << 32 | (unsigned long long)(nch - own), t0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long want = forced ? ~0ull : ep << 32 | (unsigned long long)(nch - own);
+        const unsigned long long lim = a.spin_ticks ? a.spin_ticks : kSpinTicks, t0 = __builtin_amdgcn_s_memrealtime();
         while (ld_rlx(ln + 1) != want) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) { sh.hfail = 1; break; }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > lim) { sh.hfail = 1; break; }
             __builtin_amdgcn_s_sleep(2);
         }
         st_rlx(ln, (ep + 1ull) << 40);  // closed
@@ -3619,14 +3632,17 @@ __device__ __forceinline__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
             if (!ex) {
                 const int b = (pos + lane) % B;
                 const unsigned long long w = lane < B ? ld_rlx(board_line(a, b)) : 0ull;
-                const bool open = ((w >> 40) & 1ull) && (unsigned)w < (unsigned)((w >> 32) & 0xffull);
+                auto claimable = [](unsigned long long v) {  // open pass, next chunk below the chunk count
+                    return ((v >> 40) & 1ull) && (v & kClaimFieldMask) < ((v >> kClaimChunkShift) & kClaimFieldMask);
+                };
+                const bool open = claimable(w);
                 const unsigned long long m = __ballot(open);
                 if (m) {
                     const int l = __ffsll((long long)m) - 1;
                     int cb = -1, cc = -1;
                     if (lane == l) {
                         const unsigned long long o = add_rlx(board_line(a, b), 1);
-                        if (((o >> 40) & 1ull) && (unsigned)o < (unsigned)((o >> 32) & 0xffull)) { cb = b; cc = (int)(unsigned)o; }
+                        if (claimable(o)) { cb = b; cc = (int)(o & kClaimFieldMask); }
                     }
                     gb = __builtin_amdgcn_readlane(cb, l);
                     gc = __builtin_amdgcn_readlane(cc, l);
@@ -3663,10 +3679,17 @@ __device__ __forceinline__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
         p.mu = sh.hp_mu; p.dw = sh.hp_dw; p.tau = sh.hp_tau;
         const int pk = sh.hp_pk;
         p.pass = pk & 15; p.buf = (pk >> 4) & 15; p.prep = (pk >> 8) & 15; p.mode = (pk >> 12) & 15;
-        do_chunks_helper(cw, sh, p, ci, ci + 1);  // write-through stores: no release (L2 write-back) needed
+        do_chunks_helper(cw, sh, p, ci, ci + 1);  // write-through (sc1) stores
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (lane == 0) add_rlx(board_line(a, b) + 1, 1);
+        // the done count publishes the chunk: a release add (advisor r5), so the instance's acquire synchronizes with
+        // it under the HIP memory model and not only by the sc1 + vmcnt(0) drain above (OBCA_HELPER_RELEASE 0: relaxed)
+        if (lane == 0) {
+            if constexpr (OBCA_HELPER_RELEASE)
+                __hip_atomic_fetch_add(board_line(a, b) + 1, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                add_rlx(board_line(a, b) + 1, 1);
+        }
     }
 }
 
@@ -4650,7 +4673,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
                 phase_lin(cs, sh, red);
                 stamp(sh, ston, OPH_LIN);
                 double dinf = red[0], pinf = red[1], c0 = red[2];
-                if (!isfinite(dinf) || !isfinite(pinf) || sh.hfail) { status = 4; done = true; break; }
+                if (sh.hfail) { status = kStatusHandoffTimeout; done = true; break; }
+                if (!isfinite(dinf) || !isfinite(pinf)) { status = 4; done = true; break; }
                 const double nbd = n_bounds + (R ? 2.0 * n_rows : 0.0);
                 double sd = fmax(smax, red[3] / (n_rows + nbd)) / smax, sc = fmax(smax, red[4] / nbd) / smax;
                 E0 = fmax(fmax(dinf / sd, pinf), c0 / sc);
@@ -5005,7 +5029,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         add_rlx(board_line(a, a.B), 1);
     }
     if (tid == 0) {
-        a.status[c.b] = status;
+        // a hand-off timeout overrides whatever the iteration that met it concluded (its passes ran on partial chunks)
+        a.status[c.b] = sh.hfail ? kStatusHandoffTimeout : status;
         if (a.iters) a.iters[c.b] = iter;
         if (a.kkt) a.kkt[c.b] = E0;
         if (ston) {

@@ -7,6 +7,15 @@
 // test); otherwise they call the library.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_version.h>
+
+// The restatement is checked bit for bit against THIS ROCm's ocml (tools/trig_check.hip, run by
+// tests/test_gpu_trig.py on every GPU test session).  Another ROCm may change ocml's constants or operation order, and
+// the kernels would drift silently from the library and from the lockstep parity the OBCA tests rely on: refuse to
+// build until trig_check has been re-run there (then extend this test, or build with -DTT_TRIG_UNCHECKED_ROCM).
+#if !(HIP_VERSION_MAJOR == 7 && HIP_VERSION_MINOR == 2) && !defined(TT_TRIG_UNCHECKED_ROCM)
+#error "tt_trig.hpp restates ROCm 7.2's ocml sin/cos/tan: re-run tools/trig_check on this ROCm before building"
+#endif
 
 namespace ttmpc {
 

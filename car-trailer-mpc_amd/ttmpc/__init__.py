@@ -3,7 +3,8 @@
 Reference: Avan1ko/car-trailer-mpc python-files/{mpc_control, mpc_control_nmpc, mpc_control_fuzzy,
 trajectory_planning, truck_trailer_model}.py.  All solves run in libttmpc.so on a gfx950 GPU.
 """
-from ._lib import (STATUS_NAMES, TT_ACCEPTABLE, TT_CONVERGED, TT_INFEASIBLE, TT_MAX_ITER, TT_NONFINITE, TT_STEP_FAILED,  # noqa: F401
+from ._lib import (STATUS_NAMES, TT_ACCEPTABLE, TT_CONVERGED, TT_HANDOFF_TIMEOUT, TT_INFEASIBLE, TT_MAX_ITER,  # noqa: F401
+                   TT_NONFINITE, TT_STEP_FAILED,
                    TT_VARIANT_FUZZY, TT_VARIANT_NMPC, TT_VARIANT_OBCA_PLAN, TT_VARIANT_TRACK, TT_VARIANT_TRACK_OBCA,
                    BatchSolver, ObcaSolver, TTError, lib, obca_n)
 from .mpc_control import MPCTrackingControl  # noqa: F401

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import warnings
 from pathlib import Path
 
 import numpy as np
@@ -16,9 +17,10 @@ LIB_PATH = Path(__file__).resolve().parent / "libttmpc.so"
 if os.environ.get("TTMPC_LIB"):
     LIB_PATH = Path(os.environ["TTMPC_LIB"]).resolve()
 
-TT_CONVERGED, TT_ACCEPTABLE, TT_MAX_ITER, TT_INFEASIBLE, TT_NONFINITE, TT_STEP_FAILED = range(6)
+TT_CONVERGED, TT_ACCEPTABLE, TT_MAX_ITER, TT_INFEASIBLE, TT_NONFINITE, TT_STEP_FAILED, TT_HANDOFF_TIMEOUT = range(7)
 TT_VARIANT_TRACK, TT_VARIANT_TRACK_OBCA, TT_VARIANT_NMPC, TT_VARIANT_FUZZY, TT_VARIANT_OBCA_PLAN = range(5)
-STATUS_NAMES = {0: "converged", 1: "acceptable", 2: "max_iter", 3: "infeasible", 4: "non-finite", 5: "step_failed"}
+STATUS_NAMES = {0: "converged", 1: "acceptable", 2: "max_iter", 3: "infeasible", 4: "non-finite", 5: "step_failed",
+                6: "handoff_timeout"}
 
 
 class TTConfig(C.Structure):
@@ -121,6 +123,7 @@ def lib():
            "tt_policy_plant_noise_device": [i, C.POINTER(TTPlant), i, vp, vp, ll, vp, vp, vp, vp, vp, vp, vp, vp],
            "tt_fuzzy_weights_device": [i, i, vp, vp, vp, vp]}
     sim["ttx_obca_set_helpers"] = [C.c_void_p, i]  # diagnostics (not in include/ttmpc.h)
+    sim["ttx_obca_set_handoff_debug"] = [C.c_void_p, ll, i]
     for name, args in sim.items():
         if os.environ.get("TTMPC_LIB") and not hasattr(L, name):
             continue  # A/B diagnostics against an older build
@@ -243,6 +246,15 @@ def obca_n(N: int, M: int) -> int:
     return N * (8 + 16 * M) + 6 + 16 * M
 
 
+def _warn_handoff(st):
+    """A helper hand-off timeout is a failure of the launch, not of the NLP: plan() (which by the reference's contract
+    never signals failure, trajectory_optimization.py:326-331) still returns, but not silently."""
+    bad = np.flatnonzero(np.asarray(st) == TT_HANDOFF_TIMEOUT)
+    if bad.size:
+        warnings.warn(f"OBCA helper hand-off timed out for {bad.size} instance(s) {bad[:8].tolist()}: their outputs are "
+                      "partial iterates (status TT_HANDOFF_TIMEOUT)", RuntimeWarning, stacklevel=3)
+
+
 class ObcaSolver:
     """Handle for the OBCA NLPs: TT_VARIANT_OBCA_PLAN (TrajectoryOptimization) or TT_VARIANT_TRACK_OBCA
     (MPCTrackingControlObs).  obstacles: (M,4) array of (cx, cy, w, h)."""
@@ -302,11 +314,13 @@ class ObcaSolver:
                                                      it.ctypes.data_as(_ip), _ptr(kk), _ptr(I))
             if rc != 0:
                 self._err(rc, "tt_obca_solve_batch_iterate")
+            _warn_handoff(st)
             return X, U, Z, st, it, kk, I
         rc = self._L.tt_obca_solve_batch(self._h, B, _ptr(x0), _ptr(xg), _ptr(xr), _ptr(ur), _ptr(zg), _ptr(X),
                                          _ptr(U), _ptr(Z), st.ctypes.data_as(_ip), it.ctypes.data_as(_ip), _ptr(kk))
         if rc != 0:
             self._err(rc, "tt_obca_solve_batch")
+        _warn_handoff(st)
         return X, U, Z, st, it, kk
 
     def set_helpers(self, n):
@@ -314,6 +328,13 @@ class ObcaSolver:
         passes of the instances still solving run on the idle CUs; the results are bitwise the same either way."""
         if hasattr(self._L, "ttx_obca_set_helpers"):
             self._L.ttx_obca_set_helpers(self._h, int(n))
+
+    def set_handoff_debug(self, spin_us=0, fail_b=-1):
+        """Diagnostics: the helper hand-off's spin limit in microseconds (0: the default 5 s) and one instance whose
+        hand-offs never complete (-1: none); that instance then ends with TT_HANDOFF_TIMEOUT (6)."""
+        rc = self._L.ttx_obca_set_handoff_debug(self._h, int(spin_us), int(fail_b))
+        if rc != 0:
+            self._err(rc, "ttx_obca_set_handoff_debug")
 
     def solve_device(self, B, x0, x_goal, xref, uref, z_guess, x_out, u_out, z_out, status, iters=0, kkt=0, stream=0):
         """Device pointers (ints), enqueued on ``stream``."""

@@ -29,7 +29,11 @@
  *    -ENOMEM, -EIO HIP error, -ENOSYS not built); text from tt_last_error(handle).
  *  - per-instance status: TT_CONVERGED (IPOPT tol), TT_ACCEPTABLE (acceptable_tol x acc_iter),
  *    TT_MAX_ITER, TT_INFEASIBLE (x_init outside the state box -> x_0 = x_init unsatisfiable),
- *    TT_NONFINITE, TT_STEP_FAILED (inertia correction exceeded IPOPT's max_hessian_perturbation 1e20).  CasADi's stats()['success'] == (status <= TT_ACCEPTABLE).
+ *    TT_NONFINITE, TT_STEP_FAILED (inertia correction exceeded IPOPT's max_hessian_perturbation 1e20),
+ *    TT_HANDOFF_TIMEOUT (OBCA only: an instance waited longer than the spin limit, 5 s, for the helper workgroups
+ *    that run chunks of its block passes; a synchronisation failure of the launch, not a numerical one -- the
+ *    outputs are the last iterate, possibly partial; INTEGRATION.md "Helper workgroups").
+ *    CasADi's stats()['success'] == (status <= TT_ACCEPTABLE).
  *  - a handle is not thread-safe (like the reference objects, which mutate _last_solution); use
  *    one handle per host thread.  Host-pointer calls are synchronous; device-pointer calls are
  *    asynchronous on the given HIP stream.
@@ -43,7 +47,8 @@ extern "C" {
 #endif
 
 enum { TT_CONVERGED = 0, TT_ACCEPTABLE = 1, TT_MAX_ITER = 2, TT_INFEASIBLE = 3, TT_NONFINITE = 4,
-       TT_STEP_FAILED = 5 /* IPOPT Error_In_Step_Computation: delta_w > max_hessian_perturbation (1e20) */ };
+       TT_STEP_FAILED = 5 /* IPOPT Error_In_Step_Computation: delta_w > max_hessian_perturbation (1e20) */,
+       TT_HANDOFF_TIMEOUT = 6 /* OBCA helper hand-off timed out (no IPOPT counterpart; see above) */ };
 
 enum {
     TT_VARIANT_TRACK = 0,      /* MPCTrackingControl       mpc_control.py       (max_iter 5000, tol 1e-8)  */

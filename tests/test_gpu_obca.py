@@ -190,6 +190,54 @@ def test_helper_workgroups_are_bitwise_neutral():
             assert np.array_equal(u, v)
 
 
+def test_helper_handoff_timeout_is_reported_and_isolated():
+    """A hand-off that never completes (advisor r5): with ttx_obca_set_handoff_debug one instance
+    leaves all its chunks to the helpers and waits for a done count that never comes, under a 2 ms spin limit.  It must
+    end with its own status TT_HANDOFF_TIMEOUT (6) -- not TT_NONFINITE -- and a RuntimeWarning, and every other instance
+    of the launch must be bit for bit what it is without the debug switch (the 16 MPC+OBCA windows, max_iter 400)."""
+    import ttmpc
+    from ttmpc import scenarios as sc
+    g = np.load(GOLDEN / "reference_numpy.npz")
+    x0w, xr, ur = sc.mpc_obs_batch(g["state_traj"], g["input_traj"], 16, 50, seed=0)
+    mk = lambda: _solver(50, g["obstacles"], ttmpc.TT_VARIANT_TRACK_OBCA, dict(P6, dt=0.05),  # noqa: E731
+                         (sc.XLB, sc.XUB, sc.ULB, sc.UUB), max_iter=400)
+    ref = mk().solve(x0w, xref=xr, uref=ur)
+    s = mk()
+    s.set_handoff_debug(spin_us=2000, fail_b=5)
+    with pytest.warns(RuntimeWarning, match="hand-off timed out"):
+        out = s.solve(x0w, xref=xr, uref=ur)
+    st = out[3]
+    assert st[5] == ttmpc.TT_HANDOFF_TIMEOUT, st
+    keep = np.arange(16) != 5
+    for u, v in zip(out, ref):
+        assert np.array_equal(u[keep], v[keep])
+    # the switch is per handle: back to the defaults, the same handle reproduces the reference run bit for bit
+    s.set_handoff_debug()
+    for u, v in zip(s.solve(x0w, xref=xr, uref=ur), ref):
+        assert np.array_equal(u, v)
+
+
+def test_helpers_long_horizon_many_chunks():
+    """Advisor r5 (high): a pass of N = 2100 at M = 16 has ceil(2 M (N + 1) / 256) = 263 chunks, more than the 8-bit
+    chunk field of round 5's claim word could hold, so helpers dropped chunks and the instance timed out.  With the
+    20-bit field (kClaimChunkShift) a small batch with helpers from the start runs bitwise as without helpers."""
+    from ttmpc import scenarios as sc
+    N, M = 2100, 16
+    obs = np.array([[20.0 * i, 40.0, 4.0, 2.0] for i in range(M)])
+    x0 = np.array([[0.0, 0.0, 0.0, 0.0, 0.0, 2.0], [0.0, 1.0, 0.05, 0.0, 0.0, 2.0]])
+    xg = np.array([[300.0, 0.0, 0.0, 0.0, 0.0, 0.0], [300.0, 2.0, 0.0, 0.0, 0.0, 0.0]])
+    zg = np.stack([sc.obca_guess(np.array([a[:2], b[:2]]), np.array([a[2], b[2]]), np.zeros(2), N, M, complete=True)
+                   for a, b in zip(x0, xg)])
+    runs = []
+    for nh in (-1, 0):
+        s = _solver(N, obs, max_iter=3)
+        s.set_helpers(nh)
+        runs.append(s.solve(x0, xg, z_guess=zg))
+    assert np.all(runs[0][3] <= 2), runs[0][3]        # no hand-off timeout, nothing non-finite
+    for u, v in zip(runs[0], runs[1]):
+        assert np.array_equal(u, v)
+
+
 def test_obca_lockstep_with_oracle():
     """Step-level parity: every instance of the three parity workloads (16 MPC+OBCA windows, the 14 C4 test cases, 16
     re-plans), GPU and oracle both stopped at max_iter K.  Both run the same restated IPOPT on the same inputs, so

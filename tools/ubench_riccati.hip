@@ -151,10 +151,96 @@ __device__ __forceinline__ bool ub_riccati_dpp(const Ctx<UB_BM>& c, double dw) {
     return pd;
 }
 
+// Round 6, structured stage variants (timing only; V = 30.. are not bitwise phase_riccati):
+//   30 = the input-Hessian diagonals prefetched with dw folded in (s00 = 2R00 + Sigma_u0 + dw, one fma per entry
+//        instead of three ops) and the redundant h11 > 0 test dropped (h00 > 0 and det > 1e-13 h00 h11 imply it);
+//   31 = 30 + M from the unnormalised adjugate (m' = adj(H) g, P = F - id (g' m'), K = -id m': no i00/i01/i11);
+//   32 = 31 + the four-term state sums: rows 4, 5 of D are zero, so PA and F take four FMAs plus the affine
+//        column's b^4, b^5 terms as a separate pair of FMAs only where j = 6 / i = 6 would need them (here: dropped,
+//        the lower bound of splitting the affine part off);
+//   33 = 31 + the prefetch as 10 paired reads (V = 8's layout)
+template <int V>
+__device__ __forceinline__ bool ub_riccati_s(const Ctx<UB_BM>& c, double dw) {
+    constexpr int NS = UB_N;
+    constexpr int VO = V == 33 ? 8 : 0;
+    const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
+    EpMap m;
+    m.init(i, j, c.sm + hQW);
+    const double dt = c.dt, dt2 = dt * dt;
+    const double r01 = 2.0 * c.h(hRW + 1);
+    double* PF = c.sm + hPF;
+    double* PT = c.sm + hPT;
+    double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
+    PF[c.lane] = Pij;
+    asm volatile("" ::: "memory");
+    bool pd = true;
+    const bool own_p = m.ps >= 0;
+    const bool k_row = i >= 6 && j < 7;
+    const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
+    auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
+        const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
+        const double2 p5 = ld2(PF + 44);
+        const double p44 = PF[36];
+        const double h00 = fma(dt2, p5.y, o.sgu0), h01 = fma(dt2, p5.x, r01), h11 = fma(dt2, p44, o.sgu1);
+        const double det = fma(h00, h11, -(h01 * h01));
+        pd = pd & (h00 > 0.0) & (det > 1e-13 * h00 * h11);
+        const double id = frcp(det);
+        double pa, pb;
+        if constexpr (V == 32) {
+            pa = fma(r01v.x, o.dj[0], Pij); pb = r01v.y * o.dj[1];
+            pa = fma(r23v.x, o.dj[2], pa); pb = fma(r23v.y, o.dj[3], pb);
+        } else {
+            pa = fma(r01v.x, o.dj[0], Pij); pb = r01v.y * o.dj[1];
+            pa = fma(r23v.x, o.dj[2], pa); pb = fma(r23v.y, o.dj[3], pb);
+            pa = fma(r45v.x, o.dj[4], pa); pb = fma(r45v.y, o.dj[5], pb);
+        }
+        const double PAij = pa + pb;
+        PT[8 * j + i] = PAij;
+        asm volatile("" ::: "memory");
+        const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
+        const double2 gi = ld2(PT + 8 * i + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        nx = ub_ops<VO>(c, m, kn, dw);
+        double fa, fb;
+        if constexpr (V == 32) {
+            fa = fma(o.di[0], c01.x, PAij + o.h); fb = o.di[1] * c01.y;
+            fa = fma(o.di[2], c23.x, fa); fb = fma(o.di[3], c23.y, fb);
+        } else {
+            fa = fma(o.di[0], c01.x, PAij + o.h); fb = o.di[1] * c01.y;
+            fa = fma(o.di[2], c23.x, fa); fb = fma(o.di[3], c23.y, fb);
+            fa = fma(o.di[4], c45.x, fa); fb = fma(o.di[5], c45.y, fb);
+        }
+        const double F = fa + fb;
+        const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
+        const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
+        double m0, m1;
+        if constexpr (V == 30) {
+            const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
+            m0 = fma(i00, g0j, i01 * g1j); m1 = fma(i01, g0j, i11 * g1j);
+            Pij = F - fma(g0i, m0, g1i * m1);
+        } else {
+            const double a0 = fma(h11, g0j, -(h01 * g1j)), a1 = fma(h00, g1j, -(h01 * g0j));
+            Pij = fma(-id, fma(g0i, a0, g1i * a1), F);
+            m0 = a0 * id; m1 = a1 * id;
+        }
+        PF[c.lane] = Pij;
+        asm volatile("" ::: "memory");
+        c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
+    };
+    EpOps oa = ub_ops<VO>(c, m, N - 1, dw), ob;
+#pragma unroll
+    for (int k = NS - 1; k >= 1; k -= 2) {
+        stage(k, oa, ob, k - 1);
+        stage(k - 1, ob, oa, k >= 2 ? k - 2 : 0);
+    }
+    return pd;
+}
+
 template <int V>
 __device__ __forceinline__ bool ub_riccati(const Ctx<UB_BM>& c, double dw) {
     if constexpr (V == 9) return phase_riccati<UB_BM, UB_N>(c, dw);
     if constexpr (V == 20 || V == 21) return ub_riccati_dpp<V>(c, dw);
+    if constexpr (V >= 30 && V <= 33) return ub_riccati_s<V>(c, dw);
     constexpr int NS = UB_N;
     const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
     EpMap m;
@@ -371,6 +457,13 @@ int main() {
     run<13>("prefetch all after the P-row reads");
     run<20>("P row by DPP row_newbcast + readlane");
     run<21>("20 + PA column by ds_bpermute");
+    run<30>("folded H_uu diagonals, no h11 test");
+    run<31>("30 + adjugate M");
+    run<32>("31 + four-term sums (bound)");
+    run<33>("31 + paired prefetch reads");
+    run<9>("real phase_riccati<N=20> (again)");
+    run<9>("real phase_riccati<N=20> B=256", 256);
+    run<5>("no prefetch, no store B=256", 256);
     check_unaligned();
     check_wred();
     return 0;
