@@ -985,6 +985,7 @@ __device__ __forceinline__ unsigned long long add_rlx(gu64* p, unsigned long lon
 __device__ __forceinline__ unsigned long long dbits(double v) { return (unsigned long long)__double_as_longlong(v); }
 __device__ __forceinline__ double bitsd(unsigned long long v) { return __longlong_as_double((long long)v); }
 constexpr unsigned long long kSpinTicks = 500000000ull;  // 5 s of the 100 MHz s_memrealtime clock
+constexpr unsigned long long kStartTicks = 2000ull;  // 20 us: how long a helper waits for the batch to have started
 constexpr int kStatusHandoffTimeout = 6;  // TT_HANDOFF_TIMEOUT (include/ttmpc.h)
 #ifndef OBCA_HELPER_RELEASE
 #define OBCA_HELPER_RELEASE 1
@@ -1004,6 +1005,7 @@ __device__ void run_pass(const Ctx& c, LShared& sh, const ChunkPass& p) {
             const unsigned long long fin = ld_rlx(hdr), hlp = ld_rlx(hdr + 1), started = ld_rlx(hdr + 2);
             on = hlp > 0 && hlp + fin >= started;
         }
+        on |= c.b == a.fail_b && !sh.hfail;  // the forced-timeout instance publishes whether or not helpers came
         sh.hcur = on;
     }
     __syncthreads();
@@ -3613,9 +3615,18 @@ __device__ __forceinline__ void helper_main(LArgs& a, Ctx& cw, LShared& sh) {
     const int B = a.B, lane = (int)threadIdx.x;
     gu64* hdr = board_line(a, B);
     if (lane == 0) {
-        // a helper that finds an instance not yet started leaves at once: a workgroup that waits for the batch to finish
-        // must never hold a CU an instance still needs (dispatch order is not promised)
-        sh.hexit = ld_rlx(hdr + 2) < (unsigned long long)B ? 1 : 0;
+        // a helper that finds an instance not yet started leaves: a workgroup that waits for the batch to finish must
+        // never hold a CU an instance still needs (dispatch order is not promised).  The instances count themselves at
+        // kernel entry; a helper dispatched right behind them waits up to kStartTicks (20 us) for that count before it
+        // decides -- round 5 decided at the first look, so with a small batch the helpers could all leave while the
+        // instances were still in their first instructions (a flaky 2x on the B = 1 plan).
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long st = ld_rlx(hdr + 2);
+        while (st < (unsigned long long)B && __builtin_amdgcn_s_memrealtime() - t0 < kStartTicks) {
+            __builtin_amdgcn_s_sleep(4);
+            st = ld_rlx(hdr + 2);
+        }
+        sh.hexit = st < (unsigned long long)B ? 1 : 0;
         if (!sh.hexit) add_rlx(hdr + 1, 1);
     }
     __syncthreads();
@@ -4481,6 +4492,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
     LShared& sh = *(LShared*)&sh_storage;
     extern __shared__ double dyn_lds[];
     __shared__ ObcaArgs args_lds;
+    // an instance counts itself started first thing, so that helpers dispatched right behind the instances see the
+    // whole batch started (helper_main waits briefly for that instead of leaving at the first look)
+    if (threadIdx.x == 0 && args.board && blockIdx.x < (unsigned)args.B)
+        __hip_atomic_fetch_add((unsigned long long*)(args.board + (size_t)args.B * kObcaBoardStride) + 2, 1ull,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     {
         const int* src = reinterpret_cast<const int*>(&args);
         int* dst = reinterpret_cast<int*>(&args_lds);
@@ -4551,7 +4567,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(1, 1))) void 
         sh.nfl[0] = sh.nfl[1] = 0;
         sh.hep = 0;
         sh.hfail = 0;
-        if (a.board) add_rlx(board_line(a, a.B) + 2, 1);
     }
     const unsigned long long tstart = clock64();
     // ---------------- initial point (bound push, slacks = pushed d(x0), multipliers 1 / 0) ----------------

@@ -69,6 +69,8 @@ static_assert(rDXS + 8 == kRowsPerStage, "stage record");
 // second lives (see the LDS map): curvature, Sigma, dB from the linearisation to the Riccati sweep; the
 // Riccati operands diag(Sigma) + diag(W), Sigma_u and b^ = -c_{k+1} (stage k); the trial residual c
 constexpr int rWC = rDX, rSG = rPS, rDB = rPS + 8, rHD = rDXS, rSGU = rDXS + 6, rBH = rYP, rCT = rDXS;
+// the shifted input gradient g_u' of the Newton sweep (ric_prep .. Riccati) in the b^4, b^5 rows (see gu_shift)
+constexpr int rGU = rBH + 4;
 
 // ---- wave reductions: DPP inside each 16-lane row (xor 1, xor 2, half-mirror, mirror), then the four
 // row results by v_readlane into SGPRs.  No LDS; the result is wave-uniform and bitwise identical in
@@ -901,6 +903,39 @@ __device__ __forceinline__ void mstore(const Ctx<BM>& c, bool valid, int row, in
     if (valid) c.sm[HEAD + k * SR + row] = v;
 }
 
+// The input shift of the Newton sweep (round 6).  B = dt [e5 e4]: rows 4, 5 of the dynamics (phi, v)
+// are pure integrators of the inputs, so the residual's rows 4, 5 can be carried by the input instead of the affine
+// column: du' = du + s with s = (b^5, b^4) / dt gives dx_{k+1} = A dx_k + B du' + (b^0..b^3, 0, 0).  Rows 4, 5 of
+// dt*J are zero as well, so every entry of PA = P A^ and of F = A^' PA + H^ becomes a four-term sum (round 5: six, for
+// the affine column and row).  The stage cost in du' has the linear term g_u' = g_u - H_u s, H_u = 2 Rw + Sigma_u + dw I
+// (no state-input curvature: f is linear in u); P, p and K are the same, and k_ff' = k_ff + s, which the Newton forward
+// sweep undoes (phase_forward: du = du' - s, with s taken from c_{k+1}).  g_u' depends on dw: ric_prep stores it for
+// dw = 0 and the inertia retries rewrite it (ric_gu_shift).  A different rounding, not a different method: tolerance
+// parity with the oracle (tests/test_gpu_parity.py), not bitwise identity with round 5.
+template <int BM>
+__device__ __forceinline__ void gu_shift(const Ctx<BM>& c, double gu0, double gu1, double su0, double su1, double cn4,
+                                         double cn5, double dw, double& g0, double& g1) {
+    const double idt = 1.0 / c.dt;
+    const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
+    const double s0 = -cn5 * idt, s1 = -cn4 * idt;  // (b^5, b^4) / dt, b^ = -c_{k+1}
+    const double h00 = r00 + su0 + dw, h11 = r11 + su1 + dw;
+    g0 = gu0 - fma(h00, s0, r01 * s1);
+    g1 = gu1 - fma(r01, s0, h11 * s1);
+}
+// an inertia retry with dw > 0: g_u' for the new dw (the rows gu_shift reads are intact until the forward sweep)
+template <int BM>
+__device__ __forceinline__ void ric_gu_shift(const Ctx<BM>& c, double dw) {
+    for (int k = c.lane; k < c.N; k += W) {
+        const double gu0 = c.r(rGF + 6, k), gu1 = c.r(rGF + 7, k), su0 = c.r(rSGU, k), su1 = c.r(rSGU + 1, k);
+        const double cn4 = c.r(rCC + 4, k + 1), cn5 = c.r(rCC + 5, k + 1);
+        double g0, g1;
+        gu_shift(c, gu0, gu1, su0, su1, cn4, cn5, dw, g0, g1);
+        c.r(rGU, k) = g0;
+        c.r(rGU + 1, k) = g1;
+    }
+    __syncthreads();
+}
+
 // stage-parallel: fold the barrier, curvature and constraint terms into the Riccati operand rows
 template <int BM>
 __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
@@ -927,8 +962,15 @@ __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
         c.r(rSGU, k) = su0;
         c.r(rSGU + 1, k) = su1;
         if (k < N) {
+            double cn[6];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) c.r(rBH + i, k) = -c.r(rCC + i, k + 1);
+            for (int i = 0; i < 6; ++i) cn[i] = c.r(rCC + i, k + 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) c.r(rBH + i, k) = -cn[i];
+            double g0, g1;
+            gu_shift(c, g[6], g[7], su0, su1, cn[4], cn[5], 0.0, g0, g1);
+            c.r(rGU, k) = g0;
+            c.r(rGU + 1, k) = g1;
         } else {  // terminal stage: no dynamics, so no curvature
 #pragma unroll
             for (int i = 0; i < 7; ++i) c.r(rWC + i, k) = 0.0;
@@ -939,16 +981,17 @@ __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
 
 // Per-lane slots of entry (i, j): D[m][j] (m = 0..5) for PA, D[l][i] for F, H^[i][j], store rows.
 struct EpMap {
-    int dj[6], di[6];
+    int dj[4], di[4];
     int hs, ps;
     int gj0, gj1, gi0, gi1;  // rows of g_u at the affine column / row (j or i = 6), the zero pad elsewhere
     double q2, dg;
-    __device__ __forceinline__ static int dslot(int m, int n) {  // row of D[m][n] (PAD = 0)
-        return (m < 6 && n < 6 && d_idx(m, n) >= 0) ? rAJ + d_idx(m, n) : (m < 6 && n == 6) ? rBH + m : PAD;
+    // row of D[m][n], m = 0..3 (rows 4, 5 of dt*J are zero and the shifted affine column has no rows 4, 5; PAD = 0)
+    __device__ __forceinline__ static int dslot(int m, int n) {
+        return (m < 4 && n < 6 && d_idx(m, n) >= 0) ? rAJ + d_idx(m, n) : (m < 4 && n == 6) ? rBH + m : PAD;
     }
     __device__ __forceinline__ void init(int i, int j, const double* QW) {
 #pragma unroll
-        for (int m = 0; m < 6; ++m) {
+        for (int m = 0; m < 4; ++m) {
             dj[m] = dslot(m, j);
             di[m] = dslot(m, i);
         }
@@ -958,30 +1001,30 @@ struct EpMap {
         q2 = (i < 6 && j < 6) ? 2.0 * QW[i * 6 + j] : 0.0;
         dg = (i == j && i < 6) ? 1.0 : 0.0;
         ps = (i <= j && j < 6) ? rPS + sym_idx(i, j) : (i < 6 && j == 6) ? rPV + i : -1;
-        gj0 = j == 6 ? rGF + 6 : PAD;
-        gj1 = j == 6 ? rGF + 7 : PAD;
-        gi0 = i == 6 ? rGF + 6 : PAD;
-        gi1 = i == 6 ? rGF + 7 : PAD;
+        gj0 = j == 6 ? rGU : PAD;
+        gj1 = j == 6 ? rGU + 1 : PAD;
+        gi0 = i == 6 ? rGU : PAD;
+        gi1 = i == 6 ? rGU + 1 : PAD;
     }
 };
 
 // stage operands (independent of P^_{k+1}): fetched one stage ahead so LDS latency hides
 struct EpOps {
-    double dj[6], di[6], h, sgu0, sgu1, gj0, gj1, gi0, gi1;
+    double dj[4], di[4], h, sgu0, sgu1, gj0, gj1, gi0, gi1;
 };
 // in two halves: A (D[.][j], Sigma_u) is issued behind the P-row reads, B (D[.][i], H^, g_u) behind the
 // PA-column reads, which spreads the LDS queue over the stage (tools/ubench_riccati.hip: -44 cycles/stage)
 template <int BM>
 __device__ __forceinline__ void ep_ops_a(const Ctx<BM>& c, const EpMap& m, int k, EpOps& o) {
 #pragma unroll
-    for (int t = 0; t < 6; ++t) o.dj[t] = c.r(m.dj[t], k);
+    for (int t = 0; t < 4; ++t) o.dj[t] = c.r(m.dj[t], k);
     o.sgu0 = c.r(rSGU, k);
     o.sgu1 = c.r(rSGU + 1, k);
 }
 template <int BM>
 __device__ __forceinline__ void ep_ops_b(const Ctx<BM>& c, const EpMap& m, int k, double dw, EpOps& o) {
 #pragma unroll
-    for (int t = 0; t < 6; ++t) o.di[t] = c.r(m.di[t], k);
+    for (int t = 0; t < 4; ++t) o.di[t] = c.r(m.di[t], k);
     o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
     o.gj0 = c.r(m.gj0, k);
     o.gj1 = c.r(m.gj1, k);
@@ -1034,7 +1077,7 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     // after a tile read so that waiting for the tile never waits for the prefetch)
     auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
         // row i of P^_{k+1} and the reduced input Hessian entries (uniform)
-        const double2 r01v = ld2(PF + 8 * i + sw_i), r23v = ld2(PF + 8 * i + (2 ^ sw_i)), r45v = ld2(PF + 8 * i + (4 ^ sw_i));
+        const double2 r01v = ld2(PF + 8 * i + sw_i), r23v = ld2(PF + 8 * i + (2 ^ sw_i));
         const double2 p5 = ld2(PF + 40);  // P[5][4], P[5][5] (row 5: columns 4, 5 at slots 0, 1)
         const double p44 = PF[32];        // P[4][4] (row 4: column 4 at slot 0)
         __builtin_amdgcn_sched_barrier(0);
@@ -1044,12 +1087,10 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         const double det = h00 * h11 - h01 * h01;
         pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
         const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
-        // PA[i][j] = P[i][j] + sum_m P[i][m] D[m][j]
+        // PA[i][j] = P[i][j] + sum_{m<4} P[i][m] D[m][j]
         double pa = fma(r01v.x, o.dj[0], Pij), pb = r01v.y * o.dj[1];
         pa = fma(r23v.x, o.dj[2], pa);
         pb = fma(r23v.y, o.dj[3], pb);
-        pa = fma(r45v.x, o.dj[4], pa);
-        pb = fma(r45v.y, o.dj[5], pb);
         const double PAij = pa + pb;
         PT[8 * j + (i ^ sw_j)] = PAij;
         asm volatile("" ::: "memory");  // the tile is read by other lanes: keep program order
@@ -1059,12 +1100,10 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         // next stage's operands, second half: issued behind the tile reads (LDS serves a wave in order)
         __builtin_amdgcn_sched_barrier(0);
         ep_ops_b(c, m, kn, dw, nx);
-        // F[i][j] = PA[i][j] + sum_l D[l][i] PA[l][j] + H^[i][j]
+        // F[i][j] = PA[i][j] + sum_{l<4} D[l][i] PA[l][j] + H^[i][j]
         double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
         fa = fma(o.di[2], c23.x, fa);
         fb = fma(o.di[3], c23.y, fb);
-        fa = fma(o.di[4], c45.x, fa);
-        fb = fma(o.di[5], c45.y, fb);
         const double F = fa + fb;
         // G[0][.] = dt PA[5][.] + S, G[1][.] = dt PA[4][.] + S;  M = H_uu^-1 G;  P^_k = F - G' M
         const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
@@ -1119,9 +1158,15 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bh
     const double fone = (g < 6 && mm == g) ? 1.0 : 0.0;
     // BHN: b^_k = -c_{k+1} read straight from the residual rows of stage k+1 (row SR + crow + g of stage k)
     // instead of a stored b^ row (the SOC sweep: c_soc lives where its own output dX_soc goes)
+    // The Newton sweep (!BHN) runs in the Riccati's shifted input (gu_shift): K^'s affine column is k_ff' = k_ff + s,
+    // so the state rows 4, 5 take no b^ term (dt k_ff' carries it) and du = du' - s, with -s = c_{k+1}[(5, 4)] / dt from
+    // the residual rows of stage k+1.  The SOC sweep (BHN) runs on the unshifted factors of phase_soc_backward.
+    const bool shf = !BHN && mm == 6;
     const int fas = (g < 6 && mm < 6 && d_idx(g, mm) >= 0) ? rAJ + d_idx(g, mm)
+                  : (shf && (g == 4 || g == 5)) ? PAD
+                  : (shf && g == 6) ? SR + crow + 5 : (shf && g == 7) ? SR + crow + 4
                   : (g < 6 && mm == 6) ? (BHN ? SR + crow + g : bhrow + g) : PAD;
-    const double fsg = (BHN && g < 6 && mm == 6) ? -1.0 : 1.0;
+    const double fsg = (BHN && g < 6 && mm == 6) ? -1.0 : (shf && g >= 6) ? 1.0 / c.dt : 1.0;
     const int fk = (u >= 0 && mm < 6) ? rK + 6 * u + mm : (u >= 0 && mm == 6) ? rKF + u : PAD;
     const double fkc = u >= 0 ? (g < 6 ? c.dt : 1.0) : 0.0;
     // x^_0[m] = -c_0[m] (m < 6), 1 (m = 6), 0 (m = 7)
@@ -1814,6 +1859,7 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
             phase_ric_prep(c);
             for (int attempt = 0; attempt < 30; ++attempt) {
                 COUNT(PH_NRIC);
+                if (dw > 0.0) ric_gu_shift(c, dw);
                 if (phase_riccati<BM, NS>(c, dw)) { ok = true; break; }
                 dw = (dw == 0.0) ? (dw_last == 0.0 ? 1e-4 : fmax(1e-20, dw_last / 3.0))
                                  : (dw_last == 0.0 ? 100.0 * dw : 8.0 * dw);

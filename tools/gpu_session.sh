@@ -67,7 +67,7 @@ for step in "$@"; do
         mkdir -p "$d"
         timeout -s KILL 300 rocprofv3 --pmc "$c" --kernel-trace -d "$d" -o "$n" --output-format csv \
           -- python3 bench.py --config "$a1" --cpu-budget 0 --no-latency $(args "$a2") > "$d.log" 2>&1 || fail "$step $c" "$d.log"
-        tail -1 "$d.log" > "$d.bench.json"
+        grep "^{\"metric\"" "$d.log" > "$d.bench.json"
       done ;;
     ubench)
       timeout -k 10 300 "tools/bin/ubench_$a1" > "$OUT/ubench_$a1.txt" 2>&1 || fail "$step" "$OUT/ubench_$a1.txt"

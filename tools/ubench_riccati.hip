@@ -16,311 +16,128 @@ namespace {
 
 constexpr int UB_BM = kMaskMPC | kDiagBit;
 constexpr int UB_N = 20;
-constexpr int UB_SR2 = 118;  // even stride for the paired-row emulation (V = 8); V = 10 uses SR (odd)
+constexpr int UB_SR2 = 118;  // LDS image stride of the synthetic records (>= SR)
 
-// V: 0 = copy of the shipped stage; 1 = no next-stage prefetch (operands reused); 2 = no factor-row
-//    store; 5 = 1 + 2; 8 = prefetch as 10 reads (D pairs / g_u pairs / Sigma_u pair as b128 from an even
-//    stride) instead of 19; 9 = the real phase_riccati; 10 = 8 on the odd stride (b128 at 8-byte
-//    alignment: the unaligned DS mode); 12 = dj, Sigma_u prefetched after the P-row reads, the rest after
-//    the PA-column reads; 13 = all after the P-row reads; 14 = 8 on the odd stride as ds_read2_b64
-__device__ __forceinline__ double2 ldu(const double* p) {  // b128 at 8-byte alignment (V = 10)
-    return *reinterpret_cast<const double2*>(__builtin_assume_aligned(p, 16));
-}
-template <int V>
-__device__ __forceinline__ EpOps ub_ops(const Ctx<UB_BM>& c, const EpMap& m, int k, double dw) {
-    if constexpr (V == 14) {  // the paired layout on the odd stride, as adjacent b64 reads (ds_read2_b64)
-        EpOps o;
-        const double* s = c.sm + HEAD + k * SR;
-        const int pj = 2 * (c.lane & 7), pi = 2 * (c.lane >> 3);
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const double* a = s + pj + 16 * t;
-            const double* b = s + pi + 16 * t + 48;
-            o.dj[2 * t] = a[0]; o.dj[2 * t + 1] = a[1];
-            o.di[2 * t] = b[0]; o.di[2 * t + 1] = b[1];
-        }
-        o.h = m.q2 + m.dg * dw + s[m.hs];
-        const double* gj = s + 96 + pj / 8 * 2;
-        const double* gi = s + 100 + pi / 8 * 2;
-        o.sgu0 = s[108]; o.sgu1 = s[109]; o.gj0 = gj[0]; o.gj1 = gj[1]; o.gi0 = gi[0]; o.gi1 = gi[1];
-        return o;
-    } else if constexpr (V != 8 && V != 10) {
-        return ep_ops(c, m, k, dw);
-    } else {
-        EpOps o;
-        const double* s = c.sm + HEAD + k * (V == 8 ? UB_SR2 : SR);
-        const int pj = 2 * (c.lane & 7), pi = 2 * (c.lane >> 3);  // even row offsets per lane
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            const double2 a = ldu(s + pj + 16 * t), b = ldu(s + pi + 16 * t + 48);
-            o.dj[2 * t] = a.x; o.dj[2 * t + 1] = a.y;
-            o.di[2 * t] = b.x; o.di[2 * t + 1] = b.y;
-        }
-        o.h = m.q2 + m.dg * dw + s[m.hs];
-        const double2 su = ldu(s + 108), gj = ldu(s + 96 + pj / 8 * 2), gi = ldu(s + 100 + pi / 8 * 2);
-        o.sgu0 = su.x; o.sgu1 = su.y; o.gj0 = gj.x; o.gj1 = gj.y; o.gi0 = gi.x; o.gi1 = gi.y;
-        return o;
+// Round 6: the shipped phase_riccati runs the input-shift form (four-term sums, tt_track.hip gu_shift).  V = 9 is that
+// kernel; V = 50 is a private copy of round 5's stage (six-term sums, g_u in the affine slots) for the A/B in one
+// binary; V = 51 is round 5's stage without the next-stage prefetch and the factor-row store (its floor).  The
+// earlier variants (prefetch splits, paired reads, DPP P rows, bpermute PA columns, folded H_uu diagonals, the
+// adjugate M) are recorded in DESIGN.md and profiles/r06/ubench_riccati_r5variants.txt; git history holds their code.
+struct R5Map {
+    int dj[6], di[6];
+    int hs, ps;
+    int gj0, gj1, gi0, gi1;
+    double q2, dg;
+    __device__ __forceinline__ static int dslot(int m, int n) {
+        return (m < 6 && n < 6 && d_idx(m, n) >= 0) ? rAJ + d_idx(m, n) : (m < 6 && n == 6) ? rBH + m : PAD;
     }
-}
-
-// row_newbcast:n (gfx90a+ DPP64): every lane of a 16-lane row receives lane n of that row
-template <int N_>
-__device__ __forceinline__ double nbc(double v) {
-    const long long b = __double_as_longlong(v);
-    return __longlong_as_double(__builtin_amdgcn_update_dpp(b, b, 0x150 + N_, 0xF, 0xF, false));
-}
-// row i of the 8x8 tile held entry-per-lane (lane 8i + j): lanes 16r + 8h + m, h = i & 1
-template <int M_>
-__device__ __forceinline__ double prow(double v, bool h) {
-    const double a0 = nbc<M_>(v), a1 = nbc<8 + M_>(v);
-    return h ? a1 : a0;
-}
-__device__ __forceinline__ double bperm2(double v, int src_lane) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b & 0xffffffffll));
-    const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(b >> 32));
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// V = 20: the P row by DPP row_newbcast + readlane instead of the PF tile round trip;
-// V = 21: 20 + the PA column by ds_bpermute instead of the PT tile round trip
-template <int V>
-__device__ __forceinline__ bool ub_riccati_dpp(const Ctx<UB_BM>& c, double dw) {
-    constexpr int NS = UB_N;
-    const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
-    const bool hh = i & 1;
-    EpMap m;
-    m.init(i, j, c.sm + hQW);
-    const double dt = c.dt, dt2 = dt * dt;
-    const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
-    double* PT = c.sm + hPT;
-    double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
-    bool pd = true;
-    const bool own_p = m.ps >= 0;
-    const bool k_row = i >= 6 && j < 7;
-    const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
-    auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
-        const double q0 = prow<0>(Pij, hh), q1 = prow<1>(Pij, hh), q2 = prow<2>(Pij, hh);
-        const double q3 = prow<3>(Pij, hh), q4 = prow<4>(Pij, hh), q5 = prow<5>(Pij, hh);
-        const double p54 = readlane_d(Pij, 44), p55 = readlane_d(Pij, 45), p44 = readlane_d(Pij, 36);
-        __builtin_amdgcn_sched_barrier(0);
-        ep_ops_a(c, m, kn, nx);
-        __builtin_amdgcn_sched_barrier(0);
-        const double h00 = r00 + o.sgu0 + dw + dt2 * p55, h01 = r01 + dt2 * p54, h11 = r11 + o.sgu1 + dw + dt2 * p44;
-        const double det = h00 * h11 - h01 * h01;
-        pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
-        const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
-        double pa = fma(q0, o.dj[0], Pij), pb = q1 * o.dj[1];
-        pa = fma(q2, o.dj[2], pa);
-        pb = fma(q3, o.dj[3], pb);
-        pa = fma(q4, o.dj[4], pa);
-        pb = fma(q5, o.dj[5], pb);
-        const double PAij = pa + pb;
-        double2 c01, c23, c45, gi;
-        if constexpr (V == 21) {
-            c01.x = bperm2(PAij, j); c01.y = bperm2(PAij, 8 + j);
-            c23.x = bperm2(PAij, 16 + j); c23.y = bperm2(PAij, 24 + j);
-            c45.x = bperm2(PAij, 32 + j); c45.y = bperm2(PAij, 40 + j);
-            gi.x = bperm2(PAij, 32 + i); gi.y = bperm2(PAij, 40 + i);
-        } else {
-            PT[8 * j + i] = PAij;
-            asm volatile("" ::: "memory");
-            c01 = ld2(PT + 8 * j); c23 = ld2(PT + 8 * j + 2); c45 = ld2(PT + 8 * j + 4);
-            gi = ld2(PT + 8 * i + 4);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        ep_ops_b(c, m, kn, dw, nx);
-        double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
-        fa = fma(o.di[2], c23.x, fa);
-        fb = fma(o.di[3], c23.y, fb);
-        fa = fma(o.di[4], c45.x, fa);
-        fb = fma(o.di[5], c45.y, fb);
-        const double F = fa + fb;
-        const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
-        const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
-        const double m0 = fma(i00, g0j, i01 * g1j), m1 = fma(i01, g0j, i11 * g1j);
-        Pij = F - fma(g0i, m0, g1i * m1);
-        c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
-    };
-    EpOps oa = ep_ops(c, m, N - 1, dw), ob;
+    __device__ __forceinline__ void init(int i, int j, const double* QW) {
 #pragma unroll
-    for (int k = NS - 1; k >= 1; k -= 2) {
-        stage(k, oa, ob, k - 1);
-        stage(k - 1, ob, oa, k >= 2 ? k - 2 : 0);
+        for (int m = 0; m < 6; ++m) {
+            dj[m] = dslot(m, j);
+            di[m] = dslot(m, i);
+        }
+        const int gi = (i < 6 && j == 6) ? i : (i == 6 && j < 6) ? j : -1;
+        hs = (i == j && i < 6) ? rHD + i : (i < 6 && j < 6 && w_idx(i, j) >= 0) ? rWC + w_idx(i, j)
+           : gi >= 0 ? rGF + gi : PAD;
+        q2 = (i < 6 && j < 6) ? 2.0 * QW[i * 6 + j] : 0.0;
+        dg = (i == j && i < 6) ? 1.0 : 0.0;
+        ps = (i <= j && j < 6) ? rPS + sym_idx(i, j) : (i < 6 && j == 6) ? rPV + i : -1;
+        gj0 = j == 6 ? rGF + 6 : PAD;
+        gj1 = j == 6 ? rGF + 7 : PAD;
+        gi0 = i == 6 ? rGF + 6 : PAD;
+        gi1 = i == 6 ? rGF + 7 : PAD;
     }
-    return pd;
-}
-
-// Round 6, structured stage variants (timing only; V = 30.. are not bitwise phase_riccati):
-//   30 = the input-Hessian diagonals prefetched with dw folded in (s00 = 2R00 + Sigma_u0 + dw, one fma per entry
-//        instead of three ops) and the redundant h11 > 0 test dropped (h00 > 0 and det > 1e-13 h00 h11 imply it);
-//   31 = 30 + M from the unnormalised adjugate (m' = adj(H) g, P = F - id (g' m'), K = -id m': no i00/i01/i11);
-//   32 = 31 + the four-term state sums: rows 4, 5 of D are zero, so PA and F take four FMAs plus the affine
-//        column's b^4, b^5 terms as a separate pair of FMAs only where j = 6 / i = 6 would need them (here: dropped,
-//        the lower bound of splitting the affine part off);
-//   33 = 31 + the prefetch as 10 paired reads (V = 8's layout)
-template <int V>
-__device__ __forceinline__ bool ub_riccati_s(const Ctx<UB_BM>& c, double dw) {
-    constexpr int NS = UB_N;
-    constexpr int VO = V == 33 ? 8 : 0;
-    const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
-    EpMap m;
-    m.init(i, j, c.sm + hQW);
-    const double dt = c.dt, dt2 = dt * dt;
-    const double r01 = 2.0 * c.h(hRW + 1);
-    double* PF = c.sm + hPF;
-    double* PT = c.sm + hPT;
-    double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
-    PF[c.lane] = Pij;
-    asm volatile("" ::: "memory");
-    bool pd = true;
-    const bool own_p = m.ps >= 0;
-    const bool k_row = i >= 6 && j < 7;
-    const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
-    auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
-        const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
-        const double2 p5 = ld2(PF + 44);
-        const double p44 = PF[36];
-        const double h00 = fma(dt2, p5.y, o.sgu0), h01 = fma(dt2, p5.x, r01), h11 = fma(dt2, p44, o.sgu1);
-        const double det = fma(h00, h11, -(h01 * h01));
-        pd = pd & (h00 > 0.0) & (det > 1e-13 * h00 * h11);
-        const double id = frcp(det);
-        double pa, pb;
-        if constexpr (V == 32) {
-            pa = fma(r01v.x, o.dj[0], Pij); pb = r01v.y * o.dj[1];
-            pa = fma(r23v.x, o.dj[2], pa); pb = fma(r23v.y, o.dj[3], pb);
-        } else {
-            pa = fma(r01v.x, o.dj[0], Pij); pb = r01v.y * o.dj[1];
-            pa = fma(r23v.x, o.dj[2], pa); pb = fma(r23v.y, o.dj[3], pb);
-            pa = fma(r45v.x, o.dj[4], pa); pb = fma(r45v.y, o.dj[5], pb);
-        }
-        const double PAij = pa + pb;
-        PT[8 * j + i] = PAij;
-        asm volatile("" ::: "memory");
-        const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
-        const double2 gi = ld2(PT + 8 * i + 4);
-        __builtin_amdgcn_sched_barrier(0);
-        nx = ub_ops<VO>(c, m, kn, dw);
-        double fa, fb;
-        if constexpr (V == 32) {
-            fa = fma(o.di[0], c01.x, PAij + o.h); fb = o.di[1] * c01.y;
-            fa = fma(o.di[2], c23.x, fa); fb = fma(o.di[3], c23.y, fb);
-        } else {
-            fa = fma(o.di[0], c01.x, PAij + o.h); fb = o.di[1] * c01.y;
-            fa = fma(o.di[2], c23.x, fa); fb = fma(o.di[3], c23.y, fb);
-            fa = fma(o.di[4], c45.x, fa); fb = fma(o.di[5], c45.y, fb);
-        }
-        const double F = fa + fb;
-        const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
-        const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
-        double m0, m1;
-        if constexpr (V == 30) {
-            const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
-            m0 = fma(i00, g0j, i01 * g1j); m1 = fma(i01, g0j, i11 * g1j);
-            Pij = F - fma(g0i, m0, g1i * m1);
-        } else {
-            const double a0 = fma(h11, g0j, -(h01 * g1j)), a1 = fma(h00, g1j, -(h01 * g0j));
-            Pij = fma(-id, fma(g0i, a0, g1i * a1), F);
-            m0 = a0 * id; m1 = a1 * id;
-        }
-        PF[c.lane] = Pij;
-        asm volatile("" ::: "memory");
-        c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
-    };
-    EpOps oa = ub_ops<VO>(c, m, N - 1, dw), ob;
+};
+struct R5Ops {
+    double dj[6], di[6], h, sgu0, sgu1, gj0, gj1, gi0, gi1;
+};
+__device__ __forceinline__ void r5_ops_a(const Ctx<UB_BM>& c, const R5Map& m, int k, R5Ops& o) {
 #pragma unroll
-    for (int k = NS - 1; k >= 1; k -= 2) {
-        stage(k, oa, ob, k - 1);
-        stage(k - 1, ob, oa, k >= 2 ? k - 2 : 0);
-    }
-    return pd;
+    for (int t = 0; t < 6; ++t) o.dj[t] = c.r(m.dj[t], k);
+    o.sgu0 = c.r(rSGU, k);
+    o.sgu1 = c.r(rSGU + 1, k);
+}
+__device__ __forceinline__ void r5_ops_b(const Ctx<UB_BM>& c, const R5Map& m, int k, double dw, R5Ops& o) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) o.di[t] = c.r(m.di[t], k);
+    o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
+    o.gj0 = c.r(m.gj0, k);
+    o.gj1 = c.r(m.gj1, k);
+    o.gi0 = c.r(m.gi0, k);
+    o.gi1 = c.r(m.gi1, k);
 }
 
 template <int V>
 __device__ __forceinline__ bool ub_riccati(const Ctx<UB_BM>& c, double dw) {
-    if constexpr (V == 9) return phase_riccati<UB_BM, UB_N>(c, dw);
-    if constexpr (V == 20 || V == 21) return ub_riccati_dpp<V>(c, dw);
-    if constexpr (V >= 30 && V <= 33) return ub_riccati_s<V>(c, dw);
-    constexpr int NS = UB_N;
-    const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
-    EpMap m;
-    m.init(i, j, c.sm + hQW);
-    const double dt = c.dt, dt2 = dt * dt;
-    const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
-    double* PF = c.sm + hPF;
-    double* PT = c.sm + hPT;
-    double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
-    PF[c.lane] = Pij;
-    asm volatile("" ::: "memory");
-    bool pd = true;
-    const bool own_p = m.ps >= 0;
-    const bool k_row = i >= 6 && j < 7;
-    const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
-    auto stage = [&](int k, const EpOps& o, EpOps& nx, int kn) {
-        const double2 r01v = ld2(PF + 8 * i), r23v = ld2(PF + 8 * i + 2), r45v = ld2(PF + 8 * i + 4);
-        const double2 p5 = ld2(PF + 44);
-        const double p44 = PF[36];
-        if constexpr (V == 12 || V == 13) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int t = 0; t < 6; ++t) nx.dj[t] = c.r(m.dj[t], kn);
-            nx.sgu0 = c.r(rSGU, kn);
-            nx.sgu1 = c.r(rSGU + 1, kn);
-            if constexpr (V == 13) {
-#pragma unroll
-                for (int t = 0; t < 6; ++t) nx.di[t] = c.r(m.di[t], kn);
-                nx.h = m.q2 + m.dg * dw + c.r(m.hs, kn);
-                nx.gj0 = c.r(m.gj0, kn); nx.gj1 = c.r(m.gj1, kn); nx.gi0 = c.r(m.gi0, kn); nx.gi1 = c.r(m.gi1, kn);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        const double h00 = r00 + o.sgu0 + dw + dt2 * p5.y, h01 = r01 + dt2 * p5.x, h11 = r11 + o.sgu1 + dw + dt2 * p44;
-        const double det = h00 * h11 - h01 * h01;
-        pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
-        const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
-        double pa = fma(r01v.x, o.dj[0], Pij), pb = r01v.y * o.dj[1];
-        pa = fma(r23v.x, o.dj[2], pa);
-        pb = fma(r23v.y, o.dj[3], pb);
-        pa = fma(r45v.x, o.dj[4], pa);
-        pb = fma(r45v.y, o.dj[5], pb);
-        const double PAij = pa + pb;
-        PT[8 * j + i] = PAij;
+    if constexpr (V == 9) {
+        return phase_riccati<UB_BM, UB_N>(c, dw);
+    } else {
+        constexpr int NS = UB_N;
+        constexpr bool full = V == 50;
+        const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
+        R5Map m;
+        m.init(i, j, c.sm + hQW);
+        const double dt = c.dt, dt2 = dt * dt;
+        const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
+        double* PF = c.sm + hPF;
+        double* PT = c.sm + hPT;
+        const int sw_i = i & 4, sw_j = j & 4;
+        const int pf_own = 8 * i + (j ^ sw_i);
+        double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
+        PF[pf_own] = Pij;
         asm volatile("" ::: "memory");
-        const double2 c01 = ld2(PT + 8 * j), c23 = ld2(PT + 8 * j + 2), c45 = ld2(PT + 8 * j + 4);
-        const double2 gi = ld2(PT + 8 * i + 4);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (V == 12) {
+        bool pd = true;
+        const bool own_p = m.ps >= 0;
+        const bool k_row = i >= 6 && j < 7;
+        const int st_row = own_p ? m.ps : k_row ? (j < 6 ? rK + 6 * (i - 6) + j : rKF + (i - 6)) : rDX + 7;
+        auto stage = [&](int k, const R5Ops& o, R5Ops& nx, int kn) {
+            const double2 r01v = ld2(PF + 8 * i + sw_i), r23v = ld2(PF + 8 * i + (2 ^ sw_i)), r45v = ld2(PF + 8 * i + (4 ^ sw_i));
+            const double2 p5 = ld2(PF + 40);
+            const double p44 = PF[32];
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (full) r5_ops_a(c, m, kn, nx);
+            __builtin_amdgcn_sched_barrier(0);
+            const double h00 = r00 + o.sgu0 + dw + dt2 * p5.y, h01 = r01 + dt2 * p5.x, h11 = r11 + o.sgu1 + dw + dt2 * p44;
+            const double det = h00 * h11 - h01 * h01;
+            pd = pd & (h00 > 0.0) & (h11 > 0.0) & (det > 1e-13 * h00 * h11);
+            const double id = frcp(det), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
+            double pa = fma(r01v.x, o.dj[0], Pij), pb = r01v.y * o.dj[1];
+            pa = fma(r23v.x, o.dj[2], pa);
+            pb = fma(r23v.y, o.dj[3], pb);
+            pa = fma(r45v.x, o.dj[4], pa);
+            pb = fma(r45v.y, o.dj[5], pb);
+            const double PAij = pa + pb;
+            PT[8 * j + (i ^ sw_j)] = PAij;
+            asm volatile("" ::: "memory");
+            const double2 c01 = ld2(PT + 8 * j + sw_j), c23 = ld2(PT + 8 * j + (2 ^ sw_j)), c45 = ld2(PT + 8 * j + (4 ^ sw_j));
+            const double2 gi = ld2(PT + 8 * i + (4 ^ sw_i));
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (full) r5_ops_b(c, m, kn, dw, nx); else nx = o;
+            double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
+            fa = fma(o.di[2], c23.x, fa);
+            fb = fma(o.di[3], c23.y, fb);
+            fa = fma(o.di[4], c45.x, fa);
+            fb = fma(o.di[5], c45.y, fb);
+            const double F = fa + fb;
+            const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
+            const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
+            const double m0 = fma(i00, g0j, i01 * g1j), m1 = fma(i01, g0j, i11 * g1j);
+            Pij = F - fma(g0i, m0, g1i * m1);
+            PF[pf_own] = Pij;
+            asm volatile("" ::: "memory");
+            if constexpr (full) c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
+        };
+        R5Ops oa, ob;
+        r5_ops_a(c, m, N - 1, oa);
+        r5_ops_b(c, m, N - 1, dw, oa);
 #pragma unroll
-            for (int t = 0; t < 6; ++t) nx.di[t] = c.r(m.di[t], kn);
-            nx.h = m.q2 + m.dg * dw + c.r(m.hs, kn);
-            nx.gj0 = c.r(m.gj0, kn); nx.gj1 = c.r(m.gj1, kn); nx.gi0 = c.r(m.gi0, kn); nx.gi1 = c.r(m.gi1, kn);
-        } else if constexpr (V == 13) {
-        } else if constexpr (V != 1 && V != 5) {
-            nx = ub_ops<V>(c, m, kn, dw);
-        } else {
-            nx = o;
+        for (int k = NS - 1; k >= 1; k -= 2) {
+            stage(k, oa, ob, k - 1);
+            stage(k - 1, ob, oa, k >= 2 ? k - 2 : 0);
         }
-        double fa = fma(o.di[0], c01.x, PAij + o.h), fb = o.di[1] * c01.y;
-        fa = fma(o.di[2], c23.x, fa);
-        fb = fma(o.di[3], c23.y, fb);
-        fa = fma(o.di[4], c45.x, fa);
-        fb = fma(o.di[5], c45.y, fb);
-        const double F = fa + fb;
-        const double g0j = fma(dt, c45.y, o.gj0), g1j = fma(dt, c45.x, o.gj1);
-        const double g0i = fma(dt, gi.y, o.gi0), g1i = fma(dt, gi.x, o.gi1);
-        const double m0 = fma(i00, g0j, i01 * g1j), m1 = fma(i01, g0j, i11 * g1j);
-        Pij = F - fma(g0i, m0, g1i * m1);
-        PF[c.lane] = Pij;
-        asm volatile("" ::: "memory");
-        if constexpr (V != 2 && V != 5) c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
-    };
-    EpOps oa = ub_ops<V>(c, m, N - 1, dw), ob;
-#pragma unroll
-    for (int k = NS - 1; k >= 1; k -= 2) {
-        stage(k, oa, ob, k - 1);
-        stage(k - 1, ob, oa, k >= 2 ? k - 2 : 0);
+        return pd;
     }
-    return pd;
 }
 
 template <int V>
@@ -446,24 +263,13 @@ void check_unaligned() {
 
 int main() {
     using namespace ttmpc;
-    run<9>("real phase_riccati<N=20>");
-    run<0>("copy of the shipped stage");
-    run<1>("no next-stage prefetch");
-    run<2>("no factor-row store");
-    run<5>("no prefetch, no store");
-    run<8>("prefetch as 10 paired reads");
-    run<14>("10 paired reads as read2_b64, odd stride");
-    run<12>("prefetch split: dj+sgu after the P-row reads");
-    run<13>("prefetch all after the P-row reads");
-    run<20>("P row by DPP row_newbcast + readlane");
-    run<21>("20 + PA column by ds_bpermute");
-    run<30>("folded H_uu diagonals, no h11 test");
-    run<31>("30 + adjugate M");
-    run<32>("31 + four-term sums (bound)");
-    run<33>("31 + paired prefetch reads");
-    run<9>("real phase_riccati<N=20> (again)");
-    run<9>("real phase_riccati<N=20> B=256", 256);
-    run<5>("no prefetch, no store B=256", 256);
+    run<9>("phase_riccati<N=20> (input shift, 4-term)");
+    run<50>("round-5 stage (6-term)");
+    run<51>("round-5 stage, no prefetch, no store");
+    run<9>("phase_riccati<N=20> (again)");
+    run<50>("round-5 stage (again)");
+    run<9>("phase_riccati<N=20> B=256", 256);
+    run<50>("round-5 stage B=256", 256);
     check_unaligned();
     check_wred();
     return 0;
