@@ -741,7 +741,7 @@ def main_obca(args):
                 "kernel_only_failures": np.flatnonzero((status > 1) & (stc <= 1)).tolist(),
                 "oracle_only_failures": np.flatnonzero((status <= 1) & (stc > 1)).tolist(),
                 "source": "tests/golden/c4_census.json (oracle/c/tt_obca.c on the same seeded batch)"}
-    traffic, traffic_src = obca_traffic(args.config, float(iters.sum()))
+    traffic, traffic_src, traffic_est = obca_traffic(args.config, float(iters.sum()))
     out = {
         "metric": f"OBCA {'plan' if args.config != 'cobs' else 'MPC+OBCA'} solves/sec (N={N}, M={M} obstacles, "
                   f"n={n} variables; converged or acceptable solves only)",
@@ -764,7 +764,7 @@ def main_obca(args):
         "solver": solver_rec,
         "roofline": {"bound": "valu_fp64", "achieved": round(achieved, 5), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / FP64_PEAK_TFLOPS, 7), "traffic": traffic, "traffic_source": traffic_src,
-                     "traffic_estimated": traffic is not None,
+                     "traffic_estimated": traffic_est,
                      "note": "latency-bound (serial Riccati over N stages per instance, one workgroup per instance); "
                              "flops: SURVEY §8(d) C4 block-arrow formula x per-instance iterations"},
     }
@@ -811,26 +811,35 @@ TRACK_PMC = {"c2": "profiles/r05/final3/pmc_track_c2", "c3": "profiles/r05/final
 TRACK_PMC_SOURCE = "profiles/r05/final3/SOURCE.txt"
 
 
-# committed PMC passes of obca_kernel (tools/obca_pmc.sh, one short probe per config on the shipped kernel): HBM bytes per
-# instance-iteration, scaled by a launch's summed IPM iterations for roofline.traffic of the OBCA lines -- an estimate
-# (the probe's iteration mix is not the full launch's), flagged as such in the line (traffic_estimated)
-OBCA_PMC = {"c4": "profiles/r05/final3/pmc_obca_c4", "c4all": "profiles/r05/final3/pmc_obca_c4all", "cobs": "profiles/r05/final3/pmc_obca_cobs"}
+# committed PMC passes of obca_kernel (FETCH_SIZE and WRITE_SIZE in separate rocprofv3 runs, tools/gpu_session.sh hbm:CFG).
+# c4 (round 6): passes over ONE FULL C4 launch of this bench's own batch -- when this launch ran the same IPM iterations,
+# roofline.traffic is that launch's measured bytes (traffic_estimated false).  c4all / cobs: round-5 300-iteration probes,
+# scaled by the launch's summed iterations (an estimate: the probe's iteration mix is not the full launch's)
+OBCA_PMC = {"c4": "profiles/r06/c4_full_launch", "c4all": "profiles/r05/final3/pmc_obca_c4all",
+            "cobs": "profiles/r05/final3/pmc_obca_cobs"}
 
 
 def obca_traffic(cfg, iters_sum):
+    """-> (HBM bytes per launch, source text, estimated?)"""
     d = OBCA_PMC.get(cfg)
     if d is None or not (REPO / d / "fetch" / "fetch_counter_collection.csv").exists():
-        return None, None
+        return None, None, None
     per_launch = read_traffic([REPO / d / "fetch" / "fetch_counter_collection.csv",
                                REPO / d / "write" / "write_counter_collection.csv"], kernel="obca_kernel")
     rec = json.loads((REPO / d / "fetch.bench.json").read_text())["solver"]
     if per_launch is None:
-        return None, None
-    per_iter = per_launch / (rec["iters_mean"] * rec["instances"])
+        return None, None, None
+    pass_iters = rec["iters_mean"] * rec["instances"]
+    per_iter = per_launch / pass_iters
+    if abs(pass_iters - iters_sum) < 0.5:
+        src = (f"{d}: 2 x FETCH_SIZE + WRITE_SIZE of one full obca_kernel launch of this batch (the same "
+               f"{int(iters_sum)} instance-iterations) = {per_launch / 1e9:.1f} GB, {per_iter / 1e6:.2f} MB per "
+               "instance-iteration")
+        return round(per_launch, 1), src, False
     src = (f"{d}: 2 x FETCH_SIZE + WRITE_SIZE of obca_kernel = {per_launch / 1e9:.1f} GB over "
            f"{rec['instances']} x {rec['iters_mean']:.2f} instance-iterations = {per_iter / 1e6:.2f} MB per "
            f"instance-iteration, x this launch's {int(iters_sum)} instance-iterations")
-    return round(per_iter * iters_sum, 1), src
+    return round(per_iter * iters_sum, 1), src, True
 
 
 def read_traffic(paths, kernel="track_kernel"):

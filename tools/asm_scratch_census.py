@@ -87,3 +87,52 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def frame_split(path):
+    """Per function: (prologue stores, in-body stores, in-body loads, epilogue loads), each in B/lane.  The prologue is
+    the run of scratch stores (and s_/v_writelane/v_accvgpr bookkeeping) before the first other vector instruction;
+    the epilogue the run of scratch loads before the function's last s_setpc_b64."""
+    out = {}
+    cur, body = None, []
+    for line in open(path):
+        m = re.match(r"^([A-Za-z_.$][\w.$]*):\s*(;.*)?$", line)
+        if m and not m.group(1).startswith("."):
+            cur, body = m.group(1), []
+            continue
+        if cur and re.match(r"^\s*\.size\s+" + re.escape(cur) + r",", line):
+            ins = [ln.strip() for ln in body if ln.strip() and not ln.strip().startswith((";", ".", "//"))
+                   and not ln.strip().endswith(":")]
+            nb = lambda i: BYTES.get(re.match(r"scratch_\w+?_(\w+)", i).group(1), 4)  # noqa: E731
+            pro = epi = st = ld = 0
+            k = 0
+            while k < len(ins) and (ins[k].startswith(("scratch_store", "s_", "v_writelane", "v_accvgpr_read",
+                                                        "v_mov_b32"))):
+                if ins[k].startswith("scratch_store"):
+                    pro += nb(ins[k])
+                k += 1
+            last = max((i for i, s in enumerate(ins) if s.startswith("s_setpc_b64")), default=len(ins))
+            e = last - 1
+            while e > k and ins[e].startswith(("scratch_load", "s_", "v_readlane", "v_accvgpr_write")):
+                if ins[e].startswith("scratch_load"):
+                    epi += nb(ins[e])
+                e -= 1
+            for s in ins[k:e + 1]:
+                if s.startswith("scratch_store"):
+                    st += nb(s)
+                elif s.startswith("scratch_load"):
+                    ld += nb(s)
+            out[cur] = (pro, st, ld, epi)
+            cur, body = None, []
+            continue
+        if cur:
+            body.append(line.rstrip())
+    return out
+
+
+if __name__ == "__main__" and "--prologue" in sys.argv:
+    print(f"\n{'function':70s} {'prologue st':>11s} {'body st':>8s} {'body ld':>8s} {'epilogue ld':>11s}  (B/lane)")
+    for f, (pro, st, ld, epi) in sorted(frame_split(sys.argv[1]).items(), key=lambda kv: -sum(kv[1])):
+        if pro + st + ld + epi:
+            name = re.sub(r"ttmpc::\(anonymous namespace\)::", "", demangle(f))[:70]
+            print(f"{name:70s} {pro:11d} {st:8d} {ld:8d} {epi:11d}")
