@@ -14,6 +14,9 @@
 #   hbm:CFG[:ARGS]           FETCH_SIZE and WRITE_SIZE passes of bench CFG (separate runs) -> OUT/pmc_CFG/{fetch,write}
 #   ubench:NAME              tools/bin/ubench_NAME (built on the CPU side) -> OUT/ubench_NAME.txt
 #   py:SCRIPT[:ARGS]         python -u SCRIPT ARGS (diagnostic tools, e.g. tools/obca_tail.py) -> OUT/py_<script>.txt
+#   pmcpy:NAME:CTR[,CTR]:SCRIPT[:ARGS]  one rocprofv3 --pmc pass over python3 SCRIPT ARGS -> OUT/pmcpy/NAME/ (+ run.json:
+#                            the script's JSON stdout line)
+#   listpmc                  rocprofv3 -L (the counters this box offers) -> OUT/counters.txt
 set -o pipefail
 OUT=${1:?usage: gpu_session.sh OUTDIR STEP...}
 shift
@@ -76,6 +79,16 @@ for step in "$@"; do
       f="$OUT/py_$(basename "$a1" .py).txt"
       timeout -k 10 600 python -u "$a1" $(args "$a2") > "$f" 2>&1 || fail "$step" "$f"
       tail -30 "$f" ;;
+    pmcpy)
+      d="$OUT/pmcpy/$a1"
+      mkdir -p "$d"
+      timeout -s KILL 400 rocprofv3 --pmc $(args "$a2") --kernel-trace -d "$d" -o "$a1" --output-format csv \
+        -- python3 "$a3" $(args "$a4") > "$d.log" 2>&1 || fail "$step" "$d.log"
+      grep "^{" "$d.log" > "$d/run.json"
+      cat "$d/run.json" ;;
+    listpmc)
+      timeout -s KILL 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || fail "$step" "$OUT/counters.txt"
+      wc -l "$OUT/counters.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
