@@ -17,6 +17,7 @@
 #   pmcpy:NAME:CTR[,CTR]:SCRIPT[:ARGS]  one rocprofv3 --pmc pass over python3 SCRIPT ARGS -> OUT/pmcpy/NAME/ (+ run.json:
 #                            the script's JSON stdout line)
 #   listpmc                  rocprofv3 -L (the counters this box offers) -> OUT/counters.txt
+#   abobca:N1=SO1,N2=SO2..   tools/ab_obca.sh: bitwise OBCA dumps against the first build + c4 phase stamps -> OUT/obca/
 set -o pipefail
 OUT=${1:?usage: gpu_session.sh OUTDIR STEP...}
 shift
@@ -86,6 +87,9 @@ for step in "$@"; do
         -- python3 "$a3" $(args "$a4") > "$d.log" 2>&1 || fail "$step" "$d.log"
       grep "^{" "$d.log" > "$d/run.json"
       cat "$d/run.json" ;;
+    abobca)
+      timeout -k 10 900 bash tools/ab_obca.sh "$OUT/obca" ${a1//,/ } > "$OUT/obca_ab.txt" 2>&1 || fail "$step" "$OUT/obca_ab.txt"
+      grep -E "bitwise|identical|differ|TOTAL|total|iters" "$OUT/obca_ab.txt" | head -40 ;;
     listpmc)
       timeout -s KILL 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || fail "$step" "$OUT/counters.txt"
       wc -l "$OUT/counters.txt" ;;

@@ -3,6 +3,7 @@
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d OUT/fetch -o fetch --output-format csv -- python3 tools/obca_tail_traffic.py run 4000 5000
     (the same with WRITE_SIZE, and with any other counter group, each pass in its own run)
     python tools/obca_tail_traffic.py report OUT
+    (run K1 K2 0: the same without helper workgroups, ttx_obca_set_helpers)
 
 `run` solves the bench's C4 batch (bench.py's seed 7, B = 256) twice, stopped at max_iter K1 and K2 (plain solves: no
 stamps), and writes the per-instance iterations of both to OUT-independent stdout as one JSON line.  The difference of the
@@ -19,7 +20,7 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO), str(REPO / "car-trailer-mpc_amd")]
 
 
-def run(K1, K2):
+def run(K1, K2, nhelp=-1):
     import numpy as np
     import ttmpc
     from ttmpc import scenarios as sc
@@ -31,10 +32,11 @@ def run(K1, K2):
     for K in (K1, K2):
         s = ttmpc.ObcaSolver(200, sc.OBCA_PARAMS, sc.OBCA_Q, sc.OBCA_R, sc.OBCA_XLB, sc.OBCA_XUB, sc.OBCA_ULB,
                              sc.OBCA_UUB, obs, max_iter=K)
+        s.set_helpers(nhelp)
         X, U, Z, st, it, kk = s.solve(x0, xg, z_guess=zg)
         its.append(it.astype(np.int64))
     d = its[1] - its[0]
-    print(json.dumps({"K1": K1, "K2": K2, "iters_K1": int(its[0].sum()), "iters_K2": int(its[1].sum()),
+    print(json.dumps({"K1": K1, "K2": K2, "helpers": nhelp, "iters_K1": int(its[0].sum()), "iters_K2": int(its[1].sum()),
                       "tail_instance_iterations": int(d.sum()), "tail_instances": int((d > 0).sum())}))
 
 
@@ -60,6 +62,6 @@ def report(out):
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
-        run(int(sys.argv[2]), int(sys.argv[3]))
+        run(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else -1)
     else:
         report(sys.argv[2])
