@@ -336,6 +336,33 @@ def c4_census_compare(st, X, cen, Xc):
             "rounding_sensitive": int(sens.sum())}
 
 
+def _objective(X, U, xg):
+    """The plan-mode objective (trajectory_optimization.py:170-190; Q = I, R = 10 I, 100 Q terminal): the same formula as
+    tests/golden/make_c4_census.py plan_objective, per instance."""
+    from ttmpc import scenarios as sc
+    Q, R = np.asarray(sc.OBCA_Q, float), np.asarray(sc.OBCA_R, float)
+    E = X - xg[:, None, :]
+    return (np.einsum("bki,ij,bkj->b", U, R, U) + np.einsum("bki,ij,bkj->b", E[:, :-1], Q, E[:, :-1])
+            + 100.0 * np.einsum("bi,ij,bj->b", E[:, -1], Q, E[:, -1]))
+
+
+def c4_objective_compare(st, X, U, xg, cen):
+    """For every instance where the GPU and the oracle both converge but to different points (a rounding-sensitive
+    instance of the nonconvex NLP), the GPU objective against the oracle's, and against the spread of the oracle's own
+    objectives over its one-ulp-perturbed runs (the perturbed runs that converged).  Returns the per-instance table and the
+    signed relative differences."""
+    Jg = _objective(X, U, xg)
+    Jo = np.asarray(cen["objective"])
+    stc = np.asarray(cen["status"])
+    rows = []
+    for b in np.flatnonzero((st <= 1) & (stc <= 1)):
+        pert = [p["objective"][b] for p in cen["perturbed"] if p["status"][b] <= 1]
+        rows.append({"instance": int(b), "gpu": float(Jg[b]), "oracle": float(Jo[b]),
+                     "rel": float((Jg[b] - Jo[b]) / Jo[b]),
+                     "oracle_perturbed_rel": [float((v - Jo[b]) / Jo[b]) for v in pert]})
+    return rows
+
+
 def test_c4_full_batch_properties_and_determinism():
     """BASELINE config C4 at full size: B=256 test_cases.json scenarios, N=200, M=6, max_iter 5000, compared instance by
     instance with the oracle's census of the same batch.  Where the GPU's status differs from the
@@ -374,6 +401,75 @@ def test_c4_full_batch_properties_and_determinism():
     assert np.abs(X[ok, 0] - x0[ok]).max() <= 1e-8
     assert np.abs(X[ok, -1] - xg[ok]).max() <= 1e-2 + 1e-7               # final box
     assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
+    _assert_other_optima_unbiased(st, X, U, xg, cen, Xc)
+
+
+def _assert_other_optima_unbiased(st, X, U, xg, cen, Xc):
+    """on the both-converged pairs that end at different local optima, the GPU's optimum must not be
+    systematically worse than the oracle's.  How far apart two legitimate runs of the restated IPOPT end is measured on
+    the oracle itself, under one-ulp perturbations of its guess (up to 2x in objective on this nonconvex NLP).  Each GPU
+    objective may be lower than the oracle's by any amount, and higher by at most the largest increase the oracle's own
+    perturbed runs show on that instance plus 5 %; over all such pairs the mean signed relative difference must be
+    <= +5 % (measured on the bench batch: 37 pairs, the GPU lower on 23, mean -5.2 %, median -0.3 %)."""
+    import json
+    rows = c4_objective_compare(st, X, U, xg, cen)
+    d = np.abs(X - Xc).max(axis=(1, 2))
+    far = [r for r in rows if d[r["instance"]] > 1e-6]
+    same = [r for r in rows if d[r["instance"]] <= 1e-6]
+    print("C4 other-optimum objectives:", json.dumps(far))
+    assert all(abs(r["rel"]) <= 1e-7 for r in same), same     # the same end point: the same objective
+    for r in far:
+        assert r["rel"] <= max([0.0] + r["oracle_perturbed_rel"]) + 0.05, r
+    if far:
+        assert float(np.mean([r["rel"] for r in far])) <= 0.05, far
+
+
+def _kernel_sensitive(s, x0, xg, zg, st, X):
+    """The kernel's own rounding sensitivity (tools/obca_gpu_sensitivity.py): the batch re-solved with the guess scaled
+    by the census factors; an instance is kernel-sensitive when a perturbed run changes its status, or moves a converged
+    end point by more than 1e-6 -- the experiment of tests/golden/make_c4_census.py, on the GPU."""
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    from make_c4_census import PERTURB
+    sens = np.zeros(len(st), dtype=bool)
+    for f in PERTURB:
+        Xp, Up, Zp, stp, itp, kkp = s.solve(x0, xg, z_guess=zg * f)
+        sens |= (stp != st) | ((st <= 1) & (np.abs(Xp - X).max(axis=(1, 2)) > 1e-6))
+    return sens
+
+
+def test_c4_bench_batch_against_census():
+    """The bench's own C4 batch (bench.py --config c4: B = 256, seed 7, the collision-free cases) instance by instance
+    against the oracle census of that batch with THREE one-ulp-class perturbations (tests/golden/make_c4_census.py,
+    VERDICT r5 item 1): equal status and the same end point on every instance whose oracle outcome is not
+    rounding-sensitive; every GPU-optimal end point passes IPOPT's convergence test at the oracle's evaluation; the
+    other-optimum pairs are not biased against the GPU."""
+    import json
+    from ttmpc import collision
+    from ttmpc import scenarios as sc
+    cases = json.loads((GOLDEN / "test_cases.json").read_text())["cases"]
+    obs = sc.obstacles_array(sc.load_obstacles(GOLDEN / "obstacles.json"))[:6]
+    x0, xg, zg = sc.obca_case_batch(cases, 256, 200, 6, seed=7, obstacles=obs, params=sc.OBCA_PARAMS)
+    s = _solver(200, obs)
+    X, U, Z, st, it, kk, I = s.solve(x0, xg, z_guess=zg, iterate=True)
+    _ipopt_check_at_gpu_points(_oracle(200, obs), x0, I, st, kk, x_goal=xg)
+    cen = json.loads((GOLDEN / "c4_census.json").read_text())["bench"]
+    Xc = np.load(GOLDEN / "c4_census_bench_x.npz")["X"]
+    assert len(cen["perturbed"]) == 3 and not np.any(cen["blocked"])
+    tab = c4_census_compare(st, X, cen, Xc)
+    print("C4 bench-batch census comparison:", json.dumps(tab))
+    # Two instances (28: the kernel at max_iter, 168: acceptable instead of optimal) disagree although the oracle's outcome
+    # is robust under its three perturbations.  Both are rounding-decided on the kernel's side: the kernel's OWN perturbed
+    # runs converge on 28 (1,723-1,971 iterations) and reach the optimum on 168 (DESIGN.md section 5, round 6), and the
+    # oracle built with FMA contraction (make -C oracle fma) needs 1,824 iterations on 28 instead of 983.  So a disagreement
+    # must be rounding-sensitive on one side or the other.
+    ksens = _kernel_sensitive(s, x0, xg, zg, st, X)
+    print("kernel-sensitive:", np.flatnonzero(ksens).tolist())
+    assert set(tab["status_mismatch_not_sensitive"]) <= set(np.flatnonzero(ksens).tolist()), tab
+    assert set(tab["other_point_not_sensitive"]) <= set(np.flatnonzero(ksens).tolist()), tab
+    ok = st <= 1
+    assert np.all(collision.sat_gap(X[ok], P6, obs).min(axis=(-1, -2, -3)) > 0.0)
+    _assert_other_optima_unbiased(st, X, U, xg, cen, Xc)
 
 
 def test_default_plan_matches_oracle():
