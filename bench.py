@@ -741,6 +741,14 @@ def main_obca(args):
                 "kernel_only_failures": np.flatnonzero((status > 1) & (stc <= 1)).tolist(),
                 "oracle_only_failures": np.flatnonzero((status <= 1) & (stc > 1)).tolist(),
                 "source": "tests/golden/c4_census.json (oracle/c/tt_obca.c on the same seeded batch)"}
+            if "rounding_sensitive" in cen:
+                # round 6: the census re-solves the batch under three one-ulp-class perturbations of the guess; a status
+                # disagreement on an instance whose oracle outcome does not move under them was checked against the
+                # kernel's own perturbed runs (tests/test_gpu_obca.py::test_c4_bench_batch_against_census)
+                sens = np.asarray(cen["rounding_sensitive"], dtype=bool)
+                solver_rec["oracle_census"]["oracle_rounding_sensitive"] = int(sens.sum())
+                solver_rec["oracle_census"]["status_mismatch_not_oracle_sensitive"] = \
+                    np.flatnonzero((status != stc) & ~sens).tolist()
     traffic, traffic_src, traffic_est = obca_traffic(args.config, float(iters.sum()))
     out = {
         "metric": f"OBCA {'plan' if args.config != 'cobs' else 'MPC+OBCA'} solves/sec (N={N}, M={M} obstacles, "
@@ -807,16 +815,16 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 
 # rocprofv3 PMC passes (tools/hbm_passes.sh) that the default C2 / C3 lines quote as roofline.traffic: the kernel
 # the bench runs; re-profile after a tracking-kernel change
-TRACK_PMC = {"c2": "profiles/r05/final3/pmc_track_c2", "c3": "profiles/r05/final3/pmc_track_c3"}
-TRACK_PMC_SOURCE = "profiles/r05/final3/SOURCE.txt"
+TRACK_PMC = {"c2": "profiles/r06/final/pmc_track_c2", "c3": "profiles/r06/final/pmc_track_c3"}
+TRACK_PMC_SOURCE = "profiles/r06/final/SOURCE.txt"
 
 
 # committed PMC passes of obca_kernel (FETCH_SIZE and WRITE_SIZE in separate rocprofv3 runs, tools/gpu_session.sh hbm:CFG).
-# c4 (round 6): passes over ONE FULL C4 launch of this bench's own batch -- when this launch ran the same IPM iterations,
-# roofline.traffic is that launch's measured bytes (traffic_estimated false).  c4all / cobs: round-5 300-iteration probes,
-# scaled by the launch's summed iterations (an estimate: the probe's iteration mix is not the full launch's)
-OBCA_PMC = {"c4": "profiles/r06/c4_full_launch", "c4all": "profiles/r05/final3/pmc_obca_c4all",
-            "cobs": "profiles/r05/final3/pmc_obca_cobs"}
+# Round 6: passes over ONE FULL launch of each config's own bench batch -- when a launch runs the same IPM iterations
+# (deterministic: it does), roofline.traffic is that launch's measured bytes (traffic_estimated false); otherwise the
+# pass's bytes per instance-iteration are scaled by the launch's summed iterations (traffic_estimated true)
+OBCA_PMC = {"c4": "profiles/r06/final/pmc_obca_c4", "c4all": "profiles/r06/final/pmc_obca_c4all",
+            "cobs": "profiles/r06/final/pmc_obca_cobs"}
 
 
 def obca_traffic(cfg, iters_sum):

@@ -40,6 +40,7 @@ for step in "$@"; do
       cat "$OUT/smoke.log" ;;
     bench)
       j="$OUT/bench_$a1.json"
+      n=2; while [ -e "$j" ]; do j="$OUT/bench_${a1}_$n.json"; n=$((n + 1)); done
       timeout -k 10 600 python -u bench.py --config "$a1" $(args "$a2") > "$j" 2> "${j%.json}.err" || fail "$step" "${j%.json}.err"
       cat "$j" ;;
     ab)
@@ -55,6 +56,7 @@ for step in "$@"; do
       done ;;
     prof)
       d="$OUT/prof_$a1"
+      n=2; while [ -e "$d" ]; do d="$OUT/prof_${a1}_$n"; n=$((n + 1)); done
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$d" -o run --output-format csv \
         -- python3 bench.py --config "$a1" --cpu-budget 0 --no-latency $(args "$a2") > "$d.log" 2>&1 || fail "$step" "$d.log"
       find "$d" -name '*kernel_stats.csv' -exec head -4 {} \; ;;
