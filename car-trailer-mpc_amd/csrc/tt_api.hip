@@ -7,6 +7,7 @@
 #include <errno.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -31,9 +32,10 @@ struct Handle {
     double *d_xo = nullptr, *d_uo = nullptr, *d_kkt = nullptr;
     int *d_st = nullptr, *d_it = nullptr;
     // tracking host calls: one packed device input / output block and its pinned host mirror, so a
-    // host-pointer solve is one H2D, the launch and one D2H (bytes)
+    // host-pointer solve is one H2D, the launch and one D2H (bytes).  The mirror is coherent (fine-grained) pinned
+    // memory: small batches skip both copies and let the kernel read and write it in place (zd_*: its device view)
     size_t stage_in = 0, stage_out = 0;
-    char *d_sin = nullptr, *d_sout = nullptr, *h_sin = nullptr, *h_sout = nullptr;
+    char *d_sin = nullptr, *d_sout = nullptr, *h_sin = nullptr, *h_sout = nullptr, *zd_sin = nullptr, *zd_sout = nullptr;
     std::string err;
     unsigned long long* obca_stamps = nullptr;  // diagnostics: per-phase clocks (ttx_obca_set_stamps)
     unsigned long long* d_board = nullptr;      // OBCA helper-workgroup board, (ocap + 1) lines
@@ -91,7 +93,7 @@ void free_stage(Handle* h) {
     if (h->d_sout) (void)hipFree(h->d_sout);
     if (h->h_sin) (void)hipHostFree(h->h_sin);
     if (h->h_sout) (void)hipHostFree(h->h_sout);
-    h->d_sin = h->d_sout = h->h_sin = h->h_sout = nullptr;
+    h->d_sin = h->d_sout = h->h_sin = h->h_sout = h->zd_sin = h->zd_sout = nullptr;
     h->stage_in = h->stage_out = 0;
 }
 
@@ -100,8 +102,13 @@ int ensure_stage(Handle* h, size_t in_bytes, size_t out_bytes) {
     free_stage(h);
     hipError_t e = hipMalloc((void**)&h->d_sin, in_bytes);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_sout, out_bytes);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sin, in_bytes, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sout, out_bytes, hipHostMallocDefault);
+    // coherent: the GPU does not cache these pages, so a kernel reading the mirror in place sees this call's inputs
+    // (not an L2 copy of the previous call's) and its output stores are in host memory when the stream completes
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sin, in_bytes, fl);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sout, out_bytes, fl);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->zd_sin, h->h_sin, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->zd_sout, h->h_sout, 0);
     if (e != hipSuccess) {
         free_stage(h);
         return fail(h, -ENOMEM, "staging allocation failed (%s bytes)", std::to_string(in_bytes + out_bytes).c_str());
@@ -109,6 +116,17 @@ int ensure_stage(Handle* h, size_t in_bytes, size_t out_bytes) {
     h->stage_in = in_bytes;
     h->stage_out = out_bytes;
     return 0;
+}
+
+// Largest batch a host-pointer tracking solve runs zero-copy (the kernel reads its inputs from and writes its outputs
+// to the coherent pinned mirror; no H2D / D2H on the stream).  Only where the kernel reads its inputs once, at load
+// (N < 64: the reference window lives in registers, tt_track.hip regref).  TT_ZERO_COPY_MAX overrides (0: off).
+int zero_copy_max() {
+    static const int v = [] {
+        const char* e = getenv("TT_ZERO_COPY_MAX");
+        return e ? atoi(e) : 64;
+    }();
+    return v;
 }
 
 bool is_obca(const tt_config& c) { return c.variant == TT_VARIANT_TRACK_OBCA || c.variant == TT_VARIANT_OBCA_PLAN; }
@@ -334,18 +352,22 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
     const size_t nxo = b * (N + 1) * 6, nuo = b * N * 2, out_d = nxo + nuo + b + b;  // 2 x int32 per instance = 1 double
     int rc = ensure_stage(h, in_d * 8, out_d * 8);
     if (rc) return rc;
+    // zero-copy for small batches (B = 1 latency: the two DMA copies cost more than the kernel's few PCIe reads)
+    const bool zc = B <= zero_copy_max() && N < 64;
     double* hin = reinterpret_cast<double*>(h->h_sin);
     const double* dptr[5];
     size_t off = 0;
     for (int a = 0; a < 5; ++a) {
         if (sizes[a]) memcpy(hin + off, srcs[a], sizes[a] * 8);
-        dptr[a] = reinterpret_cast<const double*>(h->d_sin) + off;
+        dptr[a] = reinterpret_cast<const double*>(zc ? h->zd_sin : h->d_sin) + off;
         off += sizes[a];
     }
     hipStream_t s = h->stream;
-    e = hipMemcpyAsync(h->d_sin, h->h_sin, in_d * 8, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(h, e, "H2D copy");
-    double* dxo = reinterpret_cast<double*>(h->d_sout);
+    if (!zc) {
+        e = hipMemcpyAsync(h->d_sin, h->h_sin, in_d * 8, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return hip_fail(h, e, "H2D copy");
+    }
+    double* dxo = reinterpret_cast<double*>(zc ? h->zd_sout : h->d_sout);
     double* duo = dxo + nxo;
     double* dkk = duo + nuo;
     int* dst = reinterpret_cast<int*>(dkk + b);
@@ -356,7 +378,7 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
         (void)hipStreamSynchronize(s);  // the H2D from the pinned staging buffer may still be in flight
         return rc;
     }
-    e = hipMemcpyAsync(h->h_sout, h->d_sout, out_d * 8, hipMemcpyDeviceToHost, s);
+    e = zc ? hipSuccess : hipMemcpyAsync(h->h_sout, h->d_sout, out_d * 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(h, e, "solve");
     const double* ho = reinterpret_cast<const double*>(h->h_sout);

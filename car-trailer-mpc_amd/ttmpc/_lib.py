@@ -211,10 +211,55 @@ class BatchSolver:
     def _err(self, rc, what):
         raise TTError(f"{what} failed ({rc}): {self._L.tt_last_error(self._h).decode()}")
 
+    # Small host calls (the reference's one-instance-per-step controllers) reuse per-shape arrays whose ctypes pointers
+    # were made once: building ten pointers per call cost more wall clock than the copies they avoid.
+    _SMALL_B = 64
+
+    def _small_call(self, B, x0, xref, uref, wq_wr, z_guess):
+        N = self.N
+        ins = [(x0, (B, 6), B * 6), (xref, (B, N + 1, 6), B * (N + 1) * 6), (uref, (B, N, 2), B * N * 2)]
+        if wq_wr is not None:
+            ins.append((wq_wr, (B, 8), B * 8))
+        if z_guess is not None:
+            ins.append((z_guess, (B, 8 * N + 6), B * (8 * N + 6)))
+        arrs = []
+        for a, _, n in ins:
+            a = np.asarray(a, dtype=np.float64)
+            if a.size != n:
+                return None  # the general path raises the shape error
+            arrs.append(a)
+        key = (B, wq_wr is not None, z_guess is not None)
+        cache = self.__dict__.setdefault("_small", {})
+        ent = cache.get(key)
+        if ent is None:
+            if len(cache) >= 8:
+                cache.clear()
+            bufs = [np.empty(shp) for _, shp, _ in ins]
+            outs = (np.empty((B, N + 1, 6)), np.empty((B, N, 2)), np.empty(B, dtype=np.int32),
+                    np.empty(B, dtype=np.int32), np.empty(B))
+            p = [_ptr(b) for b in bufs[:3]]
+            p += [_ptr(bufs[3]) if wq_wr is not None else None]
+            p += [_ptr(bufs[-1]) if z_guess is not None else None]
+            p += [_ptr(outs[0]), _ptr(outs[1]), outs[2].ctypes.data_as(_ip), outs[3].ctypes.data_as(_ip), _ptr(outs[4])]
+            ent = cache[key] = (bufs, outs, tuple(p))
+        bufs, outs, p = ent
+        for b, a in zip(bufs, arrs):
+            np.copyto(b, a.reshape(b.shape))
+        rc = self._L.tt_solve_batch(self._h, B, *p)
+        if rc != 0:
+            self._err(rc, "tt_solve_batch")
+        return tuple(o.copy() for o in outs)
+
     def solve(self, x0, xref, uref, wq_wr=None, z_guess=None):
         """Host arrays: x0 (B,6), xref (B,N+1,6), uref (B,N,2), wq_wr (B,8)|None, z_guess (B,8N+6)|None.
         Returns (X (B,N+1,6), U (B,N,2), status (B,), iters (B,), kkt (B,))."""
         N = self.N
+        x0a = np.asarray(x0)
+        B = x0a.shape[0] if x0a.ndim == 2 else 1
+        if 0 < B <= self._SMALL_B:
+            r = self._small_call(B, x0a, xref, uref, wq_wr, z_guess)
+            if r is not None:
+                return r
         x0 = _f64(x0)
         B = x0.shape[0] if x0.ndim == 2 else 1
         x0 = x0.reshape(B, 6)

@@ -190,6 +190,30 @@ def test_device_pointer_entry_point_with_torch():
     assert np.array_equal(st.cpu().numpy(), sth)
 
 
+def test_small_host_batches_zero_copy_match_the_device_path():
+    """Host calls with B <= 64 at N < 64 run zero-copy (the kernel reads and writes the coherent pinned staging block,
+    tt_api.hip zero_copy_max); B = 65 and N = 64 go through the staged copies.  Every size must give bitwise the
+    device-buffer results, and back-to-back calls on one handle must each see their own inputs (no stale pages)."""
+    import torch
+    from ttmpc.scenarios import synthetic_batch
+    for N in (20, 64):
+        x0, xr, ur = synthetic_batch(70, N, seed=47)
+        s = _gpu_solver(N)
+        dev = torch.device("cuda", s.device)
+        tx0, txr, tur = (torch.from_numpy(a).to(dev) for a in (x0, xr, ur))
+        X = torch.empty((70, N + 1, 6), dtype=torch.float64, device=dev)
+        U = torch.empty((70, N, 2), dtype=torch.float64, device=dev)
+        st = torch.empty(70, dtype=torch.int32, device=dev)
+        s.solve_device(70, tx0.data_ptr(), txr.data_ptr(), tur.data_ptr(), X.data_ptr(), U.data_ptr(), st.data_ptr(),
+                       stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        Xd, Ud, std = X.cpu().numpy(), U.cpu().numpy(), st.cpu().numpy()
+        for lo, B in ((0, 1), (1, 1), (0, 1), (3, 5), (0, 64), (2, 64), (0, 65), (5, 1)):
+            Xh, Uh, sth, _, _ = s.solve(x0[lo:lo + B], xr[lo:lo + B], ur[lo:lo + B])
+            assert np.array_equal(Xh, Xd[lo:lo + B]) and np.array_equal(Uh, Ud[lo:lo + B]), (N, lo, B)
+            assert np.array_equal(sth, std[lo:lo + B]), (N, lo, B)
+
+
 def test_reference_call_surface():
     """MPCTrackingControl / TruckTrailerNMPC / MPCTrackingControlFuzzy as the reference drivers use them."""
     import ttmpc
