@@ -212,6 +212,31 @@ def test_small_host_batches_zero_copy_match_the_device_path():
             Xh, Uh, sth, _, _ = s.solve(x0[lo:lo + B], xr[lo:lo + B], ur[lo:lo + B])
             assert np.array_equal(Xh, Xd[lo:lo + B]) and np.array_equal(Uh, Ud[lo:lo + B]), (N, lo, B)
             assert np.array_equal(sth, std[lo:lo + B]), (N, lo, B)
+    # the optional inputs travel in the same staging block: a warm-start guess (B = 1 and 64) and fuzzy weights
+    import ttmpc
+    from ttmpc import layout
+    N = 20
+    x0, xr, ur = synthetic_batch(64, N, seed=48)
+    zg = layout.pack(xr + 0.01, ur)
+    wq = 1.0 + 0.5 * np.random.default_rng(3).random((64, 8))
+    for variant, kw in ((ttmpc.TT_VARIANT_TRACK, {"z_guess": zg}), (ttmpc.TT_VARIANT_FUZZY, {"wq_wr": wq})):
+        s = _gpu_solver(N, variant=variant)
+        dev = torch.device("cuda", s.device)
+        td = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+              for k, v in (("x0", x0), ("xr", xr), ("ur", ur), ("zg", zg), ("wq", wq))}
+        X = torch.empty((64, N + 1, 6), dtype=torch.float64, device=dev)
+        U = torch.empty((64, N, 2), dtype=torch.float64, device=dev)
+        st = torch.empty(64, dtype=torch.int32, device=dev)
+        s.solve_device(64, td["x0"].data_ptr(), td["xr"].data_ptr(), td["ur"].data_ptr(), X.data_ptr(), U.data_ptr(),
+                       st.data_ptr(), wq_wr=td["wq"].data_ptr() if "wq_wr" in kw else 0,
+                       z_guess=td["zg"].data_ptr() if "z_guess" in kw else 0,
+                       stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        Xd, Ud = X.cpu().numpy(), U.cpu().numpy()
+        for lo, B in ((0, 1), (7, 1), (0, 64)):
+            sub = {k: v[lo:lo + B] for k, v in kw.items()}
+            Xh, Uh, _, _, _ = s.solve(x0[lo:lo + B], xr[lo:lo + B], ur[lo:lo + B], **sub)
+            assert np.array_equal(Xh, Xd[lo:lo + B]) and np.array_equal(Uh, Ud[lo:lo + B]), (variant, lo, B)
 
 
 def test_reference_call_surface():
