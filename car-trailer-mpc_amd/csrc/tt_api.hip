@@ -53,7 +53,12 @@ struct DeviceGuard {
     hipError_t err;
     explicit DeviceGuard(int device) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        err = hipSetDevice(device);
+        if (prev == device) {
+            prev = -1;  // already current: nothing to switch or restore (a B = 1 call pays neither)
+            err = hipSuccess;
+        } else {
+            err = hipSetDevice(device);
+        }
     }
     ~DeviceGuard() {
         if (prev >= 0) (void)hipSetDevice(prev);
