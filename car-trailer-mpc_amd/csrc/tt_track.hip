@@ -2014,6 +2014,9 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // differently from the one-wave build's and results would depend on B, test_occupancy_build_boundary_n31_n32)
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);
+    // N = 50: the reference's closed-loop horizon (simulation.py), stage-unrolled like C3 (the only build at N = 50 for
+    // every B, so results do not depend on B)
+    if (m == kMaskMPC && d && a.N == 50) return launch<kMaskMPC | kDiagBit, 1, 50>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
     if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);
     return launch<-1>(a, stream);

@@ -47,8 +47,8 @@ def test_golden_optima(golden_opt):
         assert np.max(np.abs(zg - z) / np.maximum(1.0, np.abs(z))) <= 1e-6, tag
 
 
-@pytest.mark.parametrize("N,psi,B", [(20, 0.3, 256), (40, 0.9, 256), (1, 0.3, 64), (63, 0.3, 64), (64, 0.3, 64),
-                                     (70, 0.5, 32)])
+@pytest.mark.parametrize("N,psi,B", [(20, 0.3, 256), (40, 0.9, 256), (50, 0.5, 128), (1, 0.3, 64), (63, 0.3, 64),
+                                     (64, 0.3, 64), (70, 0.5, 32)])
 def test_matches_c_oracle(N, psi, B):
     from ttmpc.scenarios import synthetic_batch
     x0, xr, ur = synthetic_batch(B, N, seed=1000 + N, psi_range=psi)
