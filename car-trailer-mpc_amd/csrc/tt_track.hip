@@ -2010,6 +2010,11 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // at 4096, so the 4096-instance chunks of the sharded C5 path ran one wave per SIMD.
     if (m == kMaskMPC && d && a.N == 20 && a.B > 2048) return launch<kMaskMPC | kDiagBit | kOccBit, 2, 20>(a, stream);
     if (m == kMaskMPC && d && a.N == 20) return launch<kMaskMPC | kDiagBit, 1, 20>(a, stream);
+    // N = 30, the NMPC driver's horizon (simulation_nmpc.py): the same pair of stage-unrolled lane-pair builds as N = 20
+    // (bitwise one another).  Against the generic builds: +30 % at B = 1024, +32 % at B = 8192, where the two-wave
+    // build beats the one-wave one by 3.5 % (profiles/r06/unrolled_n30/)
+    if (m == kMaskMPC && d && a.N == 30 && a.B > 2048) return launch<kMaskMPC | kDiagBit | kOccBit, 2, 30>(a, stream);
+    if (m == kMaskMPC && d && a.N == 30) return launch<kMaskMPC | kDiagBit, 1, 30>(a, stream);
     // (the generic two-wave build keeps the load-first order: its one-stage-per-lane passes would otherwise contract
     // differently from the one-wave build's and results would depend on B, test_occupancy_build_boundary_n31_n32)
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);

@@ -47,8 +47,8 @@ def test_golden_optima(golden_opt):
         assert np.max(np.abs(zg - z) / np.maximum(1.0, np.abs(z))) <= 1e-6, tag
 
 
-@pytest.mark.parametrize("N,psi,B", [(20, 0.3, 256), (40, 0.9, 256), (50, 0.5, 128), (1, 0.3, 64), (63, 0.3, 64),
-                                     (64, 0.3, 64), (70, 0.5, 32)])
+@pytest.mark.parametrize("N,psi,B", [(20, 0.3, 256), (30, 0.5, 256), (40, 0.9, 256), (50, 0.5, 128), (1, 0.3, 64),
+                                     (63, 0.3, 64), (64, 0.3, 64), (70, 0.5, 32)])
 def test_matches_c_oracle(N, psi, B):
     from ttmpc.scenarios import synthetic_batch
     x0, xr, ur = synthetic_batch(B, N, seed=1000 + N, psi_range=psi)
@@ -348,13 +348,14 @@ def test_c5_full_batch_through_the_sharded_path():
     assert np.array_equal(X, X2) and np.array_equal(U, U2) and np.array_equal(st, st2)
 
 
-def test_occupancy_build_is_bitwise_the_latency_build():
-    """Large batches (B > 4096, reference box, diagonal weights, N = 20) launch the two-waves-per-SIMD build of
-    the stage-unrolled NS = 20 kernel, small ones its one-wave build: the same code under a different register
-    budget, so every instance's result is bitwise independent of the batch size (and of the sharded path's chunk
-    size).  Two seeds, 4608 instances each, against 1152-instance batches."""
+@pytest.mark.parametrize("N", [20, 30])
+def test_occupancy_build_is_bitwise_the_latency_build(N):
+    """Large batches (B > 2048, reference box, diagonal weights, N = 20 or the NMPC driver's N = 30) launch the
+    two-waves-per-SIMD build of the stage-unrolled kernel, small ones its one-wave build: the same code under a
+    different register budget, so every instance's result is bitwise independent of the batch size (and of the sharded
+    path's chunk size).  Two seeds, 4608 instances each, against 1152-instance batches."""
     from ttmpc.scenarios import synthetic_batch
-    N, B = 20, 4608
+    B = 4608
     s = _gpu_solver(N)
     for seed in (77, 78):
         x0, xr, ur = synthetic_batch(B, N, seed=seed, psi_range=0.6)
