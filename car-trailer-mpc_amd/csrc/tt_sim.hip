@@ -153,25 +153,43 @@ __device__ __forceinline__ void proj(const Poly& p, double ax, double ay, double
     }
 }
 
-__device__ bool obb_aabb(const Poly& o, double cx, double cy, double hw, double hh) {
+// The oriented body's half of the separating-axis test: its axes (the AABB's two, then its own edge normals) and its
+// projections on them.  Independent of the obstacle, so a pose computes them once per body instead of once per
+// (obstacle, body) pair as check_obb_aabb_collision does; the arithmetic of every value is the reference's.
+struct ObbAxes {
+    double ax[4], ay[4], omin[4], omax[4];
+    int na;
+};
+
+__device__ __forceinline__ void obb_axes(const Poly& o, ObbAxes& r) {
+#pragma clang fp contract(off)
+    r.ax[0] = 1.0; r.ay[0] = 0.0;
+    r.ax[1] = 0.0; r.ay[1] = 1.0;
+    r.ax[2] = r.ax[3] = r.ay[2] = r.ay[3] = 0.0;
+    int na = 2;
+    const double e1x = o.x[1] - o.x[0], e1y = o.y[1] - o.y[0];
+    const double e2x = o.x[3] - o.x[0], e2y = o.y[3] - o.y[0];
+    const double n1 = sqrt(e1x * e1x + e1y * e1y), n2 = sqrt(e2x * e2x + e2y * e2y);
+    if (n1 > 1e-9) { r.ax[na] = -e1y / n1; r.ay[na] = e1x / n1; ++na; }
+    if (n2 > 1e-9) { r.ax[na] = -e2y / n2; r.ay[na] = e2x / n2; ++na; }
+    r.na = na;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < na) proj(o, r.ax[i], r.ay[i], r.omin[i], r.omax[i]);
+}
+
+// check_obb_aabb_collision (simulation.py:224-300) with the body's half precomputed (obb_axes)
+__device__ bool obb_aabb(const ObbAxes& o, double cx, double cy, double hw, double hh) {
 #pragma clang fp contract(off)
     Poly a;
     a.x[0] = cx + hw; a.y[0] = cy + hh;
     a.x[1] = cx + hw; a.y[1] = cy - hh;
     a.x[2] = cx - hw; a.y[2] = cy - hh;
     a.x[3] = cx - hw; a.y[3] = cy + hh;
-    double ax[4] = {1.0, 0.0, 0.0, 0.0}, ay[4] = {0.0, 1.0, 0.0, 0.0};
-    int na = 2;
-    const double e1x = o.x[1] - o.x[0], e1y = o.y[1] - o.y[0];
-    const double e2x = o.x[3] - o.x[0], e2y = o.y[3] - o.y[0];
-    const double n1 = sqrt(e1x * e1x + e1y * e1y), n2 = sqrt(e2x * e2x + e2y * e2y);
-    if (n1 > 1e-9) { ax[na] = -e1y / n1; ay[na] = e1x / n1; ++na; }
-    if (n2 > 1e-9) { ax[na] = -e2y / n2; ay[na] = e2x / n2; ++na; }
-    for (int i = 0; i < na; ++i) {
-        double omin, omax, amin, amax;
-        proj(o, ax[i], ay[i], omin, omax);
-        proj(a, ax[i], ay[i], amin, amax);
-        if (omax < amin || amax < omin) return false;
+    for (int i = 0; i < o.na; ++i) {
+        double amin, amax;
+        proj(a, o.ax[i], o.ay[i], amin, amax);
+        if (o.omax[i] < amin || amax < o.omin[i]) return false;
     }
     return true;
 }
@@ -184,10 +202,13 @@ __device__ bool pose_collides(const double* q, const double* obs, int M, double 
     rect_corners(x + cos(th) * L1 / 2, y + sin(th) * L1 / 2, L1 / 2, W1 / 2, th, v);          // 318-326
     const double hx = x - cos(th) * Mh, hy = y - sin(th) * Mh;                                    // 328-335
     rect_corners(hx - cos(th + ps) * L2 / 2, hy - sin(th + ps) * L2 / 2, L2 / 2, W2 / 2, th + ps, t);
+    ObbAxes va, ta;
+    obb_axes(v, va);
+    obb_axes(t, ta);
     for (int m = 0; m < M; ++m) {
         const double* o = obs + 4 * m;
-        if (obb_aabb(v, o[0], o[1], o[2] / 2, o[3] / 2)) return true;
-        if (obb_aabb(t, o[0], o[1], o[2] / 2, o[3] / 2)) return true;
+        if (obb_aabb(va, o[0], o[1], o[2] / 2, o[3] / 2)) return true;
+        if (obb_aabb(ta, o[0], o[1], o[2] / 2, o[3] / 2)) return true;
     }
     return false;
 }
