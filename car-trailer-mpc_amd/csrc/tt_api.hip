@@ -109,7 +109,7 @@ int ensure_stage(Handle* h, size_t in_bytes, size_t out_bytes) {
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_sout, out_bytes);
     // coherent: the GPU does not cache these pages, so a kernel reading the mirror in place sees this call's inputs
     // (not an L2 copy of the previous call's) and its output stores are in host memory when the stream completes
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable;
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sin, in_bytes, fl);
     if (e == hipSuccess) e = hipHostMalloc((void**)&h->h_sout, out_bytes, fl);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&h->zd_sin, h->h_sin, 0);
