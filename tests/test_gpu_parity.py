@@ -147,9 +147,10 @@ def test_rejects_bad_arguments():
         ttmpc.BatchSolver(10, P, to.DEFAULT_Q, to.DEFAULT_R, to.MPC_XUB, to.MPC_XLB, to.MPC_ULB, to.MPC_UUB)
 
 
-@pytest.mark.parametrize("N,B,psi", [(20, 1024, 0.3), (40, 8192, 0.9)])
+@pytest.mark.parametrize("N,B,psi", [(20, 1024, 0.3), (40, 8192, 0.9), (30, 8192, 0.5), (50, 1024, 0.5)])
 def test_full_size_properties(N, B, psi):
-    """BASELINE configs C2 / C3 at full size: size-independent properties (no oracle at this size)."""
+    """BASELINE configs C2 / C3 at full size, and the stage-unrolled builds of the drivers' other horizons (N = 30
+    two-wave, N = 50): size-independent properties, and a random subsample against the oracle."""
     from oracle import ttmpc_oracle as to
     from ttmpc.scenarios import synthetic_batch
     x0, xr, ur = synthetic_batch(B, N, seed=2024 + N, psi_range=psi)
