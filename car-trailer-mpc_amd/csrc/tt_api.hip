@@ -42,6 +42,9 @@ struct Handle {
     int nhelp = -1;                             // OBCA helper workgroups per launch (-1: one per CU; ttx_obca_set_helpers)
     unsigned long long spin_ticks = 0;          // hand-off spin limit (0: 5 s) and forced-timeout instance (-1: none),
     int fail_b = -1;                            //   ttx_obca_set_handoff_debug
+    // tracking builds that keep stage rows in HBM (the N = 50 build, ttmpc::track_global_bytes): one launch's rows
+    double* d_prow = nullptr;
+    size_t prow_cap = 0;  // bytes
 };
 
 thread_local std::string g_err;
@@ -132,6 +135,23 @@ int zero_copy_max() {
         return e ? atoi(e) : 64;
     }();
     return v;
+}
+
+// the HBM stage rows of a launch (grown only: a larger batch waits for the device before the old block is freed)
+int ensure_prow(Handle* h, size_t bytes) {
+    if (bytes <= h->prow_cap) return 0;
+    if (h->d_prow) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(h->d_prow);
+    }
+    h->d_prow = nullptr;
+    h->prow_cap = 0;
+    if (hipMalloc((void**)&h->d_prow, bytes) != hipSuccess) {
+        h->d_prow = nullptr;
+        return fail(h, -ENOMEM, "stage-row workspace allocation failed (%s bytes)", std::to_string(bytes).c_str());
+    }
+    h->prow_cap = bytes;
+    return 0;
 }
 
 bool is_obca(const tt_config& c) { return c.variant == TT_VARIANT_TRACK_OBCA || c.variant == TT_VARIANT_OBCA_PLAN; }
@@ -321,6 +341,11 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
     a.kkt = d_kkt_res;
     a.status = d_status;
     a.iters = d_iters;
+    if (const size_t gb = ttmpc::track_global_bytes(a)) {
+        const int rc = ensure_prow(h, gb);
+        if (rc) return rc;
+        a.prow = h->d_prow;
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     e = ttmpc::launch_track(a, s);
     if (e != hipSuccess) return hip_fail(h, e, "track kernel launch");
@@ -412,6 +437,11 @@ int ttx_solve_stamped(void* handle, int B, const double* d_x0, const double* d_x
     a.status = d_status;
     a.iters = d_iters;
     a.stamps = d_stamps;
+    if (const size_t gb = ttmpc::track_global_bytes(a)) {
+        const int rc = ensure_prow(h, gb);
+        if (rc) return rc;
+        a.prow = h->d_prow;
+    }
     hipError_t e = ttmpc::launch_track(a, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(h, e, "stamped launch");
 }
@@ -621,6 +651,7 @@ void tt_destroy(void* handle) {
     free_ws(h);
     free_ows(h);
     free_stage(h);
+    if (h->d_prow) (void)hipFree(h->d_prow);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }

@@ -26,6 +26,7 @@ struct TrackArgs {
     int* status;                          // [B]
     int* iters;                           // [B] or nullptr
     unsigned long long* stamps;           // [B][kNumPhases] cycle sums (TT_STAMPS diagnostic build only)
+    double* prow;                         // [B][N+1][kGlobalRows]: the stage rows a build keeps in HBM, or nullptr
 };
 
 // phases timed by the TT_STAMPS diagnostic build
@@ -47,6 +48,12 @@ constexpr int kMaxLdsBytes = 160 * 1024;
 inline int lds_doubles(int N) { return kRowsPerStage * (N + 1) + kScratch; }
 inline int lds_bytes(int N) { return 8 * lds_doubles(N); }
 inline int max_horizon() { return (kMaxLdsBytes / 8 - kScratch) / kRowsPerStage - 1; }
+
+// The N = 50 build keeps the 28 stage rows of the Riccati factor (P, p) and of its overlay (Sigma, dB: linearise ..
+// ric_prep) in HBM instead of LDS: a 40.4 KB record, four instances per CU instead of three (tt_track.hip, round 6).
+constexpr int kGlobalRows = 28;
+// bytes of TrackArgs::prow the launch of `a` needs (0: every stage row stays in LDS)
+size_t track_global_bytes(const TrackArgs& a);
 
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream);
 

@@ -43,6 +43,8 @@
 // BM < 0 = pattern read at run time.
 #include <math.h>
 
+#include <atomic>
+
 #include "tt_kernel.hpp"
 #include "tt_trig.hpp"
 
@@ -50,6 +52,20 @@ namespace ttmpc {
 namespace {
 
 constexpr int W = 64;
+// A stage row kept in HBM (Ctx::kPG builds): raw buffer load / store through the instance's descriptor (SGPRs) with a
+// 32-bit lane offset and a scalar offset -- the access form that needs no 64-bit address registers.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+struct GRow {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned voff, soff;
+    __device__ __forceinline__ operator double() const {
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+    }
+    __device__ __forceinline__ const GRow& operator=(double v) const {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), rs, voff, soff, 0);
+        return *this;
+    }
+};
 constexpr int SR = kRowsPerStage;
 constexpr int HEAD = kHead;
 
@@ -66,6 +82,7 @@ static_assert(HEAD >= SR, "stage -1 of the Riccati prefetch addresses head words
 constexpr int rX = 0, rY = 8, rZL = 14, rZU = 22, rDX = 30, rYP = 38, rAJ = 44, PAD = 53, rGF = 54, rCC = 62, rK = 68;
 constexpr int rKF = 80, rPS = 82, rPV = 104, rDXS = 110;
 static_assert(rDXS + 8 == kRowsPerStage, "stage record");
+static_assert(rDXS - rPS == kGlobalRows, "the HBM band of the kPG builds: P, spare, p (overlay Sigma, dB)");
 // second lives (see the LDS map): curvature, Sigma, dB from the linearisation to the Riccati sweep; the
 // Riccati operands diag(Sigma) + diag(W), Sigma_u and b^ = -c_{k+1} (stage k); the trial residual c
 constexpr int rWC = rDX, rSG = rPS, rDB = rPS + 8, rHD = rDXS, rSGU = rDXS + 6, rBH = rYP, rCT = rDXS;
@@ -256,8 +273,27 @@ struct Ctx {
     int N, lane;
     double dt, iL1, iL2, Mh;
     double mu, tau;
-    __device__ __forceinline__ double& r(int row, int k) const { return sm[HEAD + k * SR + row]; }
+    // bit 18: the build keeps the stage rows rPS .. rDXS-1 (P, spare, p; their overlay Sigma, dB) in HBM (TrackArgs::prow)
+    // and the LDS record shrinks by those kGlobalRows rows: rows from rDXS on sit kGlobalRows lower (the N = 50 build:
+    // 40.4 KB per instance, four per CU instead of three).  Rows of that band are reached through g() only; r() serves
+    // every other row, rl() an LDS row already mapped (lrow) -- in the other builds all three are the same LDS access.
+    static constexpr bool kPG = BM >= 0 && ((BM >> 18) & 1);
+    static constexpr int kSR = kPG ? SR - kGlobalRows : SR;
+    __amdgpu_buffer_rsrc_t prs;  // this instance's HBM rows (kPG builds): a buffer descriptor in SGPRs
+    __device__ __forceinline__ static int lrow(int row) { return kPG && row >= rDXS ? row - kGlobalRows : row; }
+    __device__ __forceinline__ double& r(int row, int k) const { return sm[HEAD + k * kSR + lrow(row)]; }
+    __device__ __forceinline__ double& rl(int lds_row, int k) const { return sm[HEAD + k * kSR + lds_row]; }
     __device__ __forceinline__ double& h(int i) const { return sm[i]; }
+    // g: any stage k (the stage-parallel passes: k = the lane's stage); gu: a wave-uniform stage (the serial sweep's),
+    // whose offset goes to the descriptor's scalar offset so no per-stage address is formed in VGPRs
+    __device__ __forceinline__ decltype(auto) g(int row, int k) const {
+        if constexpr (kPG) return GRow{prs, (unsigned)(k * kGlobalRows + (row - rPS)) * 8u, 0u};
+        else return static_cast<double&>(sm[HEAD + k * SR + row]);
+    }
+    __device__ __forceinline__ decltype(auto) gu(int row, int k) const {
+        if constexpr (kPG) return GRow{prs, (unsigned)(row - rPS) * 8u, (unsigned)(k * kGlobalRows) * 8u};
+        else return static_cast<double&>(sm[HEAD + k * SR + row]);
+    }
     // bit 16 of a specialised bound pattern: Q and R are diagonal (the reference's Q = I, R = 10 I)
     static constexpr bool kDiag = BM >= 0 && ((BM >> 16) & 1);
     // bit 17: the two-waves-per-SIMD build.  The one-wave builds issue every LDS read of a stage-parallel pass before its
@@ -531,8 +567,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
                 const int v = 2 * t + p;
                 if (2 * t >= 6 && k == N) break;
                 c.r(rGF + v, k) = gfv[t];
-                c.r(rSG + v, k) = sgv[t];
-                c.r(rDB + v, k) = dbv[t];
+                c.g(rSG + v, k) = sgv[t];
+                c.g(rDB + v, k) = dbv[t];
             }
             SUBSTAMP(c, 6);
             logs += ls.value();
@@ -655,8 +691,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
             c.r(rGF + v, k) = gfv[v];
-            c.r(rSG + v, k) = sgv[v];
-            c.r(rDB + v, k) = dbv[v];
+            c.g(rSG + v, k) = sgv[v];
+            c.g(rDB + v, k) = dbv[v];
         }
     }
     } else {
@@ -752,8 +788,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
                     db += rs;
                     if (su <= 0.0) bad = true; else ls.add(su);
                 }
-                c.r(rSG + v, k) = sg;
-                c.r(rDB + v, k) = db;
+                c.g(rSG + v, k) = sg;
+                c.g(rDB + v, k) = db;
                 if (!isfinite(g)) fin = false;
                 dinf = fmax(dinf, fabs(g));
             }
@@ -853,8 +889,8 @@ __device__ __forceinline__ Lin phase_linearize(const Ctx<BM>& c) {
                 db += rs;
                 if (s <= 0.0) bad = true; else ls.add(s);
             }
-            c.r(rSG + v, k) = sg;
-            c.r(rDB + v, k) = db;
+            c.g(rSG + v, k) = sg;
+            c.g(rDB + v, k) = db;
             if (!isfinite(g)) fin = false;
             dinf = fmax(dinf, fabs(g));
         }
@@ -894,13 +930,13 @@ constexpr int hPF = 128, hPT = 192;  // P tile (i, j) and transposed PA tile (j,
 // branch-free predicated LDS store: invalid lanes write their own dump slot
 template <int BM>
 __device__ __forceinline__ void pstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
-    c.sm[valid ? HEAD + k * SR + row : hDUMP + (c.lane & 31)] = v;
+    c.sm[valid ? HEAD + k * Ctx<BM>::kSR + row : hDUMP + (c.lane & 31)] = v;
 }
 // exec-masked LDS store: with k a compile-time stage (unrolled sweeps) the address is the lane's row
 // register plus an immediate offset, so the store costs no VALU address arithmetic at all
 template <int BM>
 __device__ __forceinline__ void mstore(const Ctx<BM>& c, bool valid, int row, int k, double v) {
-    if (valid) c.sm[HEAD + k * SR + row] = v;
+    if (valid) c.sm[HEAD + k * Ctx<BM>::kSR + row] = v;
 }
 
 // The input shift of the Newton sweep (round 6).  B = dt [e5 e4]: rows 4, 5 of the dynamics (phi, v)
@@ -943,15 +979,15 @@ __device__ __forceinline__ void phase_ric_prep(const Ctx<BM>& c) {
     for (int k = c.lane; k <= N; k += W) {
         double g[8], hd[6], su0 = 0.0, su1 = 0.0;   // read every source row before the first overlay write
 #pragma unroll
-        for (int v = 0; v < 8; ++v) g[v] = (v >= 6 && k == N) ? 0.0 : c.r(rGF + v, k) + c.mu * c.r(rDB + v, k);
+        for (int v = 0; v < 8; ++v) g[v] = (v >= 6 && k == N) ? 0.0 : c.r(rGF + v, k) + c.mu * c.g(rDB + v, k);
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const int wi = w_idx(i, i);
-            double d = c.r(rSG + i, k);
+            double d = c.g(rSG + i, k);
             if (wi >= 0 && k < N) d += c.r(rWC + wi, k);
             hd[i] = d;
         }
-        if (k < N) { su0 = c.r(rSG + 6, k); su1 = c.r(rSG + 7, k); }
+        if (k < N) { su0 = c.g(rSG + 6, k); su1 = c.g(rSG + 7, k); }
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= 6 && k == N) break;
@@ -1017,19 +1053,19 @@ struct EpOps {
 template <int BM>
 __device__ __forceinline__ void ep_ops_a(const Ctx<BM>& c, const EpMap& m, int k, EpOps& o) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o.dj[t] = c.r(m.dj[t], k);
+    for (int t = 0; t < 4; ++t) o.dj[t] = c.rl(m.dj[t], k);
     o.sgu0 = c.r(rSGU, k);
     o.sgu1 = c.r(rSGU + 1, k);
 }
 template <int BM>
 __device__ __forceinline__ void ep_ops_b(const Ctx<BM>& c, const EpMap& m, int k, double dw, EpOps& o) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o.di[t] = c.r(m.di[t], k);
-    o.h = m.q2 + m.dg * dw + c.r(m.hs, k);
-    o.gj0 = c.r(m.gj0, k);
-    o.gj1 = c.r(m.gj1, k);
-    o.gi0 = c.r(m.gi0, k);
-    o.gi1 = c.r(m.gi1, k);
+    for (int t = 0; t < 4; ++t) o.di[t] = c.rl(m.di[t], k);
+    o.h = m.q2 + m.dg * dw + c.rl(m.hs, k);
+    o.gj0 = c.rl(m.gj0, k);
+    o.gj1 = c.rl(m.gj1, k);
+    o.gi0 = c.rl(m.gi0, k);
+    o.gi1 = c.rl(m.gi1, k);
 }
 template <int BM>
 __device__ __forceinline__ EpOps ep_ops(const Ctx<BM>& c, const EpMap& m, int k, double dw) {
@@ -1049,6 +1085,7 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const int N = c.N, i = c.lane >> 3, j = c.lane & 7;
     EpMap m;
     m.init(i, j, c.sm + hQW);
+    m.hs = Ctx<BM>::lrow(m.hs);  // the operand slots are LDS rows (rl); the factor slot m.ps is a logical row (g)
     const double dt = c.dt, dt2 = dt * dt;
     const double r00 = 2.0 * c.h(hRW), r01 = 2.0 * c.h(hRW + 1), r11 = 2.0 * c.h(hRW + 3);
     double* PF = c.sm + hPF;
@@ -1060,10 +1097,14 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
     const int sw_i = i & 4, sw_j = j & 4;
     const int pf_own = 8 * i + (j ^ sw_i);  // this lane's P^ entry
     // terminal P^_N = H^_N (no dynamics): padded lanes hold exact zeros
-    double Pij = m.q2 + m.dg * dw + c.r(m.hs, N);
+    double Pij = m.q2 + m.dg * dw + c.rl(m.hs, N);
     PF[pf_own] = Pij;
     asm volatile("" ::: "memory");
-    pstore(c, m.ps >= 0, m.ps, N, Pij);
+    if constexpr (Ctx<BM>::kPG) {
+        if (m.ps >= 0) c.gu(m.ps, N) = Pij;
+    } else {
+        pstore(c, m.ps >= 0, m.ps, N, Pij);
+    }
     // inertia flag accumulated without branching: a failed stage only poisons the (discarded) factors
     bool pd = true;
     // The stage's factorisation rows leave in ONE unmasked ds_write per lane (three predicated stores
@@ -1113,7 +1154,12 @@ __device__ __forceinline__ bool phase_riccati(const Ctx<BM>& c, double dw) {
         PF[pf_own] = Pij;
         asm volatile("" ::: "memory");
         // factorisation rows for the forward sweep, the step and the SOC
-        c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
+        if constexpr (Ctx<BM>::kPG) {  // P^ to HBM (the kPG band), K^ rows and the dump row to LDS
+            if (own_p) c.gu(m.ps, k) = Pij;
+            else c.rl(st_row, k) = i == 6 ? -m0 : -m1;
+        } else {
+            c.r(st_row, k) = own_p ? Pij : (i == 6 ? -m0 : -m1);
+        }
     };
     // two stages per trip with ping-pong operand buffers (no register copies between stages)
     EpOps oa = ep_ops(c, m, N - 1, dw), ob;
@@ -1156,43 +1202,46 @@ __device__ __forceinline__ void phase_forward(const Ctx<BM>& c, int crow, int bh
     // output row of this lane's group: 0..5 = dx_{k+1}[g], 6/7 = du0/du1 (rows 7/8 of [Phi; K^])
     const int u = (g == 5 || g == 6) ? 0 : (g == 4 || g == 7) ? 1 : -1;
     const double fone = (g < 6 && mm == g) ? 1.0 : 0.0;
-    // BHN: b^_k = -c_{k+1} read straight from the residual rows of stage k+1 (row SR + crow + g of stage k)
+    // BHN: b^_k = -c_{k+1} read straight from the residual rows of stage k+1 (row kSR + crow + g of stage k)
     // instead of a stored b^ row (the SOC sweep: c_soc lives where its own output dX_soc goes)
     // The Newton sweep (!BHN) runs in the Riccati's shifted input (gu_shift): K^'s affine column is k_ff' = k_ff + s,
     // so the state rows 4, 5 take no b^ term (dt k_ff' carries it) and du = du' - s, with -s = c_{k+1}[(5, 4)] / dt from
     // the residual rows of stage k+1.  The SOC sweep (BHN) runs on the unshifted factors of phase_soc_backward.
     const bool shf = !BHN && mm == 6;
+    // the sweep's row offsets are LDS rows (rl): crow / orow mapped once, the next stage one LDS stride (kSR) ahead
+    constexpr int LSR = Ctx<BM>::kSR;
+    const int crl = Ctx<BM>::lrow(crow), orl = Ctx<BM>::lrow(orow);
     const int fas = (g < 6 && mm < 6 && d_idx(g, mm) >= 0) ? rAJ + d_idx(g, mm)
                   : (shf && (g == 4 || g == 5)) ? PAD
-                  : (shf && g == 6) ? SR + crow + 5 : (shf && g == 7) ? SR + crow + 4
-                  : (g < 6 && mm == 6) ? (BHN ? SR + crow + g : bhrow + g) : PAD;
+                  : (shf && g == 6) ? LSR + crl + 5 : (shf && g == 7) ? LSR + crl + 4
+                  : (g < 6 && mm == 6) ? (BHN ? LSR + crl + g : bhrow + g) : PAD;
     const double fsg = (BHN && g < 6 && mm == 6) ? -1.0 : (shf && g >= 6) ? 1.0 / c.dt : 1.0;
     const int fk = (u >= 0 && mm < 6) ? rK + 6 * u + mm : (u >= 0 && mm == 6) ? rKF + u : PAD;
     const double fkc = u >= 0 ? (g < 6 ? c.dt : 1.0) : 0.0;
     // x^_0[m] = -c_0[m] (m < 6), 1 (m = 6), 0 (m = 7)
-    double x = mm < 6 ? -c.r(crow + mm, 0) : (mm == 6 ? 1.0 : 0.0);
-    if (c.lane < 6) c.r(orow + c.lane, 0) = -c.r(crow + c.lane, 0);
+    double x = mm < 6 ? -c.rl(crl + mm, 0) : (mm == 6 ? 1.0 : 0.0);
+    if (c.lane < 6) c.rl(orl + c.lane, 0) = -c.rl(crl + c.lane, 0);
     const int src = 8 * (mm < 6 ? mm : 0);  // group holding x_{k+1}[mm]
-    double nph = fone + fsg * c.r(fas, 0) + fkc * c.r(fk, 0);
+    double nph = fone + fsg * c.rl(fas, 0) + fkc * c.rl(fk, 0);
     // unrolled builds: one unmasked store per lane and stage.  Lane 8g writes its output (dx_{k+1}[g] or
     // du_k[g-6]); the other 56 lanes write a row that is dead here -- the Hessian diagonal (rHD, consumed
     // by the Riccati) in the Newton sweep, the residual c (rCC, consumed by the SOC right-hand side) in
     // the SOC sweep
-    const int fst = mm == 0 ? (g < 6 ? SR + orow + g : orow + g) : (BHN ? rCC : rHD) + (g % 6);
+    const int fst = mm == 0 ? (g < 6 ? LSR + orl + g : orl + g) : Ctx<BM>::lrow(BHN ? rCC : rHD) + (g % 6);
     auto step = [&](int k) {
         const double ph = nph;
         const int kn = k + 1 < N ? k + 1 : k;
-        nph = fone + fsg * c.r(fas, kn) + fkc * c.r(fk, kn);
+        nph = fone + fsg * c.rl(fas, kn) + fkc * c.rl(fk, kn);
         double y = ph * x;
         y += dppd<0xB1>(y);   // quad_perm [1,0,3,2]
         y += dppd<0x4E>(y);   // quad_perm [2,3,0,1]
         y += dppd<0x141>(y);  // row_half_mirror: the 8-lane group sum, in every lane of the group
         // rows 0..5 -> dx_{k+1}; groups 6/7 -> du0/du1 at stage k
         if constexpr (NS > 0) {
-            c.sm[HEAD + k * SR + fst] = y;
+            c.sm[HEAD + k * LSR + fst] = y;
         } else {
-            pstore(c, mm == 0 && g < 6, orow + g, k + 1, y);
-            pstore(c, mm == 0 && g >= 6, orow + g, k, y);
+            pstore(c, mm == 0 && g < 6, orl + g, k + 1, y);
+            pstore(c, mm == 0 && g >= 6, orl + g, k, y);
         }
         const double xn = bperm_d(y, src);
         x = mm < 6 ? xn : (mm == 6 ? 1.0 : 0.0);
@@ -1226,21 +1275,21 @@ __device__ __forceinline__ void phase_soc_backward(const Ctx<BM>& c, double dw) 
             for (int rr = 0; rr < 6; ++rr) {
                 double s = p[rr];
 #pragma unroll
-                for (int l = 0; l < 6; ++l) s -= c.r(rPS + sym_idx(rr, l), k + 1) * cn[l];
+                for (int l = 0; l < 6; ++l) s -= c.g(rPS + sym_idx(rr, l), k + 1) * cn[l];
                 w[rr] = s;
             }
             const double h0 = c.gr(6, k) + dt * w[5], h1 = c.gr(7, k) + dt * w[4];
             // H_uu^-1 of the Riccati stage (R~ + Sigma_u + dw + dt^2 P_{k+1}[{5,4}]), recomputed
-            const double h00 = r00 + c.r(rSGU, k) + dw + dt2 * c.r(rPS + sym_idx(5, 5), k + 1);
-            const double h01 = r01 + dt2 * c.r(rPS + sym_idx(4, 5), k + 1);
-            const double h11 = r11 + c.r(rSGU + 1, k) + dw + dt2 * c.r(rPS + sym_idx(4, 4), k + 1);
+            const double h00 = r00 + c.r(rSGU, k) + dw + dt2 * c.g(rPS + sym_idx(5, 5), k + 1);
+            const double h01 = r01 + dt2 * c.g(rPS + sym_idx(4, 5), k + 1);
+            const double h11 = r11 + c.r(rSGU + 1, k) + dw + dt2 * c.g(rPS + sym_idx(4, 4), k + 1);
             const double id = frcp(h00 * h11 - h01 * h01), i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
             c.r(rKF, k) = -(i00 * h0 + i01 * h1);
             c.r(rKF + 1, k) = -(i01 * h0 + i11 * h1);
 #pragma unroll
             for (int rr = 0; rr < 6; ++rr) {
                 p[rr] = c.gr(rr, k) + w[rr] + colJ(aj, rr, w, 1) + c.r(rK + rr, k) * h0 + c.r(rK + 6 + rr, k) * h1;
-                c.r(rPV + rr, k) = p[rr];
+                c.g(rPV + rr, k) = p[rr];
             }
         }
     }
@@ -1266,9 +1315,9 @@ __device__ __forceinline__ StepInfo phase_step(const Ctx<BM>& c, int dzr, bool p
         for (int q = 0; q < 6; ++q) {
             if (c.pair && q >= 3) break;
             const int i = c.pair ? 2 * q + p : q;
-            double s = c.r(rPV + i, k);
+            double s = c.g(rPV + i, k);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) s += c.r(rPS + (c.pair ? (p ? sym_idx(2 * q + 1, j) : sym_idx(2 * q, j)) : sym_idx(q, j)), k) * dx[j];
+            for (int j = 0; j < 6; ++j) s += c.g(rPS + (c.pair ? (p ? sym_idx(2 * q + 1, j) : sym_idx(2 * q, j)) : sym_idx(q, j)), k) * dx[j];
             if constexpr (Ctx<BM>::kLF) yp[q] = -s;
             else c.r(rYP + i, k) = -s;
         }
@@ -1768,6 +1817,9 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
     c.lane = threadIdx.x;
     c.gxr = a.xref + (size_t)b * S * 6;
     c.gur = a.uref + (size_t)b * N * 2;
+    if constexpr (Ctx<BM>::kPG)  // wave-uniform base: the descriptor lives in SGPRs; out-of-range offsets are dropped
+        c.prs = __builtin_amdgcn_make_buffer_rsrc(a.prow + (size_t)b * S * kGlobalRows, (short)0,
+                                                  S * kGlobalRows * (int)sizeof(double), 0x00020000);
     c.regref = NS > 0 && NS < W;
     c.pair = Ctx<BM>::kPairSym && Ctx<BM>::kDiag && NS > 0 && NS < W / 2;
     c.rc0 = c.rc1 = c.rc2 = c.rc3 = c.rc4 = c.rc5 = c.rc6 = c.rc7 = 0.0;
@@ -1968,7 +2020,7 @@ int bound_mask(const TrackArgs& a) {
 
 template <int BM, int OCC = 1, int NS = 0>
 hipError_t launch(const TrackArgs& a, hipStream_t stream) {
-    const int bytes = lds_bytes(a.N);
+    const int bytes = 8 * (Ctx<BM>::kSR * (a.N + 1) + kScratch);
     // the >64 KB opt-in is per device and cheap: set it on every launch that needs it (no process-global
     // cache that would miss a second device or race between threads)
     if (bytes > 64 * 1024) {
@@ -1987,6 +2039,7 @@ constexpr int kMaskMPC = 0xFCFC;
 constexpr int kMaskOBCA = 0xF8F8;
 constexpr int kDiagBit = 1 << 16;  // Q, R diagonal: the cost and its gradient skip the off-diagonal terms
 constexpr int kOccBit = 1 << 17;   // the two-waves-per-SIMD build (Ctx::kLF)
+constexpr int kPGBit = 1 << 18;    // the P / p band of the stage record in HBM (Ctx::kPG)
 
 // Q and R diagonal after symmetrisation (the kernel's weights are 0.5 (Q + Q'), 0.5 (R + R'))
 bool diagonal_weights(const TrackArgs& a) {
@@ -1994,6 +2047,28 @@ bool diagonal_weights(const TrackArgs& a) {
         for (int j = i + 1; j < 6; ++j)
             if (0.5 * (a.Q[i * 6 + j] + a.Q[j * 6 + i]) != 0.0) return false;
     return 0.5 * (a.R[1] + a.R[2]) == 0.0;
+}
+
+// Above three instances per CU (768 on MI355X's 256 CUs) the LDS build of N = 50 needs a second round of instances;
+// the HBM-band build fits four per CU.  Below, the LDS build is faster per instance (B = 1 host call 0.140 vs 0.161 ms).
+// The two builds are bitwise one another (profiles/r06/n50_hbm_band/), so results do not depend on B.
+int current_cu_count() {
+    static std::atomic<int> cache[64];  // per device, 0 = not queried yet (a race only queries twice)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    if (dev < 64)
+        if (const int c = cache[dev].load(std::memory_order_relaxed)) return c;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (dev < 64) cache[dev].store(cus, std::memory_order_relaxed);
+    return cus;
+}
+bool uses_global_rows(const TrackArgs& a) {
+    return bound_mask(a) == kMaskMPC && diagonal_weights(a) && a.N == 50 && a.B > 3 * current_cu_count();
+}
+
+size_t track_global_bytes(const TrackArgs& a) {
+    return uses_global_rows(a) ? (size_t)a.B * (a.N + 1) * kGlobalRows * sizeof(double) : 0;
 }
 
 hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
@@ -2019,8 +2094,12 @@ hipError_t launch_track(const TrackArgs& a, hipStream_t stream) {
     // differently from the one-wave build's and results would depend on B, test_occupancy_build_boundary_n31_n32)
     if (m == kMaskMPC && d && a.B > 4096 && occ_room) return launch<kMaskMPC | kDiagBit, 2>(a, stream);
     if (m == kMaskMPC && d && a.N == 40) return launch<kMaskMPC | kDiagBit, 1, 40>(a, stream);
-    // N = 50: the reference's closed-loop horizon (simulation.py), stage-unrolled like C3 (the only build at N = 50 for
-    // every B, so results do not depend on B)
+    // N = 50: the reference's closed-loop horizon (simulation.py), stage-unrolled like C3; large batches keep the
+    // Riccati factor band in HBM so that four instances share a CU (uses_global_rows)
+    if (uses_global_rows(a)) {
+        if (!a.prow) return hipErrorInvalidValue;  // the caller sizes it with track_global_bytes
+        return launch<kMaskMPC | kDiagBit | kPGBit, 1, 50>(a, stream);
+    }
     if (m == kMaskMPC && d && a.N == 50) return launch<kMaskMPC | kDiagBit, 1, 50>(a, stream);
     if (m == kMaskMPC) return d ? launch<kMaskMPC | kDiagBit>(a, stream) : launch<kMaskMPC>(a, stream);
     if (m == kMaskOBCA) return d ? launch<kMaskOBCA | kDiagBit>(a, stream) : launch<kMaskOBCA>(a, stream);

@@ -382,3 +382,22 @@ def test_occupancy_build_boundary_n31_n32():
             small = s.solve(x0[lo:hi], xr[lo:hi], ur[lo:hi])
             for a, b in zip(big, small):
                 assert np.array_equal(a[lo:hi], b), N
+
+
+def test_n50_hbm_band_build_is_bitwise_the_lds_build():
+    """N = 50 (simulation.py's horizon): above three instances per CU the launch takes the build that keeps the Riccati
+    factor band of the stage record in HBM (four instances per CU), below it the all-LDS build.  Same arithmetic: the
+    instances of a 1,024 batch equal the same instances solved 256 at a time, and the HBM workspace survives a batch
+    that grows from one call to the next."""
+    from ttmpc.scenarios import synthetic_batch
+    N = 50
+    s = _gpu_solver(N)
+    x0, xr, ur = synthetic_batch(1024, N, seed=91, psi_range=0.5)
+    small = [s.solve(x0[lo:lo + 256], xr[lo:lo + 256], ur[lo:lo + 256]) for lo in range(0, 1024, 256)]
+    big = s.solve(x0[:800], xr[:800], ur[:800])       # first HBM-band launch: the workspace is allocated
+    bigger = s.solve(x0, xr, ur)                      # a larger batch: the workspace grows
+    for lo, sm in zip(range(0, 1024, 256), small):
+        for a, b in zip(bigger, sm):
+            assert np.array_equal(a[lo:lo + 256], b), lo
+    for a, b in zip(big, bigger):
+        assert np.array_equal(a, b[:800])
