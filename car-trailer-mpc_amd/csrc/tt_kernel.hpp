@@ -50,7 +50,7 @@ inline int lds_bytes(int N) { return 8 * lds_doubles(N); }
 inline int max_horizon() { return (kMaxLdsBytes / 8 - kScratch) / kRowsPerStage - 1; }
 
 // The N = 50 build keeps the 28 stage rows of the Riccati factor (P, p) and of its overlay (Sigma, dB: linearise ..
-// ric_prep) in HBM instead of LDS: a 40.4 KB record, four instances per CU instead of three (tt_track.hip, round 6).
+// ric_prep) in HBM instead of LDS: a 38.8 KB record, four instances per CU instead of three (tt_track.hip, round 6).
 constexpr int kGlobalRows = 28;
 // bytes of TrackArgs::prow the launch of `a` needs (0: every stage row stays in LDS)
 size_t track_global_bytes(const TrackArgs& a);

@@ -275,7 +275,7 @@ struct Ctx {
     double mu, tau;
     // bit 18: the build keeps the stage rows rPS .. rDXS-1 (P, spare, p; their overlay Sigma, dB) in HBM (TrackArgs::prow)
     // and the LDS record shrinks by those kGlobalRows rows: rows from rDXS on sit kGlobalRows lower (the N = 50 build:
-    // 40.4 KB per instance, four per CU instead of three).  Rows of that band are reached through g() only; r() serves
+    // 38.8 KB per instance, four per CU instead of three).  Rows of that band are reached through g() only; r() serves
     // every other row, rl() an LDS row already mapped (lrow) -- in the other builds all three are the same LDS access.
     static constexpr bool kPG = BM >= 0 && ((BM >> 18) & 1);
     static constexpr int kSR = kPG ? SR - kGlobalRows : SR;
