@@ -365,6 +365,17 @@ def test_occupancy_build_is_bitwise_the_latency_build(N):
             small = s.solve(x0[lo:lo + 1152], xr[lo:lo + 1152], ur[lo:lo + 1152])
             for a, b in zip(big, small):
                 assert np.array_equal(a[lo:lo + 1152], b), seed
+    # the NMPC driver's warm-started relaxed-tolerance solves (its own load path: a guess instead of the reference copy)
+    import ttmpc
+    from ttmpc import layout
+    sn = _gpu_solver(N, variant=ttmpc.TT_VARIANT_NMPC, tol=1e-3, acc_tol=1e-2, max_iter=2000, acc_iter=5)
+    x0, xr, ur = synthetic_batch(B, N, seed=79, psi_range=0.6)
+    zg = layout.shift(layout.pack(xr, ur), N)
+    big = sn.solve(x0, xr, ur, z_guess=zg)
+    for lo in range(0, B, 1152):
+        small = sn.solve(x0[lo:lo + 1152], xr[lo:lo + 1152], ur[lo:lo + 1152], z_guess=zg[lo:lo + 1152])
+        for a, b in zip(big, small):
+            assert np.array_equal(a[lo:lo + 1152], b), "nmpc"
 
 
 def test_occupancy_build_boundary_n31_n32():
