@@ -11,6 +11,9 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
+#include <chrono>
+#include <atomic>
 
 #include "tt_kernel.hpp"
 #include "ttmpc.h"
@@ -152,6 +155,29 @@ int ensure_prow(Handle* h, size_t bytes) {
     }
     h->prow_cap = bytes;
     return 0;
+}
+
+// a status value no kernel writes: the zero-copy path's "not finished yet"
+constexpr int kStatusPending = -0x40000000;
+
+// Wait until every instance of a zero-copy call has written its status (host memory; the kernel's release orders the
+// instance's other outputs before it).  Spins up to 2 ms, then yields to the OS between looks; gives up after 1 s, and
+// the caller then waits for the stream (which also reports a fault that kept a status from ever being written).
+bool poll_done(volatile int* st, int B) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (long long n = 0;; ++n) {
+        int i = 0;
+        while (i < B && st[i] != kStatusPending) ++i;
+        if (i == B) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return true;
+        }
+        if ((n & 255) == 255) {
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::seconds(1)) return false;
+            if (dt > std::chrono::milliseconds(2)) std::this_thread::yield();
+        }
+    }
 }
 
 bool is_obca(const tt_config& c) { return c.variant == TT_VARIANT_TRACK_OBCA || c.variant == TT_VARIANT_OBCA_PLAN; }
@@ -310,10 +336,24 @@ int tt_create(const tt_config* cfg, const double* Q, const double* R, const doub
     return 0;
 }
 
+namespace {
+int solve_device_impl(Handle* h, int B, const double* d_x0, const double* d_xref, const double* d_uref,
+                      const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out, int* d_status,
+                      int* d_iters, double* d_kkt_res, void* stream, int host_done);
+}  // namespace
+
 int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double* d_xref, const double* d_uref,
                           const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out,
                           int* d_status, int* d_iters, double* d_kkt_res, void* stream) {
-    Handle* h = static_cast<Handle*>(handle);
+    return solve_device_impl(static_cast<Handle*>(handle), B, d_x0, d_xref, d_uref, d_wq_wr, d_z_guess, d_x_out,
+                             d_u_out, d_status, d_iters, d_kkt_res, stream, 0);
+}
+
+namespace {
+int solve_device_impl(Handle* h, int B, const double* d_x0, const double* d_xref, const double* d_uref,
+                      const double* d_wq_wr, const double* d_z_guess, double* d_x_out, double* d_u_out, int* d_status,
+                      int* d_iters, double* d_kkt_res, void* stream, int host_done) {
+    void* handle = h;
     if (!h) return fail(nullptr, -EINVAL, "NULL handle%s");
     if (B < 0) return fail(h, -EINVAL, "B must be >= 0%s");
     if (B == 0) return 0;
@@ -341,6 +381,7 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
     a.kkt = d_kkt_res;
     a.status = d_status;
     a.iters = d_iters;
+    a.host_done = host_done;
     if (const size_t gb = ttmpc::track_global_bytes(a)) {
         const int rc = ensure_prow(h, gb);
         if (rc) return rc;
@@ -351,6 +392,7 @@ int tt_solve_batch_device(void* handle, int B, const double* d_x0, const double*
     if (e != hipSuccess) return hip_fail(h, e, "track kernel launch");
     return 0;
 }
+}  // namespace
 
 int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, const double* uref,
                    const double* wq_wr, const double* z_guess, double* x_out, double* u_out, int* status,
@@ -402,14 +444,21 @@ int tt_solve_batch(void* handle, int B, const double* x0, const double* xref, co
     double* dkk = duo + nuo;
     int* dst = reinterpret_cast<int*>(dkk + b);
     int* dit = dst + b;
-    rc = tt_solve_batch_device(h, B, dptr[0], dptr[1], dptr[2], wq_wr ? dptr[3] : nullptr,
-                               z_guess ? dptr[4] : nullptr, dxo, duo, dst, dit, dkk, s);
+    // zero-copy: status[] in the host block doubles as the instances' completion flags (the kernel writes each last,
+    // behind a system-scope release); a pending sentinel, then a poll of host memory instead of the stream wait
+    volatile int* hst = zc ? reinterpret_cast<volatile int*>(h->h_sout + (nxo + nuo + b) * 8) : nullptr;
+    if (zc)
+        for (int i = 0; i < B; ++i) hst[i] = kStatusPending;
+    rc = solve_device_impl(h, B, dptr[0], dptr[1], dptr[2], wq_wr ? dptr[3] : nullptr, z_guess ? dptr[4] : nullptr, dxo,
+                           duo, dst, dit, dkk, s, zc ? 1 : 0);
     if (rc) {
         (void)hipStreamSynchronize(s);  // the H2D from the pinned staging buffer may still be in flight
         return rc;
     }
+    bool done = false;
+    if (zc) done = poll_done(hst, B);
     e = zc ? hipSuccess : hipMemcpyAsync(h->h_sout, h->d_sout, out_d * 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && !done) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(h, e, "solve");
     const double* ho = reinterpret_cast<const double*>(h->h_sout);
     memcpy(x_out, ho, nxo * 8);

@@ -27,6 +27,8 @@ struct TrackArgs {
     int* iters;                           // [B] or nullptr
     unsigned long long* stamps;           // [B][kNumPhases] cycle sums (TT_STAMPS diagnostic build only)
     double* prow;                         // [B][N+1][kGlobalRows]: the stage rows a build keeps in HBM, or nullptr
+    int host_done;                        // 1: status[b] is the instance's completion flag for a polling host (zero-copy
+                                          //    host calls): written last, after a system-scope release of the rest
 };
 
 // phases timed by the TT_STAMPS diagnostic build

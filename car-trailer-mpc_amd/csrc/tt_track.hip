@@ -2000,10 +2000,16 @@ __global__ __launch_bounds__(W) __attribute__((amdgpu_waves_per_eu(OCC))) void t
         stamps.store(a.stamps ? a.stamps + (size_t)b * kNumPhases : nullptr, lane);
 #endif
         if (lane == 0) {
-            a.status[b] = status;
             if (a.iters) a.iters[b] = iter;
             if (a.kkt) a.kkt[b] = E0;
         }
+        if (a.host_done) {
+            // a zero-copy host call polls status[b] in host memory instead of waiting for the stream: every other output
+            // of the instance is made visible system-wide before it (vector stores, then the release)
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
+        if (lane == 0) a.status[b] = status;
     }
 }
 
