@@ -74,16 +74,24 @@ class ShardedBatch:
         self.in_chunk = pc * (6 + (N + 1) * 6 + N * 2)
         self.out_chunk = pc * ((N + 1) * 6 + N * 2 + 1)
         f64 = dict(dtype=torch.float64, device=self.device)
-        self.recv_in = torch.empty((C, self.in_chunk), **f64)
-        self.out_f = torch.empty((C, self.out_chunk), **f64)
-        self.out_i = torch.empty((C, 2 * pc), dtype=torch.int32, device=self.device)
-        self.parts = [_Chunk(self.recv_in[c], self.out_f[c], self.out_i[c], pc, N) for c in range(C)]
-        self.valid_mask = torch.zeros(self.per, dtype=torch.bool, device=self.device)
-        self.valid_mask[: self.valid] = True
         if self.rank == 0:
             self.gather_f = torch.empty((self.world, C, self.out_chunk), **f64)
             self.gather_i = torch.empty((self.world, C, 2 * pc), dtype=torch.int32, device=self.device)
+        self.recv_in = torch.empty((C, self.in_chunk), **f64)
+        if self.world == 1:
+            # one rank: scatter and gather are the identity, so the shard solves straight out of the packed source
+            # (pack_inputs) into the gather block -- no device copies in step()
+            self.out_f, self.out_i = self.gather_f[0], self.gather_i[0]
+        else:
+            self.out_f = torch.empty((C, self.out_chunk), **f64)
+            self.out_i = torch.empty((C, 2 * pc), dtype=torch.int32, device=self.device)
+        self._bind_parts()
+        self.valid_mask = torch.zeros(self.per, dtype=torch.bool, device=self.device)
+        self.valid_mask[: self.valid] = True
         self.send_in = None
+
+    def _bind_parts(self):
+        self.parts = [_Chunk(self.recv_in[c], self.out_f[c], self.out_i[c], self.pc, self.N) for c in range(self.chunks)]
 
     # ---- rank 0: lay the global batch out as chunk records per rank (done once, outside the step) ----
     def pack_inputs(self, x0, xref, uref):
@@ -103,6 +111,9 @@ class ShardedBatch:
         WC = W * C
         send = torch.cat([x0.reshape(WC, -1), xref.reshape(WC, -1), uref.reshape(WC, -1)], dim=1)
         self.send_in = send.reshape(W, C, self.in_chunk).to(self.device).contiguous()
+        if W == 1:
+            self.recv_in = self.send_in[0]
+            self._bind_parts()
         return self.send_in
 
     def solve_local(self):
@@ -116,11 +127,10 @@ class ShardedBatch:
         d = self.dist
         C = self.chunks
         if d is None or self.world == 1:
-            for c, p in enumerate(self.parts):
-                self.recv_in[c].copy_(self.send_in[0, c])
+            if self.send_in is None:
+                raise RuntimeError("ShardedBatch.step: pack_inputs() first (rank 0 holds the global batch)")
+            for p in self.parts:  # views of the packed source and of the gather block (see __init__)
                 self.solve_shard(p.x0, p.xr, p.ur, p.X, p.U, p.st, p.it, p.kkt)
-                self.gather_f[0, c].copy_(self.out_f[c])
-                self.gather_i[0, c].copy_(self.out_i[c])
         else:
             g = self.group
             root = self.rank == 0
