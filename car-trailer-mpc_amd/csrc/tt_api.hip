@@ -110,6 +110,8 @@ void free_stage(Handle* h) {
 
 int ensure_stage(Handle* h, size_t in_bytes, size_t out_bytes) {
     if (in_bytes <= h->stage_in && out_bytes <= h->stage_out) return 0;
+    // a zero-copy call returns once its statuses are written, before its kernel has retired: let it retire first
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_stage(h);
     hipError_t e = hipMalloc((void**)&h->d_sin, in_bytes);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_sout, out_bytes);
