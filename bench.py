@@ -815,8 +815,8 @@ def obca_cpu_baseline(cfg, N, M, params, bnd, obs, x0, xg, xr, ur, zg, max_iter,
 
 # rocprofv3 PMC passes (tools/hbm_passes.sh) that the default C2 / C3 lines quote as roofline.traffic: the kernel
 # the bench runs; re-profile after a tracking-kernel change
-TRACK_PMC = {"c2": "profiles/r06/final/pmc_track_c2", "c3": "profiles/r06/final/pmc_track_c3"}
-TRACK_PMC_SOURCE = "profiles/r06/final/SOURCE.txt"
+TRACK_PMC = {"c2": "profiles/r06/final_head/pmc_track_c2", "c3": "profiles/r06/final_head/pmc_track_c3"}
+TRACK_PMC_SOURCE = "profiles/r06/final_head/SOURCE.txt"
 
 
 # committed PMC passes of obca_kernel (FETCH_SIZE and WRITE_SIZE in separate rocprofv3 runs, tools/gpu_session.sh hbm:CFG).
